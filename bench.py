@@ -1,0 +1,186 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Qwen2-7B bf16, batch 1, prompt 2048, gen 512 on MI355X.
+
+BASELINE.json metric: "decode tokens/s + prefill tok/s, Qwen2-7B bf16 batch=1, 1/2/4/8
+MI355X".  A step = one decode step (one token per sequence) of the hipGraph-captured
+forward; `value` = decode tokens/s summed over all ranks.  Prefill tok/s is reported
+beside it.  Weights are random-init at the real Qwen2-7B shapes (synthetic; no
+checkpoints exist offline), prompts are random token ids.
+
+N>1 (torch.distributed.run, one process per GPU): each rank runs an independent replica
+of the batch-1 workload (weak scaling, no data-path collective) — see DESIGN.md §multi-GPU.
+
+JSON extras: "roofline" for the dominant kernel (gate/up GEMV, timed live with hipEvents
+on the engine stream), "step_roofline" for the whole decode step, "cpu_baseline" (the
+naive C++ oracle forward over the same synthetic weights on host cores, rank 0 / N=1).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import qwen_inference_engine_amd as Q  # noqa: E402
+from qwen_inference_engine_amd import spec as S, weights as W  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=511)
+    ap.add_argument("--warmup", type=int, default=16)
+    ap.add_argument("--model", default="Qwen2-7B", choices=sorted(S.PRESETS))
+    ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--prompt", type=int, default=2048)
+    ap.add_argument("--gen", type=int, default=512)
+    ap.add_argument("--prefill-iters", type=int, default=3)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-prompt", type=int, default=16)
+    ap.add_argument("--cpu-decode", type=int, default=8)
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+
+    spec = S.PRESETS[a.model]
+    B, P = a.batch, a.prompt
+    max_ctx = P + max(a.gen, a.steps, a.warmup) + 16
+    eng = Q.Engine(spec, device=local, max_ctx=max_ctx, use_graph=not a.no_graph)
+    eng.init_synthetic(W.SynthParams(seed=0))
+    batch = eng.batch(B, max_ctx)
+    prompts = np.random.default_rng(1 + rank).integers(0, spec.vocab, size=(B, P), dtype=np.int32)
+
+    # ---------------- prefill (first call warms up; best of the timed ones)
+    first = [batch.prefill(s, prompts[s]) for s in range(B)]
+    pts = []
+    for _ in range(max(1, a.prefill_iters)):
+        eng.sync()
+        t0 = time.perf_counter()
+        first = [batch.prefill(s, prompts[s]) for s in range(B)]
+        eng.sync()
+        pts.append(time.perf_counter() - t0)
+    t_prefill = float(np.median(pts))
+
+    # ---------------- decode: warmup, rewind to the prompt end, then K timed steps
+    batch.decode(a.warmup, want_ids=False)
+    for s in range(B):
+        batch.set_position(s, P, first[s])
+    eng.sync()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    batch.decode(a.steps, want_ids=False)
+    eng.sync()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        import torch
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        tp = torch.tensor([t_prefill], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tp, op=dist.ReduceOp.MAX)
+        t_prefill = float(tp.item())
+
+    ms_step = dt * 1e3 / max(a.steps, 1)
+    value = world * B * a.steps / dt
+    prefill_tok_s = world * B * P / t_prefill
+
+    # ---------------- dominant kernel, timed live with hipEvents on the engine stream
+    kern = {}
+    for which, name in [(0, "gate_up_gemv"), (1, "down_gemv"), (2, "qkv_gemv"), (3, "o_gemv"),
+                        (4, "lm_head_gemv"), (5, "attention")]:
+        us, by = batch.time_kernel(which, 50)
+        kern[name] = {"avg_us": round(us, 3), "bytes": by, "GBps": round(by / us / 1e3, 1)}
+    dom = kern["gate_up_gemv"]
+    avg_ctx = P + (a.steps + 1) / 2.0
+    step_bytes = spec.decode_weight_bytes() + B * spec.kv_bytes_per_position() * avg_ctx
+    step_gbs = step_bytes / (ms_step * 1e-3) / 1e9
+
+    out = {
+        "metric": "decode tokens/s + prefill tok/s, Qwen2-7B bf16 batch=1, 1/2/4/8 MI355X",
+        "value": round(value, 3),
+        "unit": "tokens/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic: random-init weights at real shapes, random prompt ids",
+        "config": {"workload": f"{spec.name} bf16 decode, batch={B}, prompt={P}, gen={a.gen}",
+                   "batch_per_gpu": B, "prompt": P, "gen": a.gen,
+                   "parallelism": "replicas" if world > 1 else "single", "graph": not a.no_graph},
+        "prefill_tok_s": round(prefill_tok_s, 1),
+        "prefill_ms": round(t_prefill * 1e3, 3),
+        "roofline": {"bound": "hbm", "kernel": "gate_up_gemv (rms + gate/up GEMV + SwiGLU, layer 0)",
+                     "achieved": dom["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(dom["GBps"] / HBM_PEAK_GBS, 4), "traffic": None},
+        "step_roofline": {"bytes_per_step": step_bytes, "achieved_GBps": round(step_gbs, 1),
+                          "frac": round(step_gbs / HBM_PEAK_GBS, 4),
+                          "roofline_tok_s": round(HBM_PEAK_GBS * 1e9 / step_bytes * B * world, 1)},
+        "kernels": kern,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(spec, a, batch, eng)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(spec, a, batch, eng):
+    """Naive C++ CPU forward (oracle/qie_oracle.cpp, OpenMP) over the same synthetic
+    weights: a bounded sample = cpu_prompt-token prefill + cpu_decode greedy decode steps.
+    Also checks the GPU's greedy ids on the same sample (size-independent parity)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "16"))
+    t0 = time.perf_counter()
+    hw = W.HostWeights.synthetic(spec, W.SynthParams(seed=0))
+    t_gen = time.perf_counter() - t0
+    m = O.Model(hw, a.cpu_prompt + a.cpu_decode + 4, nthreads=threads)
+    prompt = list(np.random.default_rng(5).integers(0, spec.vocab, a.cpu_prompt))
+    t0 = time.perf_counter()
+    lg = m.forward(prompt, 0)
+    t_pf = time.perf_counter() - t0
+    ids = [O.argmax(lg)]
+    t0 = time.perf_counter()
+    for _ in range(a.cpu_decode):
+        lg = m.forward([ids[-1]])
+        ids.append(O.argmax(lg))
+    t_dec = time.perf_counter() - t0
+    g = [batch.prefill(0, prompt)] + [int(x) for x in batch.decode(a.cpu_decode)[:, 0]]
+    return {"value": round(a.cpu_decode / t_dec, 4), "unit": "tokens/s", "cores": threads, "kind": "port",
+            "sample": f"{spec.name}: {a.cpu_prompt}-token prefill ({t_pf:.2f} s, "
+                      f"{a.cpu_prompt / t_pf:.2f} tok/s) + {a.cpu_decode} greedy decode steps "
+                      f"({t_dec:.2f} s); weights generated in {t_gen:.1f} s",
+            "prefill_tok_s": round(a.cpu_prompt / t_pf, 3),
+            "gpu_ids_match_cpu": g == ids}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,114 @@
+/*
+ * qie_engine.h — engine-level C ABI of libqie.so: weights, KV cache,
+ * prefill and hipGraph-captured decode.
+ *
+ * Replaces the reference's driver / step API:
+ *   llm()                               layers/src/qwen_main.cu:64-417, iengine.cuh:51
+ *       -> qie_prefill() (state == prefill) / qie_decode_step() (state == decode)
+ *   create_new_sequence()               layers/src/iengine.cu:25-47
+ *   initialize_model_buffers()          layers/src/utills.cu:4-129
+ *   destroy_model_buffers()             layers/src/utills.cu:142-205
+ *       -> qie_batch_create() / qie_batch_destroy()
+ *   create_page_list / allocate_page_buffers / free_page_list
+ *                                       layers/src/iengine.cu:73-109
+ *       -> the KV cache owned by qie_batch (contiguous per (layer, kv head))
+ *   load_all_weights_to_gpu_chunked()   layers/src/iengine.cu:117-223
+ *       -> qie_engine_load_weights_bin()
+ *   parsed_tensors / build_indexed_tensors (tensor_parser.cpp:31-165)
+ *       -> qie_index_* (reference-compatible weights.bin index)
+ *
+ * All functions return 0 on success; qie_last_error() (qie_ops.h) has the text.
+ */
+#ifndef QIE_ENGINE_H
+#define QIE_ENGINE_H
+
+#include "qie_types.h"
+#include "qie_ops.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct qie_engine qie_engine;
+typedef struct qie_batch qie_batch;
+typedef struct qie_index qie_index;
+
+/* ------------------------------------------------------------------ index
+ * Reference-compatible tensor index (tensor_parser.hh:204-210):
+ * {tensor_name, shape, data_offsets (bytes, re-based into one contiguous
+ * weights.bin), layer_index (-1 for globals), short_name}; lm_head.weight
+ * has short_name "logits". */
+int qie_index_load_meta(const char* meta_data_txt, qie_index** out);   /* meta_data.txt format */
+int qie_index_synthetic(const qie_model_spec* spec, qie_index** out);  /* HF names, sorted, one shard */
+int qie_index_count(const qie_index* idx);
+int qie_index_get(const qie_index* idx, int i, const char** name, const char** short_name,
+                  int32_t* layer, int64_t* off0, int64_t* off1, int32_t* ndim, int64_t* shape4);
+int64_t qie_index_total_bytes(const qie_index* idx);
+int qie_index_write_meta(const qie_index* idx, const char* path);
+void qie_index_destroy(qie_index* idx);
+
+/* ----------------------------------------------------------------- engine */
+typedef struct qie_engine_opts {
+    int32_t device;          /* HIP device ordinal                                   */
+    int32_t max_ctx;         /* RoPE table rows (reference CONTEXT_SIZE = 32786)     */
+    int32_t use_graph;       /* 1: decode steps replay a captured hipGraph           */
+    int32_t tp_rank, tp_size;/* tensor parallel (1 = off)                            */
+    void* tp_comm;           /* ncclComm_t for tp_size > 1 (RCCL over xGMI)          */
+    int32_t reserved[8];
+} qie_engine_opts;
+
+int qie_engine_create(const qie_model_spec* spec, const qie_engine_opts* opts, qie_engine** out);
+/* Synthetic checkpoint at real shapes (no weights ship here): reference-layout
+ * arena (qie_index_synthetic), every tensor filled by qie_synthetic_fill with
+ * tensor_id = qie_tensor_id(name): linear weights offset 0 / scale w_scale,
+ * norm weights 1 + norm_scale*u, biases bias_scale*u. */
+int qie_engine_init_synthetic(qie_engine* e, uint64_t seed, float w_scale, float norm_scale,
+                              float bias_scale);
+/* Reference flat weights.bin + meta_data.txt index, read in chunks through a
+ * pinned staging buffer (load_all_weights_to_gpu_chunked semantics). */
+int qie_engine_load_weights_bin(qie_engine* e, const char* weights_bin, const char* meta_data_txt,
+                                int64_t chunk_bytes);
+/* Caller-owned device weights (e.g. torch tensors); not freed by qie. */
+int qie_engine_set_weights(qie_engine* e, const qie_model_weights* w);
+int qie_engine_weights(const qie_engine* e, qie_model_weights* out, const qie_layer_weights** layers);
+int qie_engine_spec(const qie_engine* e, qie_model_spec* out);
+void* qie_engine_stream(qie_engine* e);
+int qie_engine_sync(qie_engine* e);
+void qie_engine_destroy(qie_engine* e);
+
+/* ------------------------------------------------------------------ batch
+ * B independent sequences decoded together (weights streamed once per step).
+ * KV cache [B][L][nkv][max_ctx][hd] bf16; token history [B][max_ctx]. */
+int qie_batch_create(qie_engine* e, int32_t batch, int32_t max_ctx, qie_batch** out);
+void qie_batch_destroy(qie_batch* b);
+
+/* Prefill sequence `seq` with n prompt ids (host array); writes its KV rows
+ * 0..n-1, samples the first generated token (host *next_id, may be NULL) and
+ * makes it the sequence's current token at position n. */
+int qie_prefill(qie_batch* b, int32_t seq, const int32_t* ids, int32_t n, const qie_sampling* s,
+                int32_t* next_id);
+/* One decode step for all B sequences (hipGraph replay when enabled);
+ * next_ids: host [B] or NULL (then nothing is synchronised). */
+int qie_decode_step(qie_batch* b, const qie_sampling* s, int32_t* next_ids);
+/* n_steps decode steps back to back; out_ids host [n_steps][B] (may be NULL). */
+int qie_decode(qie_batch* b, int32_t n_steps, const qie_sampling* s, int32_t* out_ids);
+/* Last logits of every sequence: host bf16 [B][V]. */
+int qie_batch_logits(qie_batch* b, void* host_out);
+/* Current positions (host int32 [B]) and token history row of `seq`. */
+int qie_batch_positions(qie_batch* b, int32_t* host_pos);
+int qie_batch_history(qie_batch* b, int32_t seq, int32_t* host_ids, int32_t n);
+/* Rewind/set sequence `seq` to position pos with current token `token`
+ * (KV rows >= pos are simply overwritten later). */
+int qie_batch_set_position(qie_batch* b, int32_t seq, int32_t pos, int32_t token);
+/* Time `iters` launches of one of the decode step's kernels with hipEvents on
+ * the engine stream (which: 0 = gate/up GEMV of layer 0, 1 = down GEMV,
+ * 2 = QKV GEMV, 3 = O GEMV, 4 = lm_head GEMV, 5 = attention).  Returns the
+ * average microseconds per launch and the algorithmic bytes per launch. */
+int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* avg_us,
+                          double* bytes);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* QIE_ENGINE_H */

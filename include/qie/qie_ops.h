@@ -1,0 +1,160 @@
+/*
+ * qie_ops.h — operator-level C ABI of libqie.so (MI355X / gfx950 HIP kernels).
+ *
+ * This replaces the reference's operator API, layers/include/helpers.cuh:45-166
+ * (launch_rms, launch_rope, launch_rope_single, launch_qknorm, launch_matmul,
+ * proj, launch_attn, launch_act, launch_elem, launch_resadd, sample_topk_bf16,
+ * copy_last_vocab_vec, copy_first_token) and the __global__ prototypes of
+ * layers/include/layers_include.cuh:15-35.
+ *
+ * Conventions (differences from the reference are deliberate):
+ *   - every pointer is a caller-owned DEVICE pointer unless stated; tensors are
+ *     bf16 (uint16_t words), row-major, linear weights in PyTorch [out, in];
+ *   - every op takes an explicit hipStream_t (passed as void*; NULL = the
+ *     legacy default stream the reference uses) and never synchronises, never
+ *     allocates — so every op can be captured into a hipGraph;
+ *   - every op returns 0 on success, a positive hipError_t, or a negative QIE
+ *     error (-22 = invalid argument); qie_last_error() returns the text.
+ *     (The reference returns void and prints to stderr.)
+ */
+#ifndef QIE_OPS_H
+#define QIE_OPS_H
+
+#include "qie_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QIE_ABI_VERSION 1
+
+const char* qie_last_error(void);
+int qie_abi_version(void);
+int qie_device_count(int* count);
+
+/* ---------------------------------------------------------------- tables
+ * Replaces precompute_cos_sin (layers/src/include.cpp:5-16, called at
+ * utills.cu:36-44).  Fills HOST fp32 tables [n_pos][head_dim/2]: the
+ * reference's exact table in REF mode, HF's bf16-rounded table in HF mode. */
+int qie_rope_table_host(float* cos_out, float* sin_out, int32_t n_pos, int32_t head_dim,
+                        float theta, int32_t numerics);
+
+/* ------------------------------------------------------------- embedding
+ * Replaces embedding_matrix_func (layers/src/embedded_matrix.cu:5-17, launched
+ * utills.cu:51-54 and qwen_main.cu:267).  out[t,:] = E[ids[t],:]. */
+int qie_embedding(const void* E, const int32_t* ids, void* out, int64_t n, int64_t H,
+                  void* stream);
+
+/* ---------------------------------------------------------------- RMSNorm
+ * Replaces launch_rms / rmsNorm (helpers.cuh:45-49, normalization.cu:5-25).
+ * y = rmsnorm(x) * w over rows of H; x and y may not alias. */
+int qie_rmsnorm(const void* x, const void* w, void* y, int64_t rows, int64_t H, float eps,
+                int32_t numerics, void* stream);
+
+/* ----------------------------------------------------------------- linear
+ * Replaces launch_matmul / proj (helpers.cuh:81-106, 132-138; matrix_mul.cu:
+ * 165-288) with fused epilogues.  y[m, n] = sum_k x[m, k] * W[n, k], fp32
+ * accumulation, one bf16 rounding.  W is up to three [rows_i, K] segments
+ * concatenated along N (fused QKV without repacking the weights.bin arena).
+ * M <= 8 runs the bandwidth-bound GEMV kernel; larger M the MFMA GEMM.
+ */
+enum {
+    QIE_EPI_STORE = 0,     /* y = bf16(acc [+ bias])                                  */
+    QIE_EPI_RESIDUAL = 1,  /* y = bf16(y + bf16(acc))   (launch_resadd fused)          */
+    QIE_EPI_SWIGLU = 2     /* segs (gate, up): y[m, j] = bf16(bf16(up) * bf16(silu(bf16(gate))))
+                              (SiLU.cu:10-23 + element_add.cu:4-12 fused); N = I      */
+};
+
+typedef struct qie_linear_args {
+    const void* x;          /* [M, K] bf16, row stride ldx (elements)                   */
+    int64_t ldx;
+    const void* w[3];       /* weight segments, each [seg_rows[i], K]                   */
+    const void* bias[3];    /* optional per-segment bias [seg_rows[i]] (Qwen2 q/k/v)    */
+    int64_t seg_rows[3];
+    int64_t M, K, N;        /* N = output columns (sum of seg_rows; I for SWIGLU)       */
+    void* y;                /* [M, N] bf16, row stride ldy                              */
+    int64_t ldy;
+    int32_t epilogue;       /* QIE_EPI_*                                                */
+    int32_t numerics;       /* for the fused norm                                       */
+    const void* norm_w;     /* optional fused RMSNorm of x (weight [K]); GEMV path only */
+    float norm_eps;
+    int32_t flags;          /* reserved, 0                                              */
+    uint64_t* argmax_keys;  /* optional [M] selection keys, atomically max-merged
+                               (fused greedy arg-max, logit_decode.cu:15-33); caller
+                               zeroes them before the launch                            */
+} qie_linear_args;
+
+int qie_linear(const qie_linear_args* args, void* stream);
+
+/* --------------------------------------------- q/k post-projection + KV append
+ * Replaces launch_qknorm (helpers.cuh:140-142, qk_norm.cu:43-79), launch_rope /
+ * launch_rope_single (helpers.cuh:51-55, 143-147; RoPE.cu:6-22) and
+ * kv_copy_layer_to_cache_prefill/decode (include_cuda.cu:165-279) in one pass:
+ *   qkv rows [M, (nq + 2*nkv)*hd] (projection output, bias already added)
+ *   -> q_out [M, nq*hd] (qk-norm'd, rotated)
+ *   -> K cache row (qk-norm'd, rotated) and V cache row at position pos[m].
+ * KV cache layout (qie): per sequence [L][nkv][max_ctx][hd] bf16, sequence s
+ * at kc + s*seq_stride; row m belongs to sequence m / rows_per_seq.
+ * (The reference's pages are [4 tok][L][kvdim] linked through managed memory,
+ * iengine.cu:73-109; qie keeps each (layer, kv head) contiguous for coalesced
+ * streaming reads.) */
+typedef struct qie_kv_cache {
+    void* k;                 /* base of sequence 0's K cache                           */
+    void* v;
+    int64_t seq_stride;      /* elements between sequences                             */
+    int32_t n_layers, n_kv_heads, head_dim, max_ctx;
+} qie_kv_cache;
+
+int qie_qkv_post(const void* qkv, int64_t M, const int32_t* pos, int32_t rows_per_seq,
+                 const void* q_norm, const void* k_norm, const float* rope_cos,
+                 const float* rope_sin, int32_t n_heads, const qie_kv_cache* cache,
+                 int32_t layer, float eps, int32_t numerics, void* q_out, void* stream);
+
+/* -------------------------------------------------------------- attention
+ * Replaces launch_attn / selfattention (helpers.cuh:121-130,
+ * self_attension.cu:10-149): GQA attention of query rows over the cache.
+ * Row m attends to positions [0, pos[m]] of sequence m / rows_per_seq
+ * (prefill: causal; decode: the whole cache incl. the new token — identical
+ * to the reference's causal / mkv = seq_len windows).  Flash-decoding split
+ * over the sequence; ws must hold qie_attention_workspace_bytes(). */
+int64_t qie_attention_workspace_bytes(int64_t M, int32_t n_heads, int32_t head_dim,
+                                      int32_t max_ctx);
+int qie_attention(const void* q, int64_t M, const int32_t* pos, int32_t rows_per_seq,
+                  const qie_kv_cache* cache, int32_t layer, int32_t n_heads, void* out,
+                  void* ws, void* stream);
+
+/* ------------------------------------------------------------- elementwise
+ * launch_act + launch_elem (helpers.cuh:108-115) and launch_resadd (:116-119)
+ * for callers that do not use the fused linear epilogues. */
+int qie_silu_mul(const void* gate, const void* up, void* h, int64_t n, void* stream);
+int qie_residual_add(void* x, const void* y, int64_t n, void* stream);
+
+/* ---------------------------------------------------------------- sampling
+ * Replaces sample_topk_bf16 / topk_temperature_softmax_sampling_kernel_bf16
+ * (helpers.cuh:157-166, logit_decode.cu:149-274).  Writes the chosen id of each
+ * of the M logit rows to out_ids (device).  top_k <= 1 -> greedy arg-max.
+ * ws must hold qie_sample_workspace_bytes(). */
+int64_t qie_sample_workspace_bytes(int64_t M, int64_t V);
+int qie_sample(const void* logits, int64_t M, int64_t V, int64_t ld, const qie_sampling* s,
+               const int32_t* step_dev, int32_t* out_ids, void* ws, void* stream);
+/* Decode fused arg-max keys (see qie_linear_args.argmax_keys) into ids. */
+int qie_keys_to_ids(const uint64_t* keys, int64_t M, int32_t* out_ids, void* stream);
+
+/* ------------------------------------------------------- synthetic weights
+ * Deterministic counter-based fill used for synthetic checkpoints (no weights
+ * ship in this environment): element i of tensor `tensor_id` is
+ *   r = splitmix64(splitmix64(seed*0x9E3779B97F4A7C15 ^ (tensor_id << 32)) + i)
+ *   u = ((int32)(r >> 40) - 2^23) * 2^-23          (exact, in [-1, 1))
+ *   value = bf16(offset + u * scale)
+ * bit-identical on the host (qie_synthetic_fill_host, OpenMP) and the GPU. */
+uint32_t qie_tensor_id(const char* name);   /* FNV-1a 32 of the tensor name */
+int qie_synthetic_fill(void* dev, int64_t n, uint32_t tensor_id, uint64_t seed, float scale,
+                       float offset, void* stream);
+int qie_synthetic_fill_host(void* host, int64_t n, uint32_t tensor_id, uint64_t seed,
+                            float scale, float offset);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* QIE_OPS_H */

@@ -1,0 +1,799 @@
+// engine.hip — qie engine: weight arena, per-batch KV cache and activations,
+// prefill and hipGraph-captured decode.
+//
+// Reference driver being replaced: llm() (layers/src/qwen_main.cu:64-417),
+// create_new_sequence (iengine.cu:25-47), initialize_model_buffers
+// (utills.cu:4-129), load_all_weights_to_gpu_chunked (iengine.cu:117-223),
+// page list helpers (iengine.cu:73-109).  Op order per layer follows
+// qwen_main.cu:77-217 (prefill) / :271-359 (decode):
+//   rms -> q,k,v -> [qk-norm] -> RoPE -> KV write -> attention -> o -> +res ->
+//   rms -> up, gate -> silu*up -> down -> +res;  final rms -> lm_head -> sample.
+// MI355X design: the decode step is 5 launches per layer
+//   [rms+QKV(+bias) GEMV] [qk-norm+RoPE+KV append] [attention(+combine)]
+//   [O GEMV + residual] [rms+gate/up GEMV + SwiGLU] [down GEMV + residual]
+// plus [rms+lm_head GEMV + fused arg-max] [finalize: id, position, next
+// embedding], captured once into a hipGraph; positions and token ids live in
+// device memory so the graph replays without host edits.
+#include "qie_common.hpp"
+#include "../../include/qie/qie_engine.h"
+#include "qie_index.hpp"
+
+#include <chrono>
+#include <cstring>
+#include <fstream>
+#include <vector>
+
+namespace qie {
+int gemv(const qie_linear_args* a, hipStream_t st);
+int gemm(const qie_linear_args* a, hipStream_t st);
+}  // namespace qie
+
+using namespace qie;
+
+struct qie_engine {
+    qie_model_spec spec{};
+    qie_engine_opts opts{};
+    hipStream_t stream = nullptr;
+    void* arena = nullptr;
+    size_t arena_bytes = 0;
+    qie_index* index = nullptr;
+    std::vector<qie_layer_weights> layers;
+    qie_model_weights w{};
+    bool have_weights = false;
+    float* rope_cos = nullptr;
+    float* rope_sin = nullptr;
+    int rope_rows = 0;
+};
+
+struct qie_batch {
+    qie_engine* e = nullptr;
+    int B = 0, max_ctx = 0;
+    uint16_t* kc = nullptr;
+    uint16_t* vc = nullptr;
+    int64_t seq_stride = 0;
+    int32_t* d_pos = nullptr;
+    int32_t* d_step = nullptr;
+    int32_t* d_hist = nullptr;
+    int32_t* d_ids = nullptr;
+    unsigned long long* d_keys = nullptr;
+    uint16_t* x_res = nullptr;
+    uint16_t* qkv = nullptr;
+    uint16_t* q = nullptr;
+    uint16_t* att = nullptr;
+    uint16_t* h = nullptr;
+    uint16_t* logits = nullptr;
+    void* attn_ws = nullptr;
+    void* samp_ws = nullptr;
+    std::vector<int32_t> h_pos;
+    // prefill scratch
+    int64_t pf_rows = 0;
+    uint16_t *pf_x = nullptr, *pf_hn = nullptr, *pf_qkv = nullptr, *pf_q = nullptr, *pf_att = nullptr,
+             *pf_h = nullptr;
+    int32_t *pf_pos = nullptr, *pf_ids = nullptr;
+    void* pf_attn_ws = nullptr;
+    // decode graph
+    hipGraphExec_t gexec = nullptr;
+    qie_sampling gs{};
+    bool graph_ok = false;
+};
+
+namespace qie {
+
+// ------------------------------------------------------------ small kernels
+// Step finalisation: chosen id -> token history, position + 1, sample step + 1,
+// next step's input row x_res[m] = E[id] (embedding_matrix_func, decode branch
+// qwen_main.cu:259-268, without the host round trip).
+__global__ __launch_bounds__(256) void finalize_kernel(int m0, unsigned long long* keys, const int32_t* ids_in,
+                                                       int32_t* ids_out, int32_t* pos, int32_t* step,
+                                                       int32_t* hist, int hist_stride, const uint4* E,
+                                                       uint4* x_res, int64_t H8, int32_t vocab) {
+    const int m = m0 + blockIdx.x;
+    int32_t tok = keys ? key_idx(keys[m]) : ids_in[m];
+    const int32_t p = pos[m];
+    __syncthreads();
+    if (tok < 0 || tok >= vocab) tok = 0;
+    if (threadIdx.x == 0) {
+        if (keys) keys[m] = 0ull;
+        if (p + 1 < hist_stride) hist[(int64_t)m * hist_stride + p + 1] = tok;
+        pos[m] = p + 1;
+        step[m] = step[m] + 1;
+        ids_out[m] = tok;
+    }
+    const uint4* src = E + (int64_t)tok * H8;
+    uint4* dst = x_res + (int64_t)m * H8;
+    for (int64_t i = threadIdx.x; i < H8; i += 256) dst[i] = src[i];
+}
+
+__global__ void set_state_kernel(int m, int32_t pos_v, int32_t step_v, int32_t tok, int32_t* pos,
+                                 int32_t* step, int32_t* hist, int hist_stride, const uint4* E,
+                                 uint4* x_res, int64_t H8, int write_row) {
+    if (threadIdx.x == 0) {
+        pos[m] = pos_v;
+        step[m] = step_v;
+        if (pos_v >= 0 && pos_v < hist_stride) hist[(int64_t)m * hist_stride + pos_v] = tok;
+    }
+    if (write_row)
+        for (int64_t i = threadIdx.x; i < H8; i += blockDim.x) x_res[(int64_t)m * H8 + i] = E[(int64_t)tok * H8 + i];
+}
+
+__global__ void iota_kernel(int32_t* p, int n, int start) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = start + i;
+}
+
+__global__ void copy_ids_kernel(const int32_t* src, int32_t* dst, int n) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[i];
+}
+
+static int dmalloc(void** p, size_t bytes) {
+    QIE_HIP(hipMalloc(p, bytes < 16 ? 16 : bytes));
+    return 0;
+}
+
+#define QIE_TRY(expr)                 \
+    do {                              \
+        int _rc = (expr);             \
+        if (_rc != 0) return _rc;     \
+    } while (0)
+
+static int build_rope(qie_engine* e) {
+    const int hd = e->spec.head_dim, half = hd / 2, rows = e->opts.max_ctx;
+    std::vector<float> c((size_t)rows * half), s((size_t)rows * half);
+    QIE_TRY(qie_rope_table_host(c.data(), s.data(), rows, hd, e->spec.rope_theta, e->spec.numerics));
+    QIE_TRY(dmalloc((void**)&e->rope_cos, c.size() * 4));
+    QIE_TRY(dmalloc((void**)&e->rope_sin, s.size() * 4));
+    QIE_HIP(hipMemcpy(e->rope_cos, c.data(), c.size() * 4, hipMemcpyHostToDevice));
+    QIE_HIP(hipMemcpy(e->rope_sin, s.data(), s.size() * 4, hipMemcpyHostToDevice));
+    e->rope_rows = rows;
+    return 0;
+}
+
+static int check_align(const void* p, const char* what, int layer) {
+    if (((uintptr_t)p) % 16 != 0)
+        return fail(-22, "weight %s (layer %d) is not 16-byte aligned", what, layer);
+    return 0;
+}
+
+// Resolve role pointers from the reference index (short_name, layer) ->
+// arena + data_offsets[0]  (assign_weight_pointer, helpers.cuh:19-30).
+static int bind_from_index(qie_engine* e) {
+    const qie_model_spec& s = e->spec;
+    char* base = (char*)e->arena;
+    auto get = [&](const char* sn, int layer, const void** out, bool required) -> int {
+        const qie_index_entry* t = index_find(e->index, sn, layer);
+        if (!t) {
+            if (required) return fail(-22, "tensor %s (layer %d) missing from index", sn, layer);
+            *out = nullptr;
+            return 0;
+        }
+        *out = base + t->off0;
+        return check_align(*out, sn, layer);
+    };
+    e->layers.assign(s.n_layers, qie_layer_weights{});
+    for (int l = 0; l < s.n_layers; l++) {
+        qie_layer_weights& L = e->layers[l];
+        QIE_TRY(get("input_layernorm.weight", l, &L.attn_norm, true));
+        QIE_TRY(get("self_attn.q_proj.weight", l, &L.wq, true));
+        QIE_TRY(get("self_attn.k_proj.weight", l, &L.wk, true));
+        QIE_TRY(get("self_attn.v_proj.weight", l, &L.wv, true));
+        QIE_TRY(get("self_attn.q_proj.bias", l, &L.bq, s.qkv_bias != 0));
+        QIE_TRY(get("self_attn.k_proj.bias", l, &L.bk, s.qkv_bias != 0));
+        QIE_TRY(get("self_attn.v_proj.bias", l, &L.bv, s.qkv_bias != 0));
+        QIE_TRY(get("self_attn.q_norm.weight", l, &L.q_norm, s.qk_norm != 0));
+        QIE_TRY(get("self_attn.k_norm.weight", l, &L.k_norm, s.qk_norm != 0));
+        QIE_TRY(get("self_attn.o_proj.weight", l, &L.wo, true));
+        QIE_TRY(get("post_attention_layernorm.weight", l, &L.ffn_norm, true));
+        QIE_TRY(get("mlp.gate_proj.weight", l, &L.w_gate, true));
+        QIE_TRY(get("mlp.up_proj.weight", l, &L.w_up, true));
+        QIE_TRY(get("mlp.down_proj.weight", l, &L.w_down, true));
+    }
+    QIE_TRY(get("embed_tokens.weight", -1, &e->w.embed, true));
+    QIE_TRY(get("norm.weight", -1, &e->w.final_norm, true));
+    if (s.tie_embeddings) e->w.lm_head = e->w.embed;
+    else QIE_TRY(get("logits", -1, &e->w.lm_head, true));
+    e->w.n_layers = s.n_layers;
+    e->w.layers = e->layers.data();
+    e->have_weights = true;
+    return 0;
+}
+
+// ------------------------------------------------------------- enqueue helpers
+static qie_linear_args lin_base() {
+    qie_linear_args a;
+    std::memset(&a, 0, sizeof(a));
+    return a;
+}
+
+static int enqueue_layer_decode(qie_batch* b, int l) {
+    qie_engine* e = b->e;
+    const qie_model_spec& s = e->spec;
+    const qie_layer_weights& L = e->layers[l];
+    hipStream_t st = e->stream;
+    const int64_t H = s.hidden, hd = s.head_dim, QD = (int64_t)s.n_heads * hd, KD = (int64_t)s.n_kv_heads * hd;
+    const int64_t QKVD = QD + 2 * KD, I = s.ffn, B = b->B;
+    qie_kv_cache cache{b->kc, b->vc, b->seq_stride, s.n_layers, s.n_kv_heads, s.head_dim, b->max_ctx};
+
+    qie_linear_args a = lin_base();
+    a.x = b->x_res; a.ldx = H;
+    a.w[0] = L.wq; a.w[1] = L.wk; a.w[2] = L.wv;
+    a.bias[0] = L.bq; a.bias[1] = L.bk; a.bias[2] = L.bv;
+    a.seg_rows[0] = QD; a.seg_rows[1] = KD; a.seg_rows[2] = KD;
+    a.M = B; a.K = H; a.N = QKVD;
+    a.y = b->qkv; a.ldy = QKVD;
+    a.epilogue = QIE_EPI_STORE;
+    a.norm_w = L.attn_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
+    QIE_TRY(gemv(&a, st));
+
+    QIE_TRY(qie_qkv_post(b->qkv, B, b->d_pos, 1, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, s.n_heads,
+                         &cache, l, s.rms_eps, s.numerics, b->q, st));
+    QIE_TRY(qie_attention(b->q, B, b->d_pos, 1, &cache, l, s.n_heads, b->att, b->attn_ws, st));
+
+    a = lin_base();
+    a.x = b->att; a.ldx = QD;
+    a.w[0] = L.wo; a.seg_rows[0] = H;
+    a.M = B; a.K = QD; a.N = H;
+    a.y = b->x_res; a.ldy = H;
+    a.epilogue = QIE_EPI_RESIDUAL;
+    QIE_TRY(gemv(&a, st));
+
+    a = lin_base();
+    a.x = b->x_res; a.ldx = H;
+    a.w[0] = L.w_gate; a.w[1] = L.w_up; a.seg_rows[0] = I; a.seg_rows[1] = I;
+    a.M = B; a.K = H; a.N = I;
+    a.y = b->h; a.ldy = I;
+    a.epilogue = QIE_EPI_SWIGLU;
+    a.norm_w = L.ffn_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
+    QIE_TRY(gemv(&a, st));
+
+    a = lin_base();
+    a.x = b->h; a.ldx = I;
+    a.w[0] = L.w_down; a.seg_rows[0] = H;
+    a.M = B; a.K = I; a.N = H;
+    a.y = b->x_res; a.ldy = H;
+    a.epilogue = QIE_EPI_RESIDUAL;
+    QIE_TRY(gemv(&a, st));
+    return 0;
+}
+
+static bool is_greedy(const qie_sampling* s) { return !s || s->top_k <= 1 || !(s->temperature > 0.f); }
+
+// lm_head over rows [m0, m0+M) of x (already the residual stream), then the
+// sampler; leaves ids in d_keys (greedy) or d_ids.
+static int enqueue_head(qie_batch* b, const uint16_t* x, int64_t ldx, int m0, int M, const qie_sampling* smp) {
+    qie_engine* e = b->e;
+    const qie_model_spec& s = e->spec;
+    hipStream_t st = e->stream;
+    qie_linear_args a = lin_base();
+    a.x = x; a.ldx = ldx;
+    a.w[0] = e->w.lm_head; a.seg_rows[0] = s.vocab;
+    a.M = M; a.K = s.hidden; a.N = s.vocab;
+    a.y = b->logits + (int64_t)m0 * s.vocab; a.ldy = s.vocab;
+    a.epilogue = QIE_EPI_STORE;
+    a.norm_w = e->w.final_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
+    const bool greedy = is_greedy(smp);
+    if (greedy) a.argmax_keys = (uint64_t*)(b->d_keys + m0);
+    QIE_TRY(gemv(&a, st));
+    if (!greedy)
+        QIE_TRY(qie_sample(b->logits + (int64_t)m0 * s.vocab, M, s.vocab, s.vocab, smp, b->d_step + m0,
+                           b->d_ids + m0, b->samp_ws, st));
+    hipLaunchKernelGGL(finalize_kernel, dim3(M), dim3(256), 0, st, m0, greedy ? b->d_keys : nullptr,
+                       b->d_ids, b->d_ids, b->d_pos, b->d_step, b->d_hist, b->max_ctx,
+                       (const uint4*)e->w.embed, (uint4*)b->x_res, (int64_t)s.hidden / 8, s.vocab);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+
+static int enqueue_decode(qie_batch* b, const qie_sampling* smp) {
+    for (int l = 0; l < b->e->spec.n_layers; l++) QIE_TRY(enqueue_layer_decode(b, l));
+    return enqueue_head(b, b->x_res, b->e->spec.hidden, 0, b->B, smp);
+}
+
+static int ensure_prefill_scratch(qie_batch* b, int64_t n) {
+    if (n <= b->pf_rows) return 0;
+    const qie_model_spec& s = b->e->spec;
+    const int64_t H = s.hidden, QD = (int64_t)s.n_heads * s.head_dim, KD = (int64_t)s.n_kv_heads * s.head_dim;
+    hipFree(b->pf_x); hipFree(b->pf_hn); hipFree(b->pf_qkv); hipFree(b->pf_q); hipFree(b->pf_att);
+    hipFree(b->pf_h); hipFree(b->pf_pos); hipFree(b->pf_ids); hipFree(b->pf_attn_ws);
+    b->pf_rows = 0;
+    QIE_TRY(dmalloc((void**)&b->pf_x, n * H * 2));
+    QIE_TRY(dmalloc((void**)&b->pf_hn, n * H * 2));
+    QIE_TRY(dmalloc((void**)&b->pf_qkv, n * (QD + 2 * KD) * 2));
+    QIE_TRY(dmalloc((void**)&b->pf_q, n * QD * 2));
+    QIE_TRY(dmalloc((void**)&b->pf_att, n * QD * 2));
+    QIE_TRY(dmalloc((void**)&b->pf_h, n * (int64_t)s.ffn * 2));
+    QIE_TRY(dmalloc((void**)&b->pf_pos, n * 4));
+    QIE_TRY(dmalloc((void**)&b->pf_ids, n * 4));
+    int64_t ws = qie_attention_workspace_bytes(n, s.n_heads, s.head_dim, b->max_ctx);
+    QIE_TRY(dmalloc(&b->pf_attn_ws, (size_t)ws));
+    b->pf_rows = n;
+    return 0;
+}
+
+static int sync_ids(qie_batch* b, int32_t* next_ids) {
+    if (!next_ids) return 0;
+    QIE_HIP(hipMemcpyAsync(next_ids, b->d_ids, b->B * 4, hipMemcpyDeviceToHost, b->e->stream));
+    QIE_HIP(hipStreamSynchronize(b->e->stream));
+    return 0;
+}
+
+}  // namespace qie
+
+extern "C" {
+
+int qie_engine_create(const qie_model_spec* spec, const qie_engine_opts* opts, qie_engine** out) {
+    QIE_REQUIRE(spec && out, "qie_engine_create: bad arguments");
+    const qie_model_spec& s = *spec;
+    QIE_REQUIRE(s.n_layers > 0 && s.hidden > 0 && s.n_heads > 0 && s.n_kv_heads > 0 && s.head_dim > 0 &&
+                    s.ffn > 0 && s.vocab > 0 && s.n_heads % s.n_kv_heads == 0,
+                "qie_engine_create: invalid model spec");
+    QIE_REQUIRE(s.hidden % 8 == 0 && s.ffn % 8 == 0 && (s.head_dim == 64 || s.head_dim == 128),
+                "qie_engine_create: hidden/ffn must be multiples of 8 and head_dim 64 or 128");
+    qie_engine* e = new qie_engine();
+    e->spec = s;
+    if (opts) e->opts = *opts;
+    if (e->opts.max_ctx <= 0) e->opts.max_ctx = 32786;   // reference CONTEXT_SIZE (iengine.cuh:19)
+    if (e->opts.tp_size <= 0) e->opts.tp_size = 1;
+    hipError_t he = hipSetDevice(e->opts.device);
+    if (he != hipSuccess) {
+        delete e;
+        return fail((int)he, "hipSetDevice(%d): %s", opts ? opts->device : 0, hipGetErrorString(he));
+    }
+    he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+    if (he != hipSuccess) {
+        delete e;
+        return fail((int)he, "hipStreamCreate: %s", hipGetErrorString(he));
+    }
+    int rc = build_rope(e);
+    if (rc) {
+        qie_engine_destroy(e);
+        return rc;
+    }
+    *out = e;
+    return 0;
+}
+
+static int alloc_arena_synthetic(qie_engine* e) {
+    if (e->index) qie_index_destroy(e->index);
+    e->index = nullptr;
+    QIE_TRY(qie_index_synthetic(&e->spec, &e->index));
+    e->arena_bytes = (size_t)qie_index_total_bytes(e->index);
+    if (e->arena) hipFree(e->arena);
+    e->arena = nullptr;
+    QIE_HIP(hipMalloc(&e->arena, e->arena_bytes));
+    return 0;
+}
+
+int qie_engine_init_synthetic(qie_engine* e, uint64_t seed, float w_scale, float norm_scale, float bias_scale) {
+    QIE_REQUIRE(e, "qie_engine_init_synthetic: null engine");
+    QIE_TRY(alloc_arena_synthetic(e));
+    const int n = qie_index_count(e->index);
+    for (int i = 0; i < n; i++) {
+        const char *name, *sn;
+        int32_t layer, nd;
+        int64_t o0, o1, shp[4];
+        qie_index_get(e->index, i, &name, &sn, &layer, &o0, &o1, &nd, shp);
+        const std::string sname(sn);
+        float scale = w_scale, offset = 0.f;
+        if (sname.find("norm") != std::string::npos) { scale = norm_scale; offset = 1.0f; }
+        else if (sname.find("bias") != std::string::npos) { scale = bias_scale; }
+        QIE_TRY(qie_synthetic_fill((char*)e->arena + o0, (o1 - o0) / 2, qie_tensor_id(name), seed, scale, offset,
+                                   e->stream));
+    }
+    QIE_HIP(hipStreamSynchronize(e->stream));
+    return bind_from_index(e);
+}
+
+int qie_engine_load_weights_bin(qie_engine* e, const char* weights_bin, const char* meta, int64_t chunk_bytes) {
+    QIE_REQUIRE(e && weights_bin && meta, "qie_engine_load_weights_bin: bad arguments");
+    if (e->index) qie_index_destroy(e->index);
+    e->index = nullptr;
+    QIE_TRY(qie_index_load_meta(meta, &e->index));
+    std::ifstream f(weights_bin, std::ios::binary | std::ios::ate);
+    QIE_REQUIRE(f.good(), "cannot open %s", weights_bin);
+    const int64_t file_bytes = (int64_t)f.tellg();
+    f.seekg(0);
+    const int64_t need = qie_index_total_bytes(e->index);
+    QIE_REQUIRE(file_bytes >= need, "%s is %lld bytes, index needs %lld", weights_bin, (long long)file_bytes,
+                (long long)need);
+    e->arena_bytes = (size_t)need;
+    if (e->arena) hipFree(e->arena);
+    e->arena = nullptr;
+    QIE_HIP(hipMalloc(&e->arena, e->arena_bytes));
+    if (chunk_bytes <= 0) chunk_bytes = (int64_t)1 << 28;
+    // Two pinned staging buffers: file read of chunk i+1 overlaps H2D of chunk i.
+    void* stage[2] = {nullptr, nullptr};
+    hipEvent_t done[2];
+    QIE_HIP(hipHostMalloc(&stage[0], chunk_bytes, hipHostMallocDefault));
+    QIE_HIP(hipHostMalloc(&stage[1], chunk_bytes, hipHostMallocDefault));
+    QIE_HIP(hipEventCreate(&done[0]));
+    QIE_HIP(hipEventCreate(&done[1]));
+    int64_t off = 0;
+    int which = 0;
+    bool pending[2] = {false, false};
+    int rc = 0;
+    while (off < need) {
+        const int64_t n = std::min<int64_t>(chunk_bytes, need - off);
+        if (pending[which]) {
+            hipEventSynchronize(done[which]);
+            pending[which] = false;
+        }
+        f.read((char*)stage[which], n);
+        if (f.gcount() != n) { rc = fail(-5, "short read of %s at %lld", weights_bin, (long long)off); break; }
+        hipError_t he = hipMemcpyAsync((char*)e->arena + off, stage[which], n, hipMemcpyHostToDevice, e->stream);
+        if (he != hipSuccess) { rc = fail((int)he, "H2D: %s", hipGetErrorString(he)); break; }
+        hipEventRecord(done[which], e->stream);
+        pending[which] = true;
+        off += n;
+        which ^= 1;
+    }
+    hipStreamSynchronize(e->stream);
+    hipEventDestroy(done[0]);
+    hipEventDestroy(done[1]);
+    hipHostFree(stage[0]);
+    hipHostFree(stage[1]);
+    if (rc) return rc;
+    return bind_from_index(e);
+}
+
+int qie_engine_set_weights(qie_engine* e, const qie_model_weights* w) {
+    QIE_REQUIRE(e && w && w->layers && w->n_layers == e->spec.n_layers && w->embed && w->final_norm && w->lm_head,
+                "qie_engine_set_weights: bad arguments");
+    e->layers.assign(w->layers, w->layers + w->n_layers);
+    for (int l = 0; l < w->n_layers; l++) {
+        const qie_layer_weights& L = e->layers[l];
+        QIE_REQUIRE(L.attn_norm && L.wq && L.wk && L.wv && L.wo && L.ffn_norm && L.w_gate && L.w_up && L.w_down,
+                    "qie_engine_set_weights: layer %d incomplete", l);
+        QIE_REQUIRE(!e->spec.qkv_bias || (L.bq && L.bk && L.bv), "layer %d: q/k/v bias missing", l);
+        QIE_REQUIRE(!e->spec.qk_norm || (L.q_norm && L.k_norm), "layer %d: q/k norm missing", l);
+        const void* ps[] = {L.attn_norm, L.wq, L.wk, L.wv, L.wo, L.ffn_norm, L.w_gate, L.w_up, L.w_down};
+        for (const void* p : ps) QIE_TRY(check_align(p, "weight", l));
+    }
+    e->w = *w;
+    e->w.layers = e->layers.data();
+    e->have_weights = true;
+    return 0;
+}
+
+int qie_engine_weights(const qie_engine* e, qie_model_weights* out, const qie_layer_weights** layers) {
+    QIE_REQUIRE(e && e->have_weights, "qie_engine_weights: no weights");
+    if (out) *out = e->w;
+    if (layers) *layers = e->layers.data();
+    return 0;
+}
+
+int qie_engine_spec(const qie_engine* e, qie_model_spec* out) {
+    QIE_REQUIRE(e && out, "qie_engine_spec: bad arguments");
+    *out = e->spec;
+    return 0;
+}
+
+void* qie_engine_stream(qie_engine* e) { return e ? (void*)e->stream : nullptr; }
+
+int qie_engine_sync(qie_engine* e) {
+    QIE_REQUIRE(e, "qie_engine_sync: null");
+    QIE_HIP(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+void qie_engine_destroy(qie_engine* e) {
+    if (!e) return;
+    if (e->stream) hipStreamSynchronize(e->stream);
+    if (e->arena) hipFree(e->arena);
+    if (e->rope_cos) hipFree(e->rope_cos);
+    if (e->rope_sin) hipFree(e->rope_sin);
+    if (e->index) qie_index_destroy(e->index);
+    if (e->stream) hipStreamDestroy(e->stream);
+    delete e;
+}
+
+int qie_batch_create(qie_engine* e, int32_t batch, int32_t max_ctx, qie_batch** out) {
+    QIE_REQUIRE(e && out && batch > 0 && batch <= 8 && max_ctx > 1, "qie_batch_create: bad arguments (B <= 8)");
+    QIE_REQUIRE(e->have_weights, "qie_batch_create: engine has no weights");
+    QIE_REQUIRE(max_ctx <= e->rope_rows, "qie_batch_create: max_ctx %d > engine max_ctx %d", max_ctx, e->rope_rows);
+    const qie_model_spec& s = e->spec;
+    qie_batch* b = new qie_batch();
+    b->e = e;
+    b->B = batch;
+    b->max_ctx = max_ctx;
+    const int64_t H = s.hidden, hd = s.head_dim, QD = (int64_t)s.n_heads * hd, KD = (int64_t)s.n_kv_heads * hd;
+    b->seq_stride = (int64_t)s.n_layers * s.n_kv_heads * max_ctx * hd;
+    int rc = 0;
+    auto A = [&](void** p, size_t bytes) {
+        if (!rc) rc = dmalloc(p, bytes);
+    };
+    A((void**)&b->kc, (size_t)batch * b->seq_stride * 2);
+    A((void**)&b->vc, (size_t)batch * b->seq_stride * 2);
+    A((void**)&b->d_pos, batch * 4);
+    A((void**)&b->d_step, batch * 4);
+    A((void**)&b->d_hist, (size_t)batch * max_ctx * 4);
+    A((void**)&b->d_ids, batch * 4);
+    A((void**)&b->d_keys, batch * 8);
+    A((void**)&b->x_res, batch * H * 2);
+    A((void**)&b->qkv, batch * (QD + 2 * KD) * 2);
+    A((void**)&b->q, batch * QD * 2);
+    A((void**)&b->att, batch * QD * 2);
+    A((void**)&b->h, batch * (int64_t)s.ffn * 2);
+    A((void**)&b->logits, batch * (int64_t)s.vocab * 2);
+    A(&b->attn_ws, (size_t)qie_attention_workspace_bytes(batch, s.n_heads, s.head_dim, max_ctx));
+    A(&b->samp_ws, (size_t)qie_sample_workspace_bytes(batch, s.vocab));
+    if (!rc) {
+        hipMemsetAsync(b->d_keys, 0, batch * 8, e->stream);
+        hipMemsetAsync(b->d_pos, 0, batch * 4, e->stream);
+        hipMemsetAsync(b->d_step, 0, batch * 4, e->stream);
+        hipMemsetAsync(b->d_ids, 0, batch * 4, e->stream);
+        hipMemsetAsync(b->d_hist, 0, (size_t)batch * max_ctx * 4, e->stream);
+        hipMemsetAsync(b->x_res, 0, batch * H * 2, e->stream);
+        hipError_t he = hipStreamSynchronize(e->stream);
+        if (he != hipSuccess) rc = fail((int)he, "batch init: %s", hipGetErrorString(he));
+    }
+    if (rc) {
+        qie_batch_destroy(b);
+        return rc;
+    }
+    b->h_pos.assign(batch, 0);
+    *out = b;
+    return 0;
+}
+
+void qie_batch_destroy(qie_batch* b) {
+    if (!b) return;
+    if (b->e && b->e->stream) hipStreamSynchronize(b->e->stream);
+    if (b->gexec) hipGraphExecDestroy(b->gexec);
+    void* ps[] = {b->kc, b->vc, b->d_pos, b->d_step, b->d_hist, b->d_ids, b->d_keys, b->x_res, b->qkv, b->q,
+                  b->att, b->h, b->logits, b->attn_ws, b->samp_ws, b->pf_x, b->pf_hn, b->pf_qkv, b->pf_q,
+                  b->pf_att, b->pf_h, b->pf_pos, b->pf_ids, b->pf_attn_ws};
+    for (void* p : ps)
+        if (p) hipFree(p);
+    delete b;
+}
+
+int qie_prefill(qie_batch* b, int32_t seq, const int32_t* ids, int32_t n, const qie_sampling* smp, int32_t* next_id) {
+    QIE_REQUIRE(b && ids && n > 0 && seq >= 0 && seq < b->B, "qie_prefill: bad arguments");
+    QIE_REQUIRE(n < b->max_ctx, "qie_prefill: prompt of %d tokens does not fit max_ctx %d", n, b->max_ctx);
+    qie_engine* e = b->e;
+    const qie_model_spec& s = e->spec;
+    for (int i = 0; i < n; i++)
+        QIE_REQUIRE(ids[i] >= 0 && ids[i] < s.vocab, "qie_prefill: token id %d out of range", ids[i]);
+    hipStream_t st = e->stream;
+    QIE_TRY(ensure_prefill_scratch(b, n));
+    const int64_t H = s.hidden, hd = s.head_dim, QD = (int64_t)s.n_heads * hd, KD = (int64_t)s.n_kv_heads * hd;
+    const int64_t QKVD = QD + 2 * KD, I = s.ffn;
+    QIE_HIP(hipMemcpyAsync(b->pf_ids, ids, (size_t)n * 4, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(iota_kernel, dim3((n + 255) / 256), dim3(256), 0, st, b->pf_pos, n, 0);
+    hipLaunchKernelGGL(copy_ids_kernel, dim3((n + 255) / 256), dim3(256), 0, st, b->pf_ids,
+                       b->d_hist + (int64_t)seq * b->max_ctx, n);
+    QIE_TRY(qie_embedding(e->w.embed, b->pf_ids, b->pf_x, n, H, st));
+    qie_kv_cache cache{b->kc + (int64_t)seq * b->seq_stride, b->vc + (int64_t)seq * b->seq_stride, b->seq_stride,
+                       s.n_layers, s.n_kv_heads, s.head_dim, b->max_ctx};
+    for (int l = 0; l < s.n_layers; l++) {
+        const qie_layer_weights& L = e->layers[l];
+        QIE_TRY(qie_rmsnorm(b->pf_x, L.attn_norm, b->pf_hn, n, H, s.rms_eps, s.numerics, st));
+        qie_linear_args a = lin_base();
+        a.x = b->pf_hn; a.ldx = H;
+        a.w[0] = L.wq; a.w[1] = L.wk; a.w[2] = L.wv;
+        a.bias[0] = L.bq; a.bias[1] = L.bk; a.bias[2] = L.bv;
+        a.seg_rows[0] = QD; a.seg_rows[1] = KD; a.seg_rows[2] = KD;
+        a.M = n; a.K = H; a.N = QKVD; a.y = b->pf_qkv; a.ldy = QKVD; a.epilogue = QIE_EPI_STORE;
+        QIE_TRY(qie_linear(&a, st));
+        QIE_TRY(qie_qkv_post(b->pf_qkv, n, b->pf_pos, n, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, s.n_heads,
+                             &cache, l, s.rms_eps, s.numerics, b->pf_q, st));
+        QIE_TRY(qie_attention(b->pf_q, n, b->pf_pos, n, &cache, l, s.n_heads, b->pf_att, b->pf_attn_ws, st));
+        a = lin_base();
+        a.x = b->pf_att; a.ldx = QD; a.w[0] = L.wo; a.seg_rows[0] = H;
+        a.M = n; a.K = QD; a.N = H; a.y = b->pf_x; a.ldy = H; a.epilogue = QIE_EPI_RESIDUAL;
+        QIE_TRY(qie_linear(&a, st));
+        QIE_TRY(qie_rmsnorm(b->pf_x, L.ffn_norm, b->pf_hn, n, H, s.rms_eps, s.numerics, st));
+        a = lin_base();
+        a.x = b->pf_hn; a.ldx = H; a.w[0] = L.w_gate; a.w[1] = L.w_up; a.seg_rows[0] = I; a.seg_rows[1] = I;
+        a.M = n; a.K = H; a.N = I; a.y = b->pf_h; a.ldy = I; a.epilogue = QIE_EPI_SWIGLU;
+        QIE_TRY(qie_linear(&a, st));
+        a = lin_base();
+        a.x = b->pf_h; a.ldx = I; a.w[0] = L.w_down; a.seg_rows[0] = H;
+        a.M = n; a.K = I; a.N = H; a.y = b->pf_x; a.ldy = H; a.epilogue = QIE_EPI_RESIDUAL;
+        QIE_TRY(qie_linear(&a, st));
+    }
+    // position of the last prompt token; finalize advances it to n (the new token).
+    hipLaunchKernelGGL(set_state_kernel, dim3(1), dim3(64), 0, st, seq, n - 1, 0, ids[n - 1], b->d_pos, b->d_step,
+                       b->d_hist, b->max_ctx, (const uint4*)e->w.embed, (uint4*)b->x_res, (int64_t)H / 8, 0);
+    QIE_TRY(enqueue_head(b, b->pf_x + (int64_t)(n - 1) * H, H, seq, 1, smp));
+    b->h_pos[seq] = n;
+    if (next_id) {
+        QIE_HIP(hipMemcpyAsync(next_id, b->d_ids + seq, 4, hipMemcpyDeviceToHost, st));
+        QIE_HIP(hipStreamSynchronize(st));
+    }
+    return 0;
+}
+
+static bool same_sampling(const qie_sampling& a, const qie_sampling* b) {
+    qie_sampling g{1, 0.f, 1.f, 0};
+    const qie_sampling& bb = b ? *b : g;
+    return a.top_k == bb.top_k && a.temperature == bb.temperature && a.top_p == bb.top_p && a.seed == bb.seed;
+}
+
+static int launch_step(qie_batch* b, const qie_sampling* smp) {
+    qie_engine* e = b->e;
+    if (!e->opts.use_graph) return enqueue_decode(b, smp);
+    if (!b->graph_ok || !same_sampling(b->gs, smp)) {
+        if (b->gexec) hipGraphExecDestroy(b->gexec);
+        b->gexec = nullptr;
+        b->graph_ok = false;
+        hipGraph_t g = nullptr;
+        QIE_HIP(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+        int rc = enqueue_decode(b, smp);
+        hipError_t he = hipStreamEndCapture(e->stream, &g);
+        if (rc) {
+            if (g) hipGraphDestroy(g);
+            return rc;
+        }
+        if (he != hipSuccess) return fail((int)he, "graph capture: %s", hipGetErrorString(he));
+        he = hipGraphInstantiate(&b->gexec, g, nullptr, nullptr, 0);
+        hipGraphDestroy(g);
+        if (he != hipSuccess) return fail((int)he, "graph instantiate: %s", hipGetErrorString(he));
+        b->gs = smp ? *smp : qie_sampling{1, 0.f, 1.f, 0};
+        b->graph_ok = true;
+    }
+    QIE_HIP(hipGraphLaunch(b->gexec, e->stream));
+    return 0;
+}
+
+int qie_decode_step(qie_batch* b, const qie_sampling* smp, int32_t* next_ids) {
+    QIE_REQUIRE(b, "qie_decode_step: null batch");
+    for (int m = 0; m < b->B; m++)
+        QIE_REQUIRE(b->h_pos[m] + 1 < b->max_ctx, "qie_decode_step: sequence %d is full (max_ctx %d)", m, b->max_ctx);
+    QIE_TRY(launch_step(b, smp));
+    for (int m = 0; m < b->B; m++) b->h_pos[m] += 1;
+    return sync_ids(b, next_ids);
+}
+
+int qie_decode(qie_batch* b, int32_t n_steps, const qie_sampling* smp, int32_t* out_ids) {
+    QIE_REQUIRE(b && n_steps >= 0, "qie_decode: bad arguments");
+    std::vector<int32_t> p0 = b->h_pos;
+    for (int m = 0; m < b->B; m++)
+        QIE_REQUIRE(b->h_pos[m] + n_steps < b->max_ctx, "qie_decode: sequence %d would exceed max_ctx", m);
+    for (int i = 0; i < n_steps; i++) {
+        QIE_TRY(launch_step(b, smp));
+        for (int m = 0; m < b->B; m++) b->h_pos[m] += 1;
+    }
+    QIE_HIP(hipStreamSynchronize(b->e->stream));
+    if (out_ids && n_steps > 0) {
+        std::vector<int32_t> row(b->max_ctx);
+        for (int m = 0; m < b->B; m++) {
+            QIE_HIP(hipMemcpy(row.data(), b->d_hist + (int64_t)m * b->max_ctx, (size_t)b->max_ctx * 4,
+                              hipMemcpyDeviceToHost));
+            for (int i = 0; i < n_steps; i++) out_ids[(int64_t)i * b->B + m] = row[p0[m] + 1 + i];
+        }
+    }
+    return 0;
+}
+
+int qie_batch_logits(qie_batch* b, void* host_out) {
+    QIE_REQUIRE(b && host_out, "qie_batch_logits: bad arguments");
+    QIE_HIP(hipStreamSynchronize(b->e->stream));
+    QIE_HIP(hipMemcpy(host_out, b->logits, (size_t)b->B * b->e->spec.vocab * 2, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int qie_batch_positions(qie_batch* b, int32_t* host_pos) {
+    QIE_REQUIRE(b && host_pos, "qie_batch_positions: bad arguments");
+    QIE_HIP(hipStreamSynchronize(b->e->stream));
+    QIE_HIP(hipMemcpy(host_pos, b->d_pos, (size_t)b->B * 4, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int qie_batch_history(qie_batch* b, int32_t seq, int32_t* host_ids, int32_t n) {
+    QIE_REQUIRE(b && host_ids && seq >= 0 && seq < b->B && n >= 0 && n <= b->max_ctx,
+                "qie_batch_history: bad arguments");
+    QIE_HIP(hipStreamSynchronize(b->e->stream));
+    QIE_HIP(hipMemcpy(host_ids, b->d_hist + (int64_t)seq * b->max_ctx, (size_t)n * 4, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int qie_batch_set_position(qie_batch* b, int32_t seq, int32_t pos, int32_t token) {
+    QIE_REQUIRE(b && seq >= 0 && seq < b->B && pos >= 0 && pos + 1 < b->max_ctx && token >= 0 &&
+                    token < b->e->spec.vocab,
+                "qie_batch_set_position: bad arguments");
+    qie_engine* e = b->e;
+    hipLaunchKernelGGL(set_state_kernel, dim3(1), dim3(256), 0, e->stream, seq, pos, pos, token, b->d_pos, b->d_step,
+                       b->d_hist, b->max_ctx, (const uint4*)e->w.embed, (uint4*)b->x_res,
+                       (int64_t)e->spec.hidden / 8, 1);
+    QIE_LAUNCH_CHECK();
+    QIE_HIP(hipStreamSynchronize(e->stream));
+    b->h_pos[seq] = pos;
+    return 0;
+}
+
+int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* avg_us, double* bytes) {
+    QIE_REQUIRE(b && iters > 0 && avg_us && bytes, "qie_batch_time_kernel: bad arguments");
+    qie_engine* e = b->e;
+    const qie_model_spec& s = e->spec;
+    const qie_layer_weights& L = e->layers[0];
+    const int64_t H = s.hidden, hd = s.head_dim, QD = (int64_t)s.n_heads * hd, KD = (int64_t)s.n_kv_heads * hd;
+    const int64_t I = s.ffn, B = b->B;
+    // scratch output so timing never disturbs the sequence state
+    uint16_t* scratch = nullptr;
+    QIE_TRY(dmalloc((void**)&scratch, (size_t)B * std::max<int64_t>(std::max(I, (int64_t)s.vocab), QD + 2 * KD) * 2));
+    qie_linear_args a = lin_base();
+    double by = 0;
+    if (which == 0) {
+        a.x = b->x_res; a.ldx = H; a.w[0] = L.w_gate; a.w[1] = L.w_up; a.seg_rows[0] = I; a.seg_rows[1] = I;
+        a.M = B; a.K = H; a.N = I; a.y = scratch; a.ldy = I; a.epilogue = QIE_EPI_SWIGLU;
+        a.norm_w = L.ffn_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
+        by = 2.0 * I * H * 2 + B * H * 2 + H * 2 + B * I * 2;
+    } else if (which == 1) {
+        a.x = b->h; a.ldx = I; a.w[0] = L.w_down; a.seg_rows[0] = H;
+        a.M = B; a.K = I; a.N = H; a.y = scratch; a.ldy = H; a.epilogue = QIE_EPI_STORE;
+        by = (double)H * I * 2 + B * I * 2 + B * H * 2;
+    } else if (which == 2) {
+        a.x = b->x_res; a.ldx = H; a.w[0] = L.wq; a.w[1] = L.wk; a.w[2] = L.wv;
+        a.bias[0] = L.bq; a.bias[1] = L.bk; a.bias[2] = L.bv;
+        a.seg_rows[0] = QD; a.seg_rows[1] = KD; a.seg_rows[2] = KD;
+        a.M = B; a.K = H; a.N = QD + 2 * KD; a.y = scratch; a.ldy = QD + 2 * KD; a.epilogue = QIE_EPI_STORE;
+        a.norm_w = L.attn_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
+        by = (double)(QD + 2 * KD) * H * 2 + B * H * 2 + B * (QD + 2 * KD) * 2;
+    } else if (which == 3) {
+        a.x = b->att; a.ldx = QD; a.w[0] = L.wo; a.seg_rows[0] = H;
+        a.M = B; a.K = QD; a.N = H; a.y = scratch; a.ldy = H; a.epilogue = QIE_EPI_STORE;
+        by = (double)H * QD * 2 + B * QD * 2 + B * H * 2;
+    } else if (which == 4) {
+        a.x = b->x_res; a.ldx = H; a.w[0] = e->w.lm_head; a.seg_rows[0] = s.vocab;
+        a.M = B; a.K = H; a.N = s.vocab; a.y = scratch; a.ldy = s.vocab; a.epilogue = QIE_EPI_STORE;
+        a.norm_w = e->w.final_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
+        by = (double)s.vocab * H * 2 + B * H * 2 + B * (double)s.vocab * 2;
+    } else if (which != 5) {
+        hipFree(scratch);
+        return fail(-22, "qie_batch_time_kernel: unknown kernel %d", which);
+    }
+    qie_kv_cache cache{b->kc, b->vc, b->seq_stride, s.n_layers, s.n_kv_heads, s.head_dim, b->max_ctx};
+    if (which == 5) {
+        std::vector<int32_t> pos(B);
+        hipMemcpy(pos.data(), b->d_pos, B * 4, hipMemcpyDeviceToHost);
+        by = 0;
+        for (int m = 0; m < B; m++) by += (double)(pos[m] + 1) * KD * 2 * 2;
+        by += (double)B * QD * 2 * 2;
+    }
+    hipEvent_t t0, t1;
+    QIE_HIP(hipEventCreate(&t0));
+    QIE_HIP(hipEventCreate(&t1));
+    auto run = [&]() -> int {
+        if (which == 5) return qie_attention(b->q, B, b->d_pos, 1, &cache, 0, s.n_heads, scratch, b->attn_ws, e->stream);
+        return qie_linear(&a, e->stream);
+    };
+    QIE_TRY(run());   // warm-up
+    QIE_HIP(hipEventRecord(t0, e->stream));
+    for (int i = 0; i < iters; i++) QIE_TRY(run());
+    QIE_HIP(hipEventRecord(t1, e->stream));
+    QIE_HIP(hipEventSynchronize(t1));
+    float ms = 0;
+    QIE_HIP(hipEventElapsedTime(&ms, t0, t1));
+    hipEventDestroy(t0);
+    hipEventDestroy(t1);
+    hipFree(scratch);
+    *avg_us = ms * 1000.0 / iters;
+    *bytes = by;
+    return 0;
+}
+
+int qie_linear(const qie_linear_args* a, void* stream) {
+    QIE_REQUIRE(a && a->x && a->y && a->w[0] && a->M > 0 && a->K > 0 && a->N > 0, "qie_linear: bad arguments");
+    QIE_REQUIRE(a->K % 8 == 0 && a->ldx >= a->K && a->ldx % 8 == 0, "qie_linear: K and ldx must be multiples of 8");
+    QIE_REQUIRE(((uintptr_t)a->x % 16) == 0, "qie_linear: x must be 16-byte aligned");
+    for (int i = 0; i < 3; i++)
+        QIE_REQUIRE(((uintptr_t)a->w[i] % 16) == 0, "qie_linear: weight segment %d must be 16-byte aligned", i);
+    if (a->epilogue == QIE_EPI_SWIGLU) {
+        QIE_REQUIRE(a->w[1] && a->seg_rows[0] == a->N && a->seg_rows[1] == a->N && a->ldy >= a->N,
+                    "qie_linear: SWIGLU needs w[0]=gate, w[1]=up with N rows each");
+    } else {
+        QIE_REQUIRE(a->seg_rows[0] + a->seg_rows[1] + a->seg_rows[2] == a->N && a->ldy >= a->N,
+                    "qie_linear: seg_rows must sum to N");
+        QIE_REQUIRE(a->seg_rows[1] == 0 || a->w[1], "qie_linear: missing weight segment 1");
+        QIE_REQUIRE(a->seg_rows[2] == 0 || a->w[2], "qie_linear: missing weight segment 2");
+    }
+    QIE_REQUIRE(a->epilogue >= 0 && a->epilogue <= 2, "qie_linear: bad epilogue");
+    QIE_REQUIRE(a->argmax_keys == nullptr || a->epilogue == QIE_EPI_STORE, "qie_linear: arg-max needs STORE");
+    hipStream_t st = (hipStream_t)stream;
+    if (a->M <= 8) return gemv(a, st);
+    return gemm(a, st);
+}
+
+}  // extern "C"

@@ -1,0 +1,236 @@
+// k_gemm.hip — MFMA bf16 GEMM for the prefill projections (M = prompt rows).
+//
+// Replaces matrix_mul (layers/src/matrix_mul.cu:165-288) for M > 8: the
+// reference computes one 16x16 WMMA tile per warp with scalar 2-byte loads into
+// per-warp smem and no pipelining.  Here (gfx950):
+//   C[M, N] = A[M, K] . W[N, K]^T   (both operands K-contiguous, "NT")
+//   * 128x128 block tile, BK = 64, 4 waves as 2x2, 64x64 per wave =
+//     4x4 v_mfma_f32_16x16x32_bf16 accumulators (fp32);
+//   * 16-byte global loads staged through registers into a double-buffered,
+//     XOR-swizzled LDS image (chunk ^= row & 7), fragments by ds_read_b128;
+//     one barrier per K-tile, next tile's global loads in flight under the
+//     current tile's MFMAs;
+//   * fused epilogues: bias, residual add, SwiGLU (tile columns pair gate/up
+//     rows of the same output column inside one wave).
+//   * blockIdx.x runs over M tiles so the blocks sharing a weight tile are
+//     adjacent in dispatch order (weights streamed ~once, activations L2/MALL).
+#include "qie_common.hpp"
+#include "../../include/qie/qie_ops.h"
+
+namespace qie {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct GemmParams {
+    const uint16_t* A;
+    int64_t lda;
+    const uint16_t* w0;
+    const uint16_t* w1;
+    const uint16_t* w2;
+    const uint16_t* b0;
+    const uint16_t* b1;
+    const uint16_t* b2;
+    int64_t n0, n01;
+    int64_t M, K, N;     // N = output columns
+    int64_t wrows;       // total weight rows addressable (for clamping)
+    uint16_t* C;
+    int64_t ldc;
+};
+
+constexpr int BM = 128, BN = 128, BK = 64;
+
+// Weight row for tile column c of block tile starting at output column n0.
+template <int EPI>
+__device__ __forceinline__ const uint16_t* w_row(const GemmParams& p, int64_t nblk, int c,
+                                                 bool& valid) {
+    if constexpr (EPI == QIE_EPI_SWIGLU) {
+        // 64 output columns per tile: cols [64wc, 64wc+32) gate, [64wc+32, 64wc+64) up.
+        const int64_t j = nblk * 64 + 32 * (c >> 6) + (c & 31);
+        valid = j < p.N;
+        const int64_t jj = valid ? j : p.N - 1;
+        return ((c >> 5) & 1) ? p.w1 + jj * p.K : p.w0 + jj * p.K;
+    } else {
+        const int64_t r = nblk * BN + c;
+        valid = r < p.N;
+        const int64_t rr = valid ? r : p.N - 1;
+        if (rr < p.n0) return p.w0 + rr * p.K;
+        if (rr < p.n01) return p.w1 + (rr - p.n0) * p.K;
+        return p.w2 + (rr - p.n01) * p.K;
+    }
+}
+
+template <int EPI>
+__global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
+#pragma clang fp contract(off)
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint16_t* As = reinterpret_cast<uint16_t*>(smem);                 // [2][BM][BK]
+    uint16_t* Bs = reinterpret_cast<uint16_t*>(smem + 2 * BM * BK * 2);  // [2][BN][BK]
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int64_t mblk = blockIdx.x, nblk = blockIdx.y;
+    const int64_t m0 = mblk * BM;
+
+    // Per-thread staging coordinates: 4 chunks (16 B) of A and of B per K-tile.
+    const uint16_t* a_src[4];
+    const uint16_t* b_src[4];
+    int lds_off[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int c = tid + 256 * i;       // chunk id 0..1023
+        const int row = c >> 3, ch = c & 7;
+        int64_t ar = m0 + row;
+        if (ar >= p.M) ar = p.M - 1;
+        a_src[i] = p.A + ar * p.lda + ch * 8;
+        bool v;
+        b_src[i] = w_row<EPI>(p, nblk, row, v) + ch * 8;
+        lds_off[i] = row * BK + ((ch ^ (row & 7)) * 8);
+    }
+
+    const int nk = (int)((p.K + BK - 1) / BK);
+    uint4 ra[4], rb[4];
+    auto gload = [&](int kt) {
+        const int64_t kbase = (int64_t)kt * BK;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int ch = (tid + 256 * i) & 7;
+            const bool ok = kbase + ch * 8 < p.K;
+            ra[i] = ok ? *reinterpret_cast<const uint4*>(a_src[i] + kbase) : make_uint4(0, 0, 0, 0);
+            rb[i] = ok ? *reinterpret_cast<const uint4*>(b_src[i] + kbase) : make_uint4(0, 0, 0, 0);
+        }
+    };
+    auto lstore = [&](int buf) {
+        uint16_t* a = As + buf * BM * BK;
+        uint16_t* b = Bs + buf * BN * BK;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            *reinterpret_cast<uint4*>(a + lds_off[i]) = ra[i];
+            *reinterpret_cast<uint4*>(b + lds_off[i]) = rb[i];
+        }
+    };
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    gload(0);
+    lstore(0);
+    __syncthreads();
+
+    const int fr = lane & 15, fq = lane >> 4;
+    int cur = 0;
+    for (int kt = 0; kt < nk; kt++) {
+        if (kt + 1 < nk) gload(kt + 1);
+        const uint16_t* a = As + cur * BM * BK;
+        const uint16_t* b = Bs + cur * BN * BK;
+#pragma unroll
+        for (int ks = 0; ks < 2; ks++) {
+            bf16x8 af[4], bfr[4];
+            const int ch = ks * 4 + fq;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int row = wr * 64 + i * 16 + fr;
+                af[i] = *reinterpret_cast<const bf16x8*>(a + row * BK + ((ch ^ (row & 7)) * 8));
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int row = wc * 64 + j * 16 + fr;
+                bfr[j] = *reinterpret_cast<const bf16x8*>(b + row * BK + ((ch ^ (row & 7)) * 8));
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+        if (kt + 1 < nk) lstore(cur ^ 1);
+        __syncthreads();
+        cur ^= 1;
+    }
+
+    // ---------------- epilogue.  C/D map: col = lane & 15, row = 4*(lane >> 4) + r.
+    if constexpr (EPI == QIE_EPI_SWIGLU) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+#pragma unroll
+            for (int jj = 0; jj < 2; jj++) {
+                const int64_t col = nblk * 64 + 32 * wc + 16 * jj + fr;
+                if (col >= p.N) continue;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int64_t row = m0 + wr * 64 + i * 16 + fq * 4 + r;
+                    if (row >= p.M) continue;
+                    float g = rbf(acc[i][jj][r]);
+                    float u = rbf(acc[i][jj + 2][r]);
+                    float av = rbf(g * (1.0f / (1.0f + expf(-g))));
+                    p.C[row * p.ldc + col] = f2bf(u * av);
+                }
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int64_t col = nblk * BN + wc * 64 + j * 16 + fr;
+            if (col >= p.N) continue;
+            float bias = 0.f;
+            if constexpr (EPI == QIE_EPI_STORE) {
+                const uint16_t* b = col < p.n0 ? p.b0 : (col < p.n01 ? p.b1 : p.b2);
+                if (b) bias = bf2f(b[col < p.n0 ? col : (col < p.n01 ? col - p.n0 : col - p.n01)]);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int64_t row = m0 + wr * 64 + i * 16 + fq * 4 + r;
+                    if (row >= p.M) continue;
+                    uint16_t* dst = p.C + row * p.ldc + col;
+                    if constexpr (EPI == QIE_EPI_RESIDUAL)
+                        *dst = f2bf(bf2f(*dst) + rbf(acc[i][j][r]));
+                    else
+                        *dst = f2bf(acc[i][j][r] + bias);
+                }
+            }
+        }
+    }
+}
+
+int gemm(const qie_linear_args* a, hipStream_t st) {
+    QIE_REQUIRE(a->norm_w == nullptr, "qie_linear: fused RMSNorm is GEMV-only (M <= 8)");
+    QIE_REQUIRE(a->argmax_keys == nullptr, "qie_linear: fused arg-max is GEMV-only (M <= 8)");
+    GemmParams p;
+    p.A = (const uint16_t*)a->x;
+    p.lda = a->ldx;
+    p.w0 = (const uint16_t*)a->w[0];
+    p.w1 = (const uint16_t*)a->w[1];
+    p.w2 = (const uint16_t*)a->w[2];
+    p.b0 = (const uint16_t*)a->bias[0];
+    p.b1 = (const uint16_t*)a->bias[1];
+    p.b2 = (const uint16_t*)a->bias[2];
+    p.n0 = a->seg_rows[0];
+    p.n01 = a->seg_rows[0] + a->seg_rows[1];
+    p.M = a->M;
+    p.K = a->K;
+    p.N = a->N;
+    p.wrows = 0;
+    p.C = (uint16_t*)a->y;
+    p.ldc = a->ldy;
+    const size_t shm = (size_t)2 * (BM + BN) * BK * 2;
+    const unsigned gm = (unsigned)cdiv(a->M, BM);
+    if (a->epilogue == QIE_EPI_SWIGLU) {
+        hipLaunchKernelGGL(gemm_kernel<QIE_EPI_SWIGLU>, dim3(gm, (unsigned)cdiv(a->N, 64)), dim3(256),
+                           shm, st, p);
+    } else if (a->epilogue == QIE_EPI_RESIDUAL) {
+        hipLaunchKernelGGL(gemm_kernel<QIE_EPI_RESIDUAL>, dim3(gm, (unsigned)cdiv(a->N, BN)), dim3(256),
+                           shm, st, p);
+    } else {
+        hipLaunchKernelGGL(gemm_kernel<QIE_EPI_STORE>, dim3(gm, (unsigned)cdiv(a->N, BN)), dim3(256),
+                           shm, st, p);
+    }
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+
+}  // namespace qie

@@ -1,0 +1,327 @@
+// k_gemv.hip — bandwidth-bound skinny GEMM (M <= 8 rows) for the decode step.
+//
+// Replaces matrix_mul (layers/src/matrix_mul.cu:165-288) at M = 1 / small M,
+// where the reference runs 16x16 WMMA tiles with 15 of 16 rows wasted and
+// 2-byte loads.  Here (gfx950, wave64):
+//   * each wave owns RPW weight rows and streams them along K with 16-byte
+//     non-temporal loads (64 lanes x 16 B = 1 KiB per wave-instruction),
+//     U chunks in flight per row;
+//   * the activation rows live in LDS (optionally produced by a fused RMSNorm
+//     prologue — the reference's launch_rms + proj pair in one launch);
+//   * fp32 accumulation, wave butterfly reduction, one bf16 rounding;
+//   * fused epilogues: bias (Qwen2), residual add (launch_resadd), SwiGLU
+//     (launch_act + launch_elem: gate/up row j handled by the same wave), and a
+//     greedy arg-max key (logit_decode.cu:15-33 tie rule) for lm_head.
+// Grid is persistent-ish: min(tasks/4, CUs * blocks_per_cu) blocks of 4 waves
+// that grid-stride over row tasks, so the norm prologue runs once per block.
+#include "qie_common.hpp"
+#include "../../include/qie/qie_ops.h"
+
+#include <cstdlib>
+
+namespace qie {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+struct GemvParams {
+    const uint16_t* x;
+    int64_t ldx;
+    const uint16_t* w0;
+    const uint16_t* w1;
+    const uint16_t* w2;
+    const uint16_t* b0;
+    const uint16_t* b1;
+    const uint16_t* b2;
+    int64_t n0, n01;   // rows in seg0, seg0+seg1
+    int64_t K, N;      // N = output columns
+    uint16_t* y;
+    int64_t ldy;
+    const uint16_t* norm_w;
+    float eps;
+    int numerics;
+    int M;             // runtime rows (<= MT)
+    int xlds;          // 1: x staged in LDS
+    unsigned long long* keys;
+    int64_t n_tasks;
+};
+
+__device__ __forceinline__ void fma8(float& acc, const float* xf, u32x4 w) {
+    acc = fmaf(xf[0], bf_lo(w.x), acc);
+    acc = fmaf(xf[1], bf_hi(w.x), acc);
+    acc = fmaf(xf[2], bf_lo(w.y), acc);
+    acc = fmaf(xf[3], bf_hi(w.y), acc);
+    acc = fmaf(xf[4], bf_lo(w.z), acc);
+    acc = fmaf(xf[5], bf_hi(w.z), acc);
+    acc = fmaf(xf[6], bf_lo(w.w), acc);
+    acc = fmaf(xf[7], bf_hi(w.w), acc);
+}
+
+__device__ __forceinline__ void unpack8(u32x4 v, float* f) {
+    f[0] = bf_lo(v.x); f[1] = bf_hi(v.x);
+    f[2] = bf_lo(v.y); f[3] = bf_hi(v.y);
+    f[4] = bf_lo(v.z); f[5] = bf_hi(v.z);
+    f[6] = bf_lo(v.w); f[7] = bf_hi(v.w);
+}
+
+template <int MT, int RPW, int EPI, int U>
+__global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint16_t* xs = reinterpret_cast<uint16_t*>(smem);
+    float* red = reinterpret_cast<float*>(smem + (p.xlds ? (size_t)MT * p.K * 2 : 0));
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t K = p.K;
+
+    // ---------------- prologue: activation rows -> LDS (optionally RMS-normed)
+    if (p.xlds) {
+        for (int m = 0; m < MT; m++) {
+            const uint16_t* xr = p.x + (int64_t)m * p.ldx;
+            uint16_t* xo = xs + (int64_t)m * K;
+            if (m >= p.M) {
+                for (int64_t k = tid * 8; k < K; k += 2048)
+                    *reinterpret_cast<uint4*>(xo + k) = make_uint4(0, 0, 0, 0);
+                continue;
+            }
+            if (p.norm_w) {
+                float ss = 0.f;
+                for (int64_t k = tid * 8; k < K; k += 2048) {
+                    uint4 v = *reinterpret_cast<const uint4*>(xr + k);
+                    float f[8];
+                    unpack8(u32x4{v.x, v.y, v.z, v.w}, f);
+#pragma unroll
+                    for (int j = 0; j < 8; j++) ss += f[j] * f[j];
+                }
+                ss = wave_sum(ss);
+                if (lane == 0) red[wave] = ss;
+                __syncthreads();
+                ss = red[0] + red[1] + red[2] + red[3];
+                __syncthreads();
+                const float rms = sqrtf((ss / (float)K) + p.eps);
+                const float inv = 1.0f / rms;
+                const bool hf = p.numerics == QIE_NUMERICS_HF;
+                for (int64_t k = tid * 8; k < K; k += 2048) {
+#pragma clang fp contract(off)
+                    uint4 v = *reinterpret_cast<const uint4*>(xr + k);
+                    uint4 wv = *reinterpret_cast<const uint4*>(p.norm_w + k);
+                    float f[8], wf[8];
+                    unpack8(u32x4{v.x, v.y, v.z, v.w}, f);
+                    unpack8(u32x4{wv.x, wv.y, wv.z, wv.w}, wf);
+                    uint32_t o[4];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        float y0, y1;
+                        if (hf) {
+                            y0 = wf[2 * j] * rbf(f[2 * j] * inv);
+                            y1 = wf[2 * j + 1] * rbf(f[2 * j + 1] * inv);
+                        } else {
+                            y0 = (f[2 * j] / rms) * wf[2 * j];
+                            y1 = (f[2 * j + 1] / rms) * wf[2 * j + 1];
+                        }
+                        o[j] = pack2(y0, y1);
+                    }
+                    *reinterpret_cast<uint4*>(xo + k) = make_uint4(o[0], o[1], o[2], o[3]);
+                }
+            } else {
+                for (int64_t k = tid * 8; k < K; k += 2048)
+                    *reinterpret_cast<uint4*>(xo + k) = *reinterpret_cast<const uint4*>(xr + k);
+            }
+        }
+        __syncthreads();
+    }
+
+    // ---------------- main loop over row tasks
+    for (int64_t task = (int64_t)blockIdx.x * 4 + wave; task < p.n_tasks;
+         task += (int64_t)gridDim.x * 4) {
+        const u32x4* wr[RPW];
+        int64_t col[RPW];
+        if constexpr (EPI == QIE_EPI_SWIGLU) {
+            constexpr int P2 = RPW / 2;
+#pragma unroll
+            for (int i = 0; i < P2; i++) {
+                int64_t j = task * P2 + i;
+                col[i] = col[P2 + i] = j;
+                if (j >= p.N) j = p.N - 1;
+                wr[i] = reinterpret_cast<const u32x4*>(p.w0 + j * K);
+                wr[P2 + i] = reinterpret_cast<const u32x4*>(p.w1 + j * K);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < RPW; i++) {
+                int64_t r = task * RPW + i;
+                col[i] = r;
+                if (r >= p.N) r = p.N - 1;
+                const uint16_t* base;
+                if (r < p.n0) base = p.w0 + r * K;
+                else if (r < p.n01) base = p.w1 + (r - p.n0) * K;
+                else base = p.w2 + (r - p.n01) * K;
+                wr[i] = reinterpret_cast<const u32x4*>(base);
+            }
+        }
+
+        float acc[MT][RPW];
+#pragma unroll
+        for (int m = 0; m < MT; m++)
+#pragma unroll
+            for (int i = 0; i < RPW; i++) acc[m][i] = 0.f;
+
+        for (int64_t k0 = (int64_t)lane * 8; k0 < K; k0 += 512 * U) {
+            u32x4 wv[U][RPW];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int64_t k = k0 + u * 512;
+#pragma unroll
+                for (int i = 0; i < RPW; i++)
+                    wv[u][i] = (k < K) ? __builtin_nontemporal_load(wr[i] + (k >> 3))
+                                       : u32x4{0u, 0u, 0u, 0u};
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int64_t k = k0 + u * 512;
+                if (k < K) {
+#pragma unroll
+                    for (int m = 0; m < MT; m++) {
+                        uint4 xv = p.xlds ? *reinterpret_cast<const uint4*>(xs + (int64_t)m * K + k)
+                                          : (m < p.M ? *reinterpret_cast<const uint4*>(
+                                                           p.x + (int64_t)m * p.ldx + k)
+                                                     : make_uint4(0, 0, 0, 0));
+                        float xf[8];
+                        unpack8(u32x4{xv.x, xv.y, xv.z, xv.w}, xf);
+#pragma unroll
+                        for (int i = 0; i < RPW; i++) fma8(acc[m][i], xf, wv[u][i]);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < MT; m++)
+#pragma unroll
+            for (int i = 0; i < RPW; i++) acc[m][i] = wave_sum(acc[m][i]);
+
+        // ---------------- epilogue (lane 0 writes; outputs are tiny)
+        if (lane == 0) {
+#pragma clang fp contract(off)
+            for (int m = 0; m < p.M && m < MT; m++) {
+                uint16_t* yr = p.y + (int64_t)m * p.ldy;
+                if constexpr (EPI == QIE_EPI_SWIGLU) {
+                    constexpr int P2 = RPW / 2;
+#pragma unroll
+                    for (int i = 0; i < P2; i++) {
+                        if (col[i] >= p.N) continue;
+                        float g = rbf(acc[m][i]);
+                        float u = rbf(acc[m][P2 + i]);
+                        float a = rbf(g * (1.0f / (1.0f + expf(-g))));
+                        yr[col[i]] = f2bf(u * a);
+                    }
+                } else if constexpr (EPI == QIE_EPI_RESIDUAL) {
+#pragma unroll
+                    for (int i = 0; i < RPW; i++) {
+                        if (col[i] >= p.N) continue;
+                        yr[col[i]] = f2bf(bf2f(yr[col[i]]) + rbf(acc[m][i]));
+                    }
+                } else {
+                    unsigned long long best = 0ull;
+#pragma unroll
+                    for (int i = 0; i < RPW; i++) {
+                        const int64_t c = col[i];
+                        if (c >= p.N) continue;
+                        float v = acc[m][i];
+                        const uint16_t* b = c < p.n0 ? p.b0 : (c < p.n01 ? p.b1 : p.b2);
+                        if (b) {
+                            int64_t bi = c < p.n0 ? c : (c < p.n01 ? c - p.n0 : c - p.n01);
+                            v = v + bf2f(b[bi]);
+                        }
+                        uint16_t o = f2bf(v);
+                        yr[c] = o;
+                        if (p.keys) {
+                            unsigned long long kk = sel_key(bf2f(o), (uint32_t)c);
+                            best = kk > best ? kk : best;
+                        }
+                    }
+                    if (p.keys && best) atomicMax(p.keys + m, best);
+                }
+            }
+        }
+    }
+}
+
+template <int MT, int RPW, int EPI>
+static int launch_gemv_t(const GemvParams& p, hipStream_t st, int blocks_per_cu) {
+    constexpr int U = (RPW >= 4) ? 4 : 8;
+    const int64_t n_blocks_needed = (p.n_tasks + 3) / 4;
+    const int64_t cap = (int64_t)device_cu_count() * blocks_per_cu;
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min(n_blocks_needed, cap));
+    const size_t shm = (p.xlds ? (size_t)MT * p.K * 2 : 0) + 64;
+    if (shm > 65536) {
+        static bool raised = false;   // per instantiation
+        if (!raised) {
+            QIE_HIP(hipFuncSetAttribute((const void*)gemv_kernel<MT, RPW, EPI, U>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+            raised = true;
+        }
+    }
+    hipLaunchKernelGGL((gemv_kernel<MT, RPW, EPI, U>), dim3(grid), dim3(256), shm, st, p);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+
+template <int MT>
+static int launch_gemv_m(const GemvParams& p, int rpw, int epi, hipStream_t st, int bpc) {
+    if (epi == QIE_EPI_SWIGLU) {
+        return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_SWIGLU>(p, st, bpc)
+                        : launch_gemv_t<MT, 2, QIE_EPI_SWIGLU>(p, st, bpc);
+    } else if (epi == QIE_EPI_RESIDUAL) {
+        return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_RESIDUAL>(p, st, bpc)
+                        : launch_gemv_t<MT, 2, QIE_EPI_RESIDUAL>(p, st, bpc);
+    }
+    return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_STORE>(p, st, bpc)
+                    : launch_gemv_t<MT, 2, QIE_EPI_STORE>(p, st, bpc);
+}
+
+static int env_int(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v ? atoi(v) : dflt;
+}
+
+constexpr size_t kGemvLdsCap = 96 * 1024;
+
+int gemv(const qie_linear_args* a, hipStream_t st) {
+    GemvParams p;
+    p.x = (const uint16_t*)a->x;
+    p.ldx = a->ldx;
+    p.w0 = (const uint16_t*)a->w[0];
+    p.w1 = (const uint16_t*)a->w[1];
+    p.w2 = (const uint16_t*)a->w[2];
+    p.b0 = (const uint16_t*)a->bias[0];
+    p.b1 = (const uint16_t*)a->bias[1];
+    p.b2 = (const uint16_t*)a->bias[2];
+    p.n0 = a->seg_rows[0];
+    p.n01 = a->seg_rows[0] + a->seg_rows[1];
+    p.K = a->K;
+    p.N = a->N;
+    p.y = (uint16_t*)a->y;
+    p.ldy = a->ldy;
+    p.norm_w = (const uint16_t*)a->norm_w;
+    p.eps = a->norm_eps;
+    p.numerics = a->numerics;
+    p.M = (int)a->M;
+    p.keys = (unsigned long long*)a->argmax_keys;
+    const int MT = a->M <= 1 ? 1 : a->M <= 2 ? 2 : a->M <= 4 ? 4 : 8;
+    p.xlds = ((size_t)MT * a->K * 2 <= kGemvLdsCap) ? 1 : 0;
+    QIE_REQUIRE(p.xlds || !p.norm_w,
+                "qie_linear: fused RMSNorm needs M*K*2 <= %zu bytes (M=%lld K=%lld)", kGemvLdsCap,
+                (long long)a->M, (long long)a->K);
+    // Rows per wave: 4 while the grid still has >= 2 waves per SIMD of work.
+    const int cus = device_cu_count();
+    const int64_t rows = a->epilogue == QIE_EPI_SWIGLU ? 2 * a->N : a->N;
+    int rpw = env_int("QIE_GEMV_RPW", 0);
+    if (rpw != 2 && rpw != 4) rpw = (rows / 4 / 4 >= (int64_t)cus * 2) ? 4 : 2;
+    p.n_tasks = (rows + rpw - 1) / rpw;
+    const int bpc = std::max(1, env_int("QIE_GEMV_BLOCKS_PER_CU", 4));
+    switch (MT) {
+        case 1: return launch_gemv_m<1>(p, rpw, a->epilogue, st, bpc);
+        case 2: return launch_gemv_m<2>(p, rpw, a->epilogue, st, bpc);
+        case 4: return launch_gemv_m<4>(p, rpw, a->epilogue, st, bpc);
+        default: return launch_gemv_m<8>(p, rpw, a->epilogue, st, bpc);
+    }
+}
+
+}  // namespace qie

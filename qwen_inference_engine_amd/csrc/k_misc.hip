@@ -1,0 +1,448 @@
+// k_misc.hip — error plumbing, embedding gather, row RMSNorm, q/k post-projection
+// (qk-norm + RoPE + KV append), elementwise ops, synthetic weight fill.
+//
+// Reference kernels restated for gfx950 (wave64, 16-byte vector accesses):
+//   embedding_matrix_func  layers/src/embedded_matrix.cu:5-17
+//   rmsNorm                layers/src/normalization.cu:5-25
+//   qkNorm                 layers/src/qk_norm.cu:43-79
+//   RoPE                   layers/src/RoPE.cu:6-22
+//   activation/element_mul layers/src/SiLU.cu:10-23, element_add.cu:4-12
+//   residual_add           layers/src/residual_add.cu:7-18
+//   kv_copy_layer_to_cache_{prefill,decode} layers/src/include_cuda.cu:165-279
+#include "qie_common.hpp"
+#include "../../include/qie/qie_ops.h"
+
+#include <cmath>
+#include <cstdarg>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+namespace qie {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+int fail(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+int device_cu_count() {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (cus[dev] == 0) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
+            cus[dev] = prop.multiProcessorCount;
+        else
+            cus[dev] = 256;
+    }
+    return cus[dev];
+}
+
+// ------------------------------------------------------------ embedding
+// One block per token row, 16-byte copies (the reference copies one bf16 at a
+// time from pinned host memory with one thread per row).
+__global__ __launch_bounds__(256) void embedding_kernel(const uint4* __restrict__ E,
+                                                        const int32_t* __restrict__ ids,
+                                                        uint4* __restrict__ out, int64_t H8) {
+    const int64_t t = blockIdx.x;
+    const int64_t row = ids[t];
+    const uint4* src = E + row * H8;
+    uint4* dst = out + t * H8;
+    for (int64_t i = threadIdx.x; i < H8; i += blockDim.x) dst[i] = src[i];
+}
+
+// ------------------------------------------------------------- RMSNorm
+// Block per row; fp32 sum of squares (wave butterfly + LDS), then
+//   REF: y = bf16((x / sqrtf(ss/H + eps)) * w)          normalization.cu:5-25
+//   HF : y = bf16(w * bf16(x * (1/sqrtf(ss/H + eps))))
+__device__ __forceinline__ float block_sum_256(float v, float* red) {
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) red[wave] = v;
+    __syncthreads();
+    float t = red[0] + red[1] + red[2] + red[3];
+    __syncthreads();
+    return t;
+}
+
+__device__ __forceinline__ uint4 rms_apply8(uint4 xv, uint4 wv, float rms, float inv, int numerics) {
+#pragma clang fp contract(off)
+    uint32_t xs[4] = {xv.x, xv.y, xv.z, xv.w};
+    uint32_t ws[4] = {wv.x, wv.y, wv.z, wv.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        float a0 = bf_lo(xs[j]), a1 = bf_hi(xs[j]);
+        float w0 = bf_lo(ws[j]), w1 = bf_hi(ws[j]);
+        float y0, y1;
+        if (numerics == QIE_NUMERICS_HF) {
+            y0 = w0 * rbf(a0 * inv);
+            y1 = w1 * rbf(a1 * inv);
+        } else {
+            y0 = (a0 / rms) * w0;
+            y1 = (a1 / rms) * w1;
+        }
+        o[j] = pack2(y0, y1);
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+__global__ __launch_bounds__(256) void rmsnorm_kernel(const uint4* __restrict__ x,
+                                                      const uint4* __restrict__ w,
+                                                      uint4* __restrict__ y, int64_t H, float eps,
+                                                      int numerics) {
+    __shared__ float red[4];
+    const int64_t H8 = H / 8;
+    const uint4* xr = x + blockIdx.x * H8;
+    uint4* yr = y + blockIdx.x * H8;
+    float ss = 0.f;
+    for (int64_t i = threadIdx.x; i < H8; i += 256) {
+        uint4 v = xr[i];
+        uint32_t a[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            float l = bf_lo(a[j]), h = bf_hi(a[j]);
+            ss += l * l + h * h;
+        }
+    }
+    ss = block_sum_256(ss, red);
+    const float rms = sqrtf((ss / (float)H) + eps);
+    const float inv = 1.0f / rms;
+    for (int64_t i = threadIdx.x; i < H8; i += 256) yr[i] = rms_apply8(xr[i], w[i], rms, inv, numerics);
+}
+
+// ------------------------------------------- q/k post-projection + KV append
+// Block per row, one wave per head.  Each lane owns one RoPE pair:
+//   REF: (2*lane, 2*lane+1) interleaved (RoPE.cu:12-18)
+//   HF : (lane, lane + hd/2) rotate_half
+// qk-norm (Qwen3 only) is the per-head RMSNorm of qk_norm.cu:43-79.
+struct QkvPostArgs {
+    const uint16_t* qkv;
+    const int32_t* pos;
+    int rows_per_seq;
+    const uint16_t* q_norm;
+    const uint16_t* k_norm;
+    const float* cs;
+    const float* sn;
+    int nq, nkv, hd;
+    uint16_t* kc;
+    uint16_t* vc;
+    int64_t seq_stride;
+    int layer, max_ctx;
+    float eps;
+    int numerics;
+    uint16_t* q_out;
+};
+
+__global__ __launch_bounds__(256) void qkv_post_kernel(QkvPostArgs a) {
+#pragma clang fp contract(off)
+    const int64_t m = blockIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int hd = a.hd, half = hd / 2;
+    const int QD = a.nq * hd, KD = a.nkv * hd;
+    const int ptot = a.nq + 2 * a.nkv;
+    const int p = a.pos[m];
+    const int64_t seq = m / a.rows_per_seq;
+    const uint16_t* row = a.qkv + m * (int64_t)(QD + 2 * KD);
+    const bool hf = a.numerics == QIE_NUMERICS_HF;
+    const bool active = lane < half;
+    const int i0 = hf ? lane : 2 * lane;
+    const int i1 = hf ? lane + half : 2 * lane + 1;
+    const float c = active ? a.cs[(int64_t)p * half + lane] : 0.f;
+    const float s = active ? a.sn[(int64_t)p * half + lane] : 0.f;
+    for (int h = wave; h < ptot; h += 4) {
+        const uint16_t* src;
+        uint16_t* dst;
+        const uint16_t* nw = nullptr;
+        bool rope = true;
+        if (h < a.nq) {
+            src = row + h * hd;
+            dst = a.q_out + m * (int64_t)QD + h * hd;
+            nw = a.q_norm;
+        } else if (h < a.nq + a.nkv) {
+            const int g = h - a.nq;
+            src = row + QD + g * hd;
+            dst = a.kc + seq * a.seq_stride +
+                  (((int64_t)a.layer * a.nkv + g) * a.max_ctx + p) * (int64_t)hd;
+            nw = a.k_norm;
+        } else {
+            const int g = h - a.nq - a.nkv;
+            src = row + QD + KD + g * hd;
+            dst = a.vc + seq * a.seq_stride +
+                  (((int64_t)a.layer * a.nkv + g) * a.max_ctx + p) * (int64_t)hd;
+            rope = false;
+        }
+        float x0 = active ? bf2f(src[i0]) : 0.f;
+        float x1 = active ? bf2f(src[i1]) : 0.f;
+        if (rope && nw) {
+            float ss = wave_sum(x0 * x0 + x1 * x1);
+            float rms = sqrtf((ss / (float)hd) + a.eps);
+            if (hf) {
+                float inv = 1.0f / rms;
+                x0 = rbf(bf2f(nw[i0]) * rbf(x0 * inv));
+                x1 = rbf(bf2f(nw[i1]) * rbf(x1 * inv));
+            } else {
+                x0 = rbf((x0 / rms) * bf2f(nw[i0]));
+                x1 = rbf((x1 / rms) * bf2f(nw[i1]));
+            }
+        }
+        float y0 = x0, y1 = x1;
+        if (rope) {
+            if (hf) {
+                y0 = rbf(rbf(x0 * c) + rbf(-x1 * s));
+                y1 = rbf(rbf(x1 * c) + rbf(x0 * s));
+            } else {
+                y0 = x0 * c - x1 * s;
+                y1 = x1 * c + x0 * s;
+            }
+        }
+        if (active) {
+            if (hf) {
+                dst[i0] = f2bf(y0);
+                dst[i1] = f2bf(y1);
+            } else {
+                reinterpret_cast<uint32_t*>(dst)[lane] = pack2(y0, y1);
+            }
+        }
+    }
+}
+
+// ----------------------------------------------------------- elementwise
+__global__ __launch_bounds__(256) void silu_mul_kernel(const uint4* __restrict__ g,
+                                                       const uint4* __restrict__ u,
+                                                       uint4* __restrict__ h, int64_t n8) {
+#pragma clang fp contract(off)
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+        uint4 gv = g[i], uv = u[i];
+        uint32_t ga[4] = {gv.x, gv.y, gv.z, gv.w}, ua[4] = {uv.x, uv.y, uv.z, uv.w}, o[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            float g0 = bf_lo(ga[j]), g1 = bf_hi(ga[j]);
+            float a0 = rbf(g0 * (1.0f / (1.0f + expf(-g0))));
+            float a1 = rbf(g1 * (1.0f / (1.0f + expf(-g1))));
+            o[j] = pack2(bf_lo(ua[j]) * a0, bf_hi(ua[j]) * a1);
+        }
+        h[i] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+}
+
+__global__ __launch_bounds__(256) void resadd_kernel(uint4* __restrict__ x, const uint4* __restrict__ y,
+                                                     int64_t n8) {
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+        uint4 a = x[i], b = y[i];
+        uint32_t aa[4] = {a.x, a.y, a.z, a.w}, bb[4] = {b.x, b.y, b.z, b.w}, o[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) o[j] = pack2(bf_lo(aa[j]) + bf_lo(bb[j]), bf_hi(aa[j]) + bf_hi(bb[j]));
+        x[i] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+}
+
+// ------------------------------------------------------ synthetic weights
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__host__ __device__ __forceinline__ uint64_t synth_base(uint32_t tensor_id, uint64_t seed) {
+    return splitmix64((seed * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)tensor_id << 32));
+}
+
+__host__ __device__ __forceinline__ float synth_value(uint64_t base, int64_t i, float scale,
+                                                      float offset) {
+    uint64_t r = splitmix64(base + (uint64_t)i);
+    float u = (float)((int32_t)(r >> 40) - 8388608) * (1.0f / 8388608.0f);
+    return offset + u * scale;
+}
+
+__global__ __launch_bounds__(256) void synth_kernel(uint32_t* __restrict__ out, int64_t n2,
+                                                    uint64_t base, float scale, float offset,
+                                                    int64_t n) {
+#pragma clang fp contract(off)
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n2; i += (int64_t)gridDim.x * 256) {
+        float a = synth_value(base, 2 * i, scale, offset);
+        float b = (2 * i + 1 < n) ? synth_value(base, 2 * i + 1, scale, offset) : 0.f;
+        out[i] = pack2(a, b);
+    }
+}
+
+static inline uint16_t host_f2bf(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)0x7fff;
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+
+}  // namespace qie
+
+using namespace qie;
+
+extern "C" {
+
+const char* qie_last_error(void) { return g_last_error.c_str(); }
+int qie_abi_version(void) { return QIE_ABI_VERSION; }
+
+int qie_device_count(int* count) {
+    QIE_HIP(hipGetDeviceCount(count));
+    return 0;
+}
+
+int qie_rope_table_host(float* cos_out, float* sin_out, int32_t n_pos, int32_t head_dim,
+                        float theta, int32_t numerics) {
+    QIE_REQUIRE(cos_out && sin_out && n_pos > 0 && head_dim > 0 && head_dim % 2 == 0,
+                "qie_rope_table_host: bad arguments");
+    const int half = head_dim / 2;
+    if (numerics == QIE_NUMERICS_HF) {
+        for (int i = 0; i < half; i++) {
+            float ex = (float)(2 * i) / (float)head_dim;
+            float inv = 1.0f / powf(theta, ex);
+            for (int p = 0; p < n_pos; p++) {
+                float fr = (float)p * inv;
+                uint32_t cu = (uint32_t)host_f2bf(cosf(fr)) << 16, su = (uint32_t)host_f2bf(sinf(fr)) << 16;
+                std::memcpy(&cos_out[(size_t)p * half + i], &cu, 4);
+                std::memcpy(&sin_out[(size_t)p * half + i], &su, 4);
+            }
+        }
+    } else {
+        // precompute_cos_sin, layers/src/include.cpp:5-16 (float pow, int*float angle).
+        for (int i = 0; i < half; i++) {
+            float exponent = 2 * ((float)i / (float)head_dim);
+            float th = std::pow(theta, -exponent);
+            for (int p = 0; p < n_pos; p++) {
+                cos_out[(size_t)p * half + i] = cosf(p * th);
+                sin_out[(size_t)p * half + i] = sinf(p * th);
+            }
+        }
+    }
+    return 0;
+}
+
+int qie_embedding(const void* E, const int32_t* ids, void* out, int64_t n, int64_t H, void* stream) {
+    QIE_REQUIRE(E && ids && out && n >= 0 && H > 0 && H % 8 == 0, "qie_embedding: bad arguments");
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(embedding_kernel, dim3((unsigned)n), dim3(256), 0, (hipStream_t)stream,
+                       (const uint4*)E, ids, (uint4*)out, H / 8);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+
+int qie_rmsnorm(const void* x, const void* w, void* y, int64_t rows, int64_t H, float eps,
+                int32_t numerics, void* stream) {
+    QIE_REQUIRE(x && w && y && rows >= 0 && H > 0 && H % 8 == 0 && x != y,
+                "qie_rmsnorm: bad arguments");
+    if (rows == 0) return 0;
+    hipLaunchKernelGGL(rmsnorm_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream,
+                       (const uint4*)x, (const uint4*)w, (uint4*)y, H, eps, numerics);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+
+int qie_qkv_post(const void* qkv, int64_t M, const int32_t* pos, int32_t rows_per_seq,
+                 const void* q_norm, const void* k_norm, const float* rope_cos,
+                 const float* rope_sin, int32_t n_heads, const qie_kv_cache* cache, int32_t layer,
+                 float eps, int32_t numerics, void* q_out, void* stream) {
+    QIE_REQUIRE(qkv && pos && cache && cache->k && cache->v && rope_cos && rope_sin && q_out &&
+                    M >= 0 && rows_per_seq > 0 && n_heads > 0 && cache->n_kv_heads > 0 &&
+                    n_heads % cache->n_kv_heads == 0 && layer >= 0 && layer < cache->n_layers,
+                "qie_qkv_post: bad arguments");
+    QIE_REQUIRE(cache->head_dim % 2 == 0 && cache->head_dim <= 128,
+                "qie_qkv_post: head_dim must be even and <= 128");
+    if (M == 0) return 0;
+    QkvPostArgs a;
+    a.qkv = (const uint16_t*)qkv;
+    a.pos = pos;
+    a.rows_per_seq = rows_per_seq;
+    a.q_norm = (const uint16_t*)q_norm;
+    a.k_norm = (const uint16_t*)k_norm;
+    a.cs = rope_cos;
+    a.sn = rope_sin;
+    a.nq = n_heads;
+    a.nkv = cache->n_kv_heads;
+    a.hd = cache->head_dim;
+    a.kc = (uint16_t*)cache->k;
+    a.vc = (uint16_t*)cache->v;
+    a.seq_stride = cache->seq_stride;
+    a.layer = layer;
+    a.max_ctx = cache->max_ctx;
+    a.eps = eps;
+    a.numerics = numerics;
+    a.q_out = (uint16_t*)q_out;
+    hipLaunchKernelGGL(qkv_post_kernel, dim3((unsigned)M), dim3(256), 0, (hipStream_t)stream, a);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+
+int qie_silu_mul(const void* gate, const void* up, void* h, int64_t n, void* stream) {
+    QIE_REQUIRE(gate && up && h && n >= 0 && n % 8 == 0, "qie_silu_mul: bad arguments");
+    if (n == 0) return 0;
+    int64_t n8 = n / 8;
+    unsigned grid = (unsigned)std::min<int64_t>((n8 + 255) / 256, 8192);
+    hipLaunchKernelGGL(silu_mul_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       (const uint4*)gate, (const uint4*)up, (uint4*)h, n8);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+
+int qie_residual_add(void* x, const void* y, int64_t n, void* stream) {
+    QIE_REQUIRE(x && y && n >= 0 && n % 8 == 0, "qie_residual_add: bad arguments");
+    if (n == 0) return 0;
+    int64_t n8 = n / 8;
+    unsigned grid = (unsigned)std::min<int64_t>((n8 + 255) / 256, 8192);
+    hipLaunchKernelGGL(resadd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (uint4*)x,
+                       (const uint4*)y, n8);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+
+uint32_t qie_tensor_id(const char* name) {
+    uint32_t h = 2166136261u;
+    for (const unsigned char* p = (const unsigned char*)name; *p; ++p) {
+        h ^= *p;
+        h *= 16777619u;
+    }
+    return h;
+}
+
+int qie_synthetic_fill(void* dev, int64_t n, uint32_t tensor_id, uint64_t seed, float scale,
+                       float offset, void* stream) {
+    QIE_REQUIRE(dev && n >= 0 && ((uintptr_t)dev % 4) == 0, "qie_synthetic_fill: bad arguments");
+    if (n == 0) return 0;
+    QIE_REQUIRE(n % 2 == 0, "qie_synthetic_fill: n must be even");
+    int64_t n2 = n / 2;
+    unsigned grid = (unsigned)std::min<int64_t>((n2 + 255) / 256, 16384);
+    hipLaunchKernelGGL(synth_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (uint32_t*)dev,
+                       n2, synth_base(tensor_id, seed), scale, offset, n);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+
+int qie_synthetic_fill_host(void* host, int64_t n, uint32_t tensor_id, uint64_t seed, float scale,
+                            float offset) {
+    QIE_REQUIRE(host && n >= 0, "qie_synthetic_fill_host: bad arguments");
+    uint16_t* out = (uint16_t*)host;
+    const uint64_t base = synth_base(tensor_id, seed);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; i++) {
+#pragma clang fp contract(off)
+        out[i] = host_f2bf(synth_value(base, i, scale, offset));
+    }
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,185 @@
+"""Python host mirror of the reference driver, over libqie.so's C ABI.
+
+Reference driver (layers/src/iengine.cu:226-456, qwen_main.cu:64-417):
+``create_new_sequence`` -> ``llm()`` with ``state == prefill`` -> loop ``llm()`` with
+``state == decode`` (one token per call).  Here: ``Engine`` (weights + RoPE tables),
+``Batch`` (KV cache + per-sequence state for B sequences), ``Batch.prefill`` and
+``Batch.decode_step`` / ``Batch.decode`` (hipGraph replays).  All compute runs in
+libqie's HIP kernels; there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import dataclasses
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from .spec import ModelSpec
+from .weights import SynthParams
+
+REF_PREFILL_SAMPLING = dict(top_k=50, temperature=1.0, seed=1234)   # qwen_main.cu:241
+REF_DECODE_SAMPLING = dict(top_k=50, temperature=0.7, seed=1234)    # qwen_main.cu:381-388 (+ step)
+REF_EOS = 151645                                                    # qwen_main.cu:257
+
+
+@dataclasses.dataclass
+class Sampling:
+    top_k: int = 1
+    temperature: float = 1.0
+    top_p: float = 1.0
+    seed: int = 1234
+
+    def to_c(self) -> _lib.SamplingC:
+        s = _lib.SamplingC()
+        s.top_k, s.temperature, s.top_p, s.seed = self.top_k, self.temperature, self.top_p, self.seed
+        return s
+
+
+GREEDY = Sampling()
+
+_ROLE_FIELDS = {
+    "input_layernorm.weight": "attn_norm", "self_attn.q_proj.weight": "wq",
+    "self_attn.k_proj.weight": "wk", "self_attn.v_proj.weight": "wv",
+    "self_attn.q_proj.bias": "bq", "self_attn.k_proj.bias": "bk", "self_attn.v_proj.bias": "bv",
+    "self_attn.q_norm.weight": "q_norm", "self_attn.k_norm.weight": "k_norm",
+    "self_attn.o_proj.weight": "wo", "post_attention_layernorm.weight": "ffn_norm",
+    "mlp.gate_proj.weight": "w_gate", "mlp.up_proj.weight": "w_up", "mlp.down_proj.weight": "w_down",
+}
+
+
+def weights_struct(spec: ModelSpec, ptr: Dict[str, int]):
+    """Build a qie_model_weights from {full tensor name: pointer}.  Returns (struct, keepalive)."""
+    layers = (_lib.LayerWeightsC * spec.n_layers)()
+    for l in range(spec.n_layers):
+        for short, field in _ROLE_FIELDS.items():
+            setattr(layers[l], field, ptr.get(f"model.layers.{l}.{short}"))
+    w = _lib.ModelWeightsC()
+    w.embed = ptr["model.embed_tokens.weight"]
+    w.final_norm = ptr["model.norm.weight"]
+    w.lm_head = ptr["model.embed_tokens.weight"] if spec.tie_embeddings else ptr["lm_head.weight"]
+    w.n_layers = spec.n_layers
+    w.layers = C.cast(layers, C.POINTER(_lib.LayerWeightsC))
+    return w, layers
+
+
+class Engine:
+    def __init__(self, spec: ModelSpec, device: int = 0, max_ctx: int = 4096, use_graph: bool = True):
+        self.lib = _lib.load()
+        self.spec = spec
+        self._spec_c = spec.to_c()
+        opts = _lib.EngineOptsC()
+        opts.device, opts.max_ctx, opts.use_graph = device, max_ctx, int(use_graph)
+        opts.tp_rank, opts.tp_size = 0, 1
+        h = C.c_void_p()
+        _lib.check(self.lib.qie_engine_create(C.byref(self._spec_c), C.byref(opts), C.byref(h)),
+                   "qie_engine_create")
+        self.h = h
+        self.max_ctx = max_ctx
+        self._keep = None
+
+    def init_synthetic(self, p: SynthParams = SynthParams()) -> "Engine":
+        _lib.check(self.lib.qie_engine_init_synthetic(self.h, p.seed, p.w_scale, p.norm_scale, p.bias_scale),
+                   "qie_engine_init_synthetic")
+        return self
+
+    def load_weights_bin(self, bin_path: str, meta_path: str, chunk_bytes: int = 1 << 28) -> "Engine":
+        _lib.check(self.lib.qie_engine_load_weights_bin(self.h, bin_path.encode(), meta_path.encode(),
+                                                        chunk_bytes), "qie_engine_load_weights_bin")
+        return self
+
+    def set_weights(self, dev_ptrs: Dict[str, int], keepalive=None) -> "Engine":
+        w, layers = weights_struct(self.spec, dev_ptrs)
+        _lib.check(self.lib.qie_engine_set_weights(self.h, C.byref(w)), "qie_engine_set_weights")
+        self._keep = (w, layers, keepalive)
+        return self
+
+    @property
+    def stream(self) -> int:
+        return self.lib.qie_engine_stream(self.h)
+
+    def sync(self) -> None:
+        _lib.check(self.lib.qie_engine_sync(self.h), "qie_engine_sync")
+
+    def batch(self, batch: int = 1, max_ctx: Optional[int] = None) -> "Batch":
+        return Batch(self, batch, max_ctx or self.max_ctx)
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            self.lib.qie_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Batch:
+    def __init__(self, engine: Engine, batch: int, max_ctx: int):
+        self.e = engine
+        self.lib = engine.lib
+        self.B = batch
+        self.max_ctx = max_ctx
+        h = C.c_void_p()
+        _lib.check(self.lib.qie_batch_create(engine.h, batch, max_ctx, C.byref(h)), "qie_batch_create")
+        self.h = h
+
+    def prefill(self, seq: int, ids: Sequence[int], sampling: Sampling = GREEDY) -> int:
+        arr = (C.c_int32 * len(ids))(*[int(i) for i in ids])
+        out = C.c_int32(-1)
+        sc = sampling.to_c()
+        _lib.check(self.lib.qie_prefill(self.h, seq, arr, len(ids), C.byref(sc), C.byref(out)), "qie_prefill")
+        return out.value
+
+    def decode_step(self, sampling: Sampling = GREEDY) -> List[int]:
+        out = (C.c_int32 * self.B)()
+        sc = sampling.to_c()
+        _lib.check(self.lib.qie_decode_step(self.h, C.byref(sc), out), "qie_decode_step")
+        return list(out)
+
+    def decode(self, n_steps: int, sampling: Sampling = GREEDY, want_ids: bool = True) -> Optional[np.ndarray]:
+        out = np.zeros((max(n_steps, 1), self.B), dtype=np.int32)
+        sc = sampling.to_c()
+        ptr = out.ctypes.data_as(C.POINTER(C.c_int32)) if want_ids else None
+        _lib.check(self.lib.qie_decode(self.h, n_steps, C.byref(sc), ptr), "qie_decode")
+        return out[:n_steps] if want_ids else None
+
+    def logits(self) -> np.ndarray:
+        out = np.zeros((self.B, self.e.spec.vocab), dtype=np.uint16)
+        _lib.check(self.lib.qie_batch_logits(self.h, out.ctypes.data), "qie_batch_logits")
+        return out
+
+    def positions(self) -> np.ndarray:
+        out = np.zeros(self.B, dtype=np.int32)
+        _lib.check(self.lib.qie_batch_positions(self.h, out.ctypes.data_as(C.POINTER(C.c_int32))),
+                   "qie_batch_positions")
+        return out
+
+    def history(self, seq: int, n: int) -> np.ndarray:
+        out = np.zeros(n, dtype=np.int32)
+        _lib.check(self.lib.qie_batch_history(self.h, seq, out.ctypes.data_as(C.POINTER(C.c_int32)), n),
+                   "qie_batch_history")
+        return out
+
+    def set_position(self, seq: int, pos: int, token: int) -> None:
+        _lib.check(self.lib.qie_batch_set_position(self.h, seq, pos, token), "qie_batch_set_position")
+
+    def time_kernel(self, which: int = 0, iters: int = 20):
+        us, by = C.c_double(), C.c_double()
+        _lib.check(self.lib.qie_batch_time_kernel(self.h, which, iters, C.byref(us), C.byref(by)),
+                   "qie_batch_time_kernel")
+        return us.value, by.value
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            self.lib.qie_batch_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,152 @@
+"""GPU end-to-end parity: the libqie engine (prefill + hipGraph decode) against the CPU
+oracle's full forward on identical synthetic weights and prompts.
+
+Bar: greedy token ids identical to the oracle's; per-step bf16 logits within a few bf16
+ulps of the oracle's (different fp32 summation orders inside the dot products); engine
+invariants (graph == eager, batch == single, weights.bin == synthetic init, rewind) are
+bit-exact.
+"""
+import numpy as np
+import pytest
+
+import gpu_util as G
+from conftest import rng
+
+import qwen_inference_engine_amd as Q
+from qwen_inference_engine_amd import spec as S, weights as W
+
+pytestmark = pytest.mark.gpu
+
+CONFIGS = {
+    "qwen2-bias-hd64": S.tiny("t-q2", n_layers=3, hidden=256, n_heads=4, n_kv_heads=2, head_dim=64, ffn=512,
+                              vocab=1000, bias=True),
+    "qwen3-qknorm-hd128": S.tiny("t-q3", n_layers=2, hidden=512, n_heads=8, n_kv_heads=2, head_dim=128, ffn=768,
+                                 vocab=1536, bias=False, qk_norm=True),
+    "tied-g7": S.tiny("t-tied", n_layers=2, hidden=448, n_heads=7, n_kv_heads=1, head_dim=64, ffn=640,
+                      vocab=777 * 2, tie=True, bias=True),
+}
+SYN = W.SynthParams(seed=11, w_scale=0.08, norm_scale=0.25, bias_scale=0.05)
+
+
+def make_pair(spec, oracle, max_ctx=128, use_graph=True, syn=SYN):
+    eng = Q.Engine(spec, max_ctx=max_ctx, use_graph=use_graph).init_synthetic(syn)
+    hw = W.HostWeights.synthetic(spec, syn)
+    return eng, hw, oracle.Model(hw, max_ctx)
+
+
+def logits_close(got, want, what=""):
+    g, w = G.bf(got).astype(np.float64), G.bf(want).astype(np.float64)
+    tol = 4 * 2.0 ** -7 * max(1.0, np.abs(w).max())
+    assert np.abs(g - w).max() <= tol, f"{what}: max |dlogit| {np.abs(g - w).max()} > {tol}"
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+@pytest.mark.parametrize("num", ["ref", "hf"])
+@pytest.mark.parametrize("P", [5, 23])
+def test_greedy_generation_matches_oracle(oracle, name, num, P):
+    spec = CONFIGS[name].with_numerics(num)
+    eng, hw, om = make_pair(spec, oracle)
+    prompt = list(rng(P).integers(0, spec.vocab, P))
+    n_new = 12
+    want_ids, want_lg = om.generate_greedy(prompt, n_new)
+    b = eng.batch(1, 128)
+    first = b.prefill(0, prompt)
+    logits_close(b.logits()[0], want_lg[0], "prefill")
+    got = [first]
+    for i in range(1, n_new):
+        got.append(b.decode_step()[0])
+        logits_close(b.logits()[0], want_lg[i], f"step {i}")
+    assert got == want_ids
+
+
+def test_graph_equals_eager_and_batch_equals_single(oracle):
+    spec = CONFIGS["qwen2-bias-hd64"]
+    prompts = [list(rng(i).integers(0, spec.vocab, n)) for i, n in enumerate([7, 19, 3])]
+    outs = {}
+    for graph in (True, False):
+        eng = Q.Engine(spec, max_ctx=96, use_graph=graph).init_synthetic(SYN)
+        singles = []
+        for pr in prompts:
+            b = eng.batch(1, 96)
+            t0 = b.prefill(0, pr)
+            singles.append([t0] + list(b.decode(10)[:, 0]))
+        b3 = eng.batch(3, 96)
+        firsts = [b3.prefill(i, pr) for i, pr in enumerate(prompts)]
+        rest = b3.decode(10)
+        multi = [[firsts[i]] + list(rest[:, i]) for i in range(3)]
+        assert multi == singles
+        outs[graph] = singles
+    assert outs[True] == outs[False]
+
+
+def test_weights_bin_loader_equals_synthetic(oracle, tmp_path):
+    spec = CONFIGS["qwen3-qknorm-hd128"]
+    hw = W.HostWeights.synthetic(spec, SYN)
+    hw.write_weights_bin(str(tmp_path / "weights.bin"), str(tmp_path / "meta_data.txt"))
+    prompt = [1, 2, 3, 4, 5, 6, 7, 8, 9]
+    e1 = Q.Engine(spec, max_ctx=64).init_synthetic(SYN)
+    e2 = Q.Engine(spec, max_ctx=64).load_weights_bin(str(tmp_path / "weights.bin"), str(tmp_path / "meta_data.txt"),
+                                                     chunk_bytes=1 << 16)
+    r = []
+    for e in (e1, e2):
+        b = e.batch(1, 64)
+        r.append([b.prefill(0, prompt)] + list(b.decode(8)[:, 0]))
+    assert r[0] == r[1]
+
+
+def test_set_weights_from_device_tensors(oracle):
+    spec = CONFIGS["tied-g7"]
+    hw = W.HostWeights.synthetic(spec, SYN)
+    dev = {n: G.dev(a) for n, a in hw.tensors.items()}
+    e = Q.Engine(spec, max_ctx=64).set_weights({n: t.data_ptr() for n, t in dev.items()}, keepalive=dev)
+    om = oracle.Model(hw, 64)
+    want, _ = om.generate_greedy([5, 4, 3, 2, 1], 8)
+    b = e.batch(1, 64)
+    assert [b.prefill(0, [5, 4, 3, 2, 1])] + list(b.decode(7)[:, 0]) == want
+
+
+def test_rewind_reproduces(oracle):
+    spec = CONFIGS["qwen2-bias-hd64"]
+    e = Q.Engine(spec, max_ctx=64).init_synthetic(SYN)
+    b = e.batch(1, 64)
+    prompt = [9, 8, 7, 6, 5, 4]
+    t0 = b.prefill(0, prompt)
+    a = list(b.decode(10)[:, 0])
+    b.set_position(0, len(prompt), t0)
+    assert list(b.decode(10)[:, 0]) == a
+    hist = b.history(0, len(prompt) + 11)
+    assert list(hist[:len(prompt)]) == prompt and hist[len(prompt)] == t0 and list(hist[len(prompt) + 1:]) == a
+
+
+def test_topk_sampling_matches_oracle(oracle):
+    """Reference sampling schedule: prefill (k=50, T=1.0, seed 1234), decode step s
+    (k=50, T=0.7, seed 1234+s) — qwen_main.cu:241, 381-388."""
+    spec = CONFIGS["qwen2-bias-hd64"]
+    eng, hw, om = make_pair(spec, oracle)
+    prompt = [11, 22, 33, 44, 55, 66, 77]
+    b = eng.batch(1, 128)
+    got = [b.prefill(0, prompt, Q.Sampling(top_k=50, temperature=1.0, seed=1234))]
+    lg = om.forward(prompt, 0)
+    want = [oracle.sample(lg, 50, 1.0, 1.0, 1234)]
+    for s in range(1, 10):
+        got.append(b.decode_step(Q.Sampling(top_k=50, temperature=0.7, seed=1234))[0])
+        lg = om.forward([want[-1]])
+        want.append(oracle.sample(lg, 50, 0.7, 1.0, 1234 + s))
+        assert got == want
+
+
+@pytest.mark.slow
+def test_qwen2_0_5b_config1_greedy_matches_oracle(oracle):
+    """BASELINE config 1 shape (Qwen2-0.5B, prompt 16, gen 16, greedy) at full size."""
+    spec = S.QWEN2_0_5B
+    syn = W.SynthParams(seed=0)
+    eng, hw, om = make_pair(spec, oracle, max_ctx=64, syn=syn)
+    prompt = list(rng(1).integers(0, spec.vocab, 16))
+    want, want_lg = om.generate_greedy(prompt, 16)
+    b = eng.batch(1, 64)
+    got = [b.prefill(0, prompt)]
+    logits_close(b.logits()[0], want_lg[0], "prefill")
+    for i in range(1, 16):
+        got.append(b.decode_step()[0])
+        logits_close(b.logits()[0], want_lg[i], f"step {i}")
+    assert got == want

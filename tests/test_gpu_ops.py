@@ -1,0 +1,300 @@
+"""GPU parity: every libqie op (C ABI) against the CPU oracle on identical bf16 inputs.
+
+Tolerances (written per test): bit-exact for copies, selection and the elementwise ops
+whose arithmetic is restated without contraction; <= 1 bf16 ulp (>= 98 % exact) where
+only an fp32 summation order differs (RMSNorm, qk-norm); for dot products
+|got - want| <= max(1 bf16 ulp, 1e-5 * sum|a*w|) (accumulation order of K terms).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import gpu_util as G
+from conftest import rng
+
+from qwen_inference_engine_amd import _lib
+from qwen_inference_engine_amd._lib import LinearArgsC, KvCacheC, SamplingC
+
+pytestmark = pytest.mark.gpu
+
+
+def rand_bf16(oracle, shape, scale=1.0, seed=0):
+    return oracle.f32_to_bf16((rng(seed).standard_normal(shape) * scale).astype(np.float32))
+
+
+# ------------------------------------------------------------------------ embedding
+def test_embedding_exact(oracle, qlib):
+    E = rand_bf16(oracle, (1000, 256), seed=1)
+    ids = np.array([0, 999, 5, 5, 123, 999, 0], np.int32)
+    out = G.zeros_bf16(len(ids), 256)
+    dE, dI = G.dev(E), G.dev(ids)
+    G.check(qlib.qie_embedding(G.p(dE), G.p(dI), G.p(out), len(ids), 256, None))
+    assert np.array_equal(G.host_bf16(out), E[ids])
+
+
+# -------------------------------------------------------------------------- RMSNorm
+@pytest.mark.parametrize("rows,H", [(1, 128), (3, 896), (17, 3584), (2, 8192)])
+@pytest.mark.parametrize("num", ["ref", "hf"])
+def test_rmsnorm(oracle, qlib, rows, H, num):
+    x = rand_bf16(oracle, (rows, H), seed=rows + H)
+    w = oracle.f32_to_bf16((1 + 0.2 * rng(7).standard_normal(H)).astype(np.float32))
+    eps = 1e-4 if num == "ref" else 1e-6
+    want = oracle.rmsnorm(x, w, eps, num)
+    y = G.zeros_bf16(rows, H)
+    dx, dw = G.dev(x), G.dev(w)
+    G.check(qlib.qie_rmsnorm(G.p(dx), G.p(dw), G.p(y), rows, H, eps, 0 if num == "ref" else 1, None))
+    G.assert_bf16_close(G.host_bf16(y), want, max_ulp=1, min_exact=0.98, what="rmsnorm")
+
+
+# --------------------------------------------------------------------------- linear
+def _linear(qlib, x, segs, biases, M, K, N, y, epi, norm_w=None, eps=1e-4, num=0, keys=None, ldy=None):
+    a = LinearArgsC()
+    a.x, a.ldx = G.p(x), K
+    for i, s in enumerate(segs):
+        a.w[i] = G.p(s[0])
+        a.seg_rows[i] = s[1]
+    for i, b in enumerate(biases):
+        a.bias[i] = G.p(b) if b is not None else None
+    a.M, a.K, a.N = M, K, N
+    a.y, a.ldy = G.p(y), ldy or N
+    a.epilogue = epi
+    a.norm_w = G.p(norm_w) if norm_w is not None else None
+    a.norm_eps, a.numerics = eps, num
+    a.argmax_keys = G.p(keys) if keys is not None else None
+    G.check(qlib.qie_linear(C.byref(a), None), "qie_linear")
+
+
+def _abs_scale(oracle, x, w):
+    return np.abs(oracle.bf16_to_f32(x).astype(np.float64)) @ np.abs(oracle.bf16_to_f32(w).astype(np.float64)).T
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 5, 8, 9, 64, 130, 300])
+@pytest.mark.parametrize("K,n", [(128, (64, 32, 32)), (896, (896, 128, 128)), (3584, (512, 128, 128)),
+                                 (3696, (200, 8, 48))])
+def test_linear_store_bias_3seg(oracle, qlib, M, K, n):
+    if M > 64 and K > 1000:
+        pytest.skip("covered at smaller M")
+    x = rand_bf16(oracle, (M, K), seed=M)
+    ws = [rand_bf16(oracle, (r, K), 0.05, seed=10 + i) for i, r in enumerate(n)]
+    bs = [rand_bf16(oracle, (r,), 0.1, seed=20 + i) for i, r in enumerate(n)]
+    N = sum(n)
+    want = np.concatenate([oracle.matmul(x, w, b) for w, b in zip(ws, bs)], axis=1)
+    dws, dbs = [G.dev(w) for w in ws], [G.dev(b) for b in bs]
+    y = G.zeros_bf16(M, N)
+    _linear(qlib, G.dev(x), list(zip(dws, n)), dbs, M, K, N, y, _lib.QIE_EPI_STORE)
+    scale = np.concatenate([_abs_scale(oracle, x, w) for w in ws], axis=1)
+    G.assert_sum_close(G.host_bf16(y), want, scale, what=f"linear M={M} K={K}")
+
+
+@pytest.mark.parametrize("M", [1, 4, 8, 33, 256])
+@pytest.mark.parametrize("K,N", [(896, 896), (4864, 896), (1024, 8192), (18944, 3584)])
+def test_linear_residual(oracle, qlib, M, K, N):
+    if M * K * N > 256 * 4864 * 896 * 2:
+        pytest.skip("oracle time")
+    x = rand_bf16(oracle, (M, K), seed=3)
+    w = rand_bf16(oracle, (N, K), 0.02, seed=4)
+    res = rand_bf16(oracle, (M, N), seed=5)
+    want = oracle.resadd(res, oracle.matmul(x, w))
+    y = G.dev(res)
+    _linear(qlib, G.dev(x), [(G.dev(w), N)], [], M, K, N, y, _lib.QIE_EPI_RESIDUAL)
+    got = G.host_bf16(y)
+    # residual adds one more rounding on top of the bf16(acc) that may differ by 1 ulp
+    d = G.ulp_diff(got, want)
+    assert (d <= 1).mean() > 0.995 and d.max() <= 2, f"max {d.max()}"
+
+
+@pytest.mark.parametrize("M", [1, 2, 8, 17, 128])
+@pytest.mark.parametrize("K,I", [(128, 256), (896, 4864), (3584, 640)])
+def test_linear_swiglu(oracle, qlib, M, K, I):
+    x = rand_bf16(oracle, (M, K), seed=6)
+    wg = rand_bf16(oracle, (I, K), 0.08, seed=7)
+    wu = rand_bf16(oracle, (I, K), 0.08, seed=8)
+    want = oracle.silu_mul(oracle.matmul(x, wg), oracle.matmul(x, wu))
+    y = G.zeros_bf16(M, I)
+    _linear(qlib, G.dev(x), [(G.dev(wg), I), (G.dev(wu), I)], [], M, K, I, y, _lib.QIE_EPI_SWIGLU)
+    got = G.host_bf16(y)
+    d = G.ulp_diff(got, want)
+    assert (d == 0).mean() > 0.97 and d.max() <= 3, f"max {d.max()}"
+
+
+@pytest.mark.parametrize("M", [1, 3, 8])
+@pytest.mark.parametrize("num", ["ref", "hf"])
+def test_linear_fused_norm_and_argmax(oracle, qlib, M, num):
+    K, N = 896, 5000
+    x = rand_bf16(oracle, (M, K), seed=11)
+    nw = oracle.f32_to_bf16((1 + 0.2 * rng(12).standard_normal(K)).astype(np.float32))
+    w = rand_bf16(oracle, (N, K), 0.05, seed=13)
+    eps = 1e-4 if num == "ref" else 1e-6
+    xn = oracle.rmsnorm(x, nw, eps, num)
+    want = oracle.matmul(xn, w)
+    y = G.zeros_bf16(M, N)
+    keys = G.dev(np.zeros(M, np.uint64))
+    _linear(qlib, G.dev(x), [(G.dev(w), N)], [], M, K, N, y, _lib.QIE_EPI_STORE, norm_w=G.dev(nw), eps=eps,
+            num=0 if num == "ref" else 1, keys=keys)
+    got = G.host_bf16(y)
+    G.assert_sum_close(got, want, _abs_scale(oracle, xn, w) * 2, rel=2e-5, what="fused norm")
+    ids = G.torch().zeros(M, dtype=G.torch().int32, device="cuda")
+    G.check(qlib.qie_keys_to_ids(G.p(keys), M, G.p(ids), None))
+    for m in range(M):   # fused arg-max == reference rule on the kernel's own logits
+        assert G.host(ids)[m] == oracle.argmax(got[m])
+
+
+# -------------------------------------------------------------------- q/k post + KV
+def _cache(kc, vc, L, nkv, hd, ctx, seq_stride):
+    c = KvCacheC()
+    c.k, c.v, c.seq_stride = G.p(kc), G.p(vc), seq_stride
+    c.n_layers, c.n_kv_heads, c.head_dim, c.max_ctx = L, nkv, hd, ctx
+    return c
+
+
+@pytest.mark.parametrize("hd", [64, 128])
+@pytest.mark.parametrize("qkn", [False, True])
+@pytest.mark.parametrize("num", ["ref", "hf"])
+@pytest.mark.parametrize("mode", ["prefill", "decode"])
+def test_qkv_post(oracle, qlib, hd, qkn, num, mode):
+    nq, nkv, L, ctx, layer = 6, 2, 3, 40, 1
+    QD, KD = nq * hd, nkv * hd
+    if mode == "prefill":
+        M, rps = 9, 9
+        pos = np.arange(3, 3 + M, dtype=np.int32)
+    else:
+        M, rps = 3, 1
+        pos = np.array([5, 0, 39], np.int32)
+    qkv = rand_bf16(oracle, (M, QD + 2 * KD), seed=hd + M)
+    qn = oracle.f32_to_bf16((1 + 0.3 * rng(1).standard_normal(hd)).astype(np.float32)) if qkn else None
+    kn = oracle.f32_to_bf16((1 + 0.3 * rng(2).standard_normal(hd)).astype(np.float32)) if qkn else None
+    eps = 1e-4 if num == "ref" else 1e-6
+    cs, sn = oracle.rope_table(ctx, hd, 1e6, num)
+    q = qkv[:, :QD].copy()
+    k = qkv[:, QD:QD + KD].copy()
+    v = qkv[:, QD + KD:].copy()
+    if qkn:
+        q = oracle.qknorm(q, qn, nq, hd, eps, num)
+        k = oracle.qknorm(k, kn, nkv, hd, eps, num)
+    q = oracle.rope(q, cs, sn, pos, nq, hd, num)
+    k = oracle.rope(k, cs, sn, pos, nkv, hd, num)
+    nseq = M // rps
+    seq_stride = L * nkv * ctx * hd
+    kc = G.zeros_bf16(nseq * seq_stride)
+    vc = G.zeros_bf16(nseq * seq_stride)
+    qo = G.zeros_bf16(M, QD)
+    c = _cache(kc, vc, L, nkv, hd, ctx, seq_stride)
+    dcs, dsn = G.dev(cs), G.dev(sn)
+    dqn = G.dev(qn) if qkn else None
+    dkn = G.dev(kn) if qkn else None
+    G.check(qlib.qie_qkv_post(G.p(G.dev(qkv)), M, G.p(G.dev(pos)), rps, G.p(dqn) if qkn else None,
+                              G.p(dkn) if qkn else None, G.p(dcs), G.p(dsn), nq, C.byref(c), layer, eps,
+                              0 if num == "ref" else 1, G.p(qo), None))
+    G.assert_bf16_close(G.host_bf16(qo), q, max_ulp=1, min_exact=0.98 if qkn else 1.0, what="q")
+    hk = G.host_bf16(kc).reshape(nseq, L, nkv, ctx, hd)
+    hv = G.host_bf16(vc).reshape(nseq, L, nkv, ctx, hd)
+    for m in range(M):
+        s = m // rps
+        for g in range(nkv):
+            G.assert_bf16_close(hk[s, layer, g, pos[m]], k[m, g * hd:(g + 1) * hd], 1,
+                                0.9 if qkn else 1.0, "k")
+            assert np.array_equal(hv[s, layer, g, pos[m]], v[m, g * hd:(g + 1) * hd])
+    # nothing else written
+    mask = np.zeros_like(hk, bool)
+    for m in range(M):
+        mask[m // rps, layer, :, pos[m]] = True
+    assert not hk[~mask].any() and not hv[~mask].any()
+
+
+# ----------------------------------------------------------------------- attention
+@pytest.mark.parametrize("hd", [64, 128])
+@pytest.mark.parametrize("nq,nkv", [(4, 4), (14, 2), (28, 4), (16, 2)])
+@pytest.mark.parametrize("ctxs", [[1], [5, 64, 65], [1000], [2049, 3]])
+def test_attention_decode(oracle, qlib, hd, nq, nkv, ctxs):
+    L, layer, maxc = 2, 1, 2304
+    B = len(ctxs)
+    seq_stride = L * nkv * maxc * hd
+    kc_h = rand_bf16(oracle, (B, L, nkv, maxc, hd), seed=hd + nq)
+    vc_h = rand_bf16(oracle, (B, L, nkv, maxc, hd), seed=hd + nq + 1)
+    q = rand_bf16(oracle, (B, nq * hd), seed=3)
+    pos = np.array(ctxs, np.int32) - 1
+    ws_bytes = qlib.qie_attention_workspace_bytes(B, nq, hd, maxc)
+    ws = G.torch().zeros(max(ws_bytes, 16), dtype=G.torch().uint8, device="cuda")
+    kc, vc = G.dev(kc_h), G.dev(vc_h)
+    out = G.zeros_bf16(B, nq * hd)
+    c = _cache(kc, vc, L, nkv, hd, maxc, seq_stride)
+    G.check(qlib.qie_attention(G.p(G.dev(q)), B, G.p(G.dev(pos)), 1, C.byref(c), layer, nq, G.p(out), G.p(ws), None))
+    got = G.host_bf16(out)
+    for b in range(B):
+        want = oracle.attention(q[b:b + 1], kc_h[b, layer, :, :ctxs[b]], vc_h[b, layer, :, :ctxs[b]], nq, nkv, hd,
+                                False, 0)
+        d = np.abs(G.bf(got[b]) - G.bf(want[0]))
+        assert d.max() <= 2 ** -7 * max(1.0, np.abs(G.bf(want[0])).max()) * 2, f"ctx {ctxs[b]}: {d.max()}"
+
+
+@pytest.mark.parametrize("P", [1, 7, 64, 257])
+def test_attention_prefill_causal(oracle, qlib, P):
+    nq, nkv, hd, L, layer, maxc = 14, 2, 64, 1, 0, 512
+    seq_stride = L * nkv * maxc * hd
+    kc_h = rand_bf16(oracle, (1, L, nkv, maxc, hd), seed=P)
+    vc_h = rand_bf16(oracle, (1, L, nkv, maxc, hd), seed=P + 1)
+    q = rand_bf16(oracle, (P, nq * hd), seed=P + 2)
+    pos = np.arange(P, dtype=np.int32)
+    ws_bytes = qlib.qie_attention_workspace_bytes(P, nq, hd, maxc)
+    ws = G.torch().zeros(max(ws_bytes, 16), dtype=G.torch().uint8, device="cuda")
+    kc, vc = G.dev(kc_h), G.dev(vc_h)
+    out = G.zeros_bf16(P, nq * hd)
+    c = _cache(kc, vc, L, nkv, hd, maxc, seq_stride)
+    G.check(qlib.qie_attention(G.p(G.dev(q)), P, G.p(G.dev(pos)), P, C.byref(c), layer, nq, G.p(out), G.p(ws), None))
+    want = oracle.attention(q, kc_h[0, layer, :, :P], vc_h[0, layer, :, :P], nq, nkv, hd, True, 0)
+    d = np.abs(G.bf(G.host_bf16(out)) - G.bf(want))
+    assert d.max() <= 2 ** -6, d.max()
+
+
+# --------------------------------------------------------------------- elementwise
+def test_silu_mul_and_residual(oracle, qlib):
+    n = 8 * 5000
+    g = rand_bf16(oracle, (n,), 3.0, seed=1)
+    u = rand_bf16(oracle, (n,), seed=2)
+    h = G.zeros_bf16(n)
+    G.check(qlib.qie_silu_mul(G.p(G.dev(g)), G.p(G.dev(u)), G.p(h), n, None))
+    G.assert_bf16_close(G.host_bf16(h), oracle.silu_mul(g, u), max_ulp=1, min_exact=0.999, what="silu")
+    x = G.dev(g)
+    G.check(qlib.qie_residual_add(G.p(x), G.p(G.dev(u)), n, None))
+    assert np.array_equal(G.host_bf16(x), oracle.resadd(g, u))
+
+
+# ------------------------------------------------------------------------ sampling
+@pytest.mark.parametrize("V", [1000, 151936, 152064])
+@pytest.mark.parametrize("kind", ["normal", "ties"])
+def test_sampling_greedy_topk_and_draw(oracle, qlib, V, kind):
+    M = 3
+    r = rng(V)
+    if kind == "ties":
+        lg = oracle.f32_to_bf16(r.integers(0, 6, (M, V)).astype(np.float32))
+    else:
+        lg = oracle.f32_to_bf16((r.standard_normal((M, V)) * 3).astype(np.float32))
+    dl = G.dev(lg)
+    ws = G.torch().zeros(qlib.qie_sample_workspace_bytes(M, V), dtype=G.torch().uint8, device="cuda")
+    ids = G.torch().zeros(M, dtype=G.torch().int32, device="cuda")
+    step = G.dev(np.array([0, 1, 7], np.int32))
+    for k, T, tp in [(1, 1.0, 1.0), (50, 0.7, 1.0), (50, 1.0, 1.0), (5, 1.3, 1.0), (256, 0.9, 1.0), (50, 0.8, 0.9)]:
+        s = SamplingC()
+        s.top_k, s.temperature, s.top_p, s.seed = k, T, tp, 1234
+        G.check(qlib.qie_sample(G.p(dl), M, V, V, C.byref(s), G.p(step), G.p(ids), G.p(ws), None))
+        got = G.host(ids)
+        for m in range(M):
+            sd = 1234 + [0, 1, 7][m]
+            want = oracle.argmax(lg[m]) if k == 1 else oracle.sample(lg[m], k, T, tp, sd)
+            assert got[m] == want, (k, T, tp, m)
+
+
+# ---------------------------------------------------------------- synthetic weights
+def test_synthetic_fill_device_equals_host(qlib):
+    from qwen_inference_engine_amd import weights as W
+    n = 1 << 20
+    t = G.zeros_bf16(n)
+    name = "model.layers.0.self_attn.q_proj.weight"
+    G.check(qlib.qie_synthetic_fill(G.p(t), n, W.tensor_id(name), 42, 0.0346, 0.0, None))
+    host = W.synthetic_tensor(name, "self_attn.q_proj.weight", n, W.SynthParams(seed=42))
+    assert np.array_equal(G.host_bf16(t), host)
+    G.check(qlib.qie_synthetic_fill(G.p(t), n, 77, 1, 0.25, 1.0, None))
+    h2 = np.empty(n, np.uint16)
+    G.check(qlib.qie_synthetic_fill_host(h2.ctypes.data, n, 77, 1, 0.25, 1.0))
+    assert np.array_equal(G.host_bf16(t), h2)

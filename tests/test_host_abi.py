@@ -1,0 +1,120 @@
+"""CPU: the C-ABI library loads, exports every symbol include/qie/*.h declares, and its
+host-side pieces (synthetic generator, weights.bin writer/loader index) behave."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, rng
+
+from qwen_inference_engine_amd import _lib, weights as W, spec as S
+
+HEADERS = [os.path.join(ROOT, "include", "qie", h) for h in ("qie_ops.h", "qie_engine.h")]
+
+
+def declared_functions():
+    names = set()
+    for h in HEADERS:
+        text = open(h).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w\s\*]*?\b(qie_\w+)\s*\(", text, flags=re.M):
+            names.add(m.group(1))
+    return names
+
+
+def test_library_exports_every_declared_symbol(qlib):
+    names = declared_functions()
+    assert len(names) >= 40
+    out = subprocess.check_output(["nm", "-D", "--defined-only", _lib.LIB_PATH]).decode()
+    exported = {l.split()[-1] for l in out.splitlines() if " T " in l}
+    missing = sorted(n for n in names if n not in exported)
+    assert not missing, missing
+    # the Python binding covers every declared function with an explicit signature
+    bound = {n for n, _, _ in _lib.SIGNATURES}
+    assert names <= bound, sorted(names - bound)
+
+
+def test_abi_version_and_error_channel(qlib):
+    assert qlib.qie_abi_version() == 1
+    # invalid call reports through qie_last_error without touching a GPU
+    rc = qlib.qie_embedding(None, None, None, 1, 8, None)
+    assert rc == -22
+    assert b"qie_embedding" in qlib.qie_last_error()
+
+
+def test_no_oracle_or_cpu_fallback_in_product():
+    """The product package never imports the oracle and libqie never links it."""
+    pkg = os.path.join(ROOT, "qwen_inference_engine_amd")
+    for dp, _, fs in os.walk(pkg):
+        for f in fs:
+            if f.endswith((".py", ".hip", ".cpp", ".hpp")):
+                t = open(os.path.join(dp, f)).read()
+                assert "import oracle" not in t and "liboracle" not in t and "or_forward" not in t, f
+    out = subprocess.check_output(["ldd", _lib.LIB_PATH]).decode()
+    assert "oracle" not in out
+
+
+def _np_splitmix(z):
+    z = (z + np.uint64(0x9E3779B97F4A7C15))
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def test_synthetic_generator_matches_its_definition(qlib, oracle):
+    """qie_synthetic_fill_host == the documented formula (qie_ops.h), restated in numpy."""
+    name, seed, scale, off = "model.layers.3.mlp.up_proj.weight", 7, 0.0346, 0.0
+    n = 4099 * 2
+    got = W.synthetic_tensor(name, "mlp.up_proj.weight", n, W.SynthParams(seed=seed))
+    with np.errstate(over="ignore"):
+        tid = np.uint64(W.tensor_id(name))
+        base = _np_splitmix(np.array([np.uint64(seed) * np.uint64(0x9E3779B97F4A7C15) ^ (tid << np.uint64(32))],
+                                     dtype=np.uint64))[0]
+        r = _np_splitmix(base + np.arange(n, dtype=np.uint64))
+    u = ((r >> np.uint64(40)).astype(np.int64) - 8388608).astype(np.float32) * np.float32(1.0 / 8388608.0)
+    want = oracle.f32_to_bf16(np.float32(off) + u * np.float32(scale))
+    assert np.array_equal(got, want)
+    assert W.tensor_id(name) == qlib.qie_tensor_id(name.encode())
+
+
+def test_weights_bin_roundtrip(tmp_path):
+    spec = S.tiny(n_layers=3, tie=True)
+    hw = W.HostWeights.synthetic(spec, W.SynthParams(seed=3, norm_scale=0.2))
+    idx = hw.write_weights_bin(str(tmp_path / "weights.bin"), str(tmp_path / "meta_data.txt"))
+    assert [t.tensor_name for t in idx] == [t.tensor_name for t in W.synthetic_index(spec)]
+    back = W.HostWeights.from_weights_bin(spec, str(tmp_path / "weights.bin"), str(tmp_path / "meta_data.txt"))
+    for k, v in hw.tensors.items():
+        assert np.array_equal(back.tensors[k], v), k
+
+
+def test_convert_safetensors(tmp_path):
+    """safetensors shards -> weights.bin + meta_data.txt (reference parser semantics)."""
+    import json
+    import struct
+    r = rng(9)
+    shards = []
+    expect = {}
+    for si, keys in enumerate([["model.b.weight", "lm_head.weight", "model.a.weight"],
+                               ["model.layers.1.x.weight", "model.layers.0.x.weight", "other.bias"]]):
+        hdr, blobs, off = {"__metadata__": {"format": "pt"}}, [], 0
+        for k in keys:
+            a = r.integers(0, 65535, (3, 5), dtype=np.uint16)
+            expect[k] = a
+            hdr[k] = {"dtype": "BF16", "shape": [3, 5], "data_offsets": [off, off + a.nbytes]}
+            blobs.append(a.tobytes())
+            off += a.nbytes
+        hb = json.dumps(hdr).encode()
+        p = tmp_path / f"model-{si}.safetensors"
+        p.write_bytes(struct.pack("<Q", len(hb)) + hb + b"".join(blobs))
+        shards.append(str(p))
+    idx = W.convert_safetensors(shards, str(tmp_path / "w.bin"), str(tmp_path / "m.txt"))
+    assert [t.tensor_name for t in idx] == ["lm_head.weight", "model.a.weight", "model.b.weight",
+                                            "model.layers.0.x.weight", "model.layers.1.x.weight"]
+    assert [t.short_name for t in idx] == ["logits", "a.weight", "b.weight", "x.weight", "x.weight"]
+    assert [t.layer_index for t in idx] == [-1, -1, -1, 0, 1]
+    data = np.fromfile(tmp_path / "w.bin", dtype=np.uint16)
+    for t in idx:
+        assert np.array_equal(data[t.data_offsets[0] // 2:t.data_offsets[1] // 2].reshape(3, 5), expect[t.tensor_name])

@@ -1,0 +1,19 @@
+#!/bin/bash
+# One GPU-box pass: parity tests, smoke, bench.  Stops at the first fault/abort/timeout
+# (exit codes other than 0/1 from pytest), never retries a GPU step.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+timeout -k 10 ${PYTEST_TIMEOUT:-900} python -m pytest tests -m gpu -q -p no:cacheprovider ${PYTEST_ARGS:-} \
+    > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+tail -5 gpurun_out/pytest_gpu.log
+echo "pytest rc=$rc"
+case $rc in 0|1) ;; *) exit $rc ;; esac
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc=$?; tail -2 gpurun_out/smoke.log; echo "smoke rc=$rc"
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+[ "${SKIP_BENCH:-0}" = "1" ] && exit 0
+timeout -k 10 ${BENCH_TIMEOUT:-600} python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
+rc=$?; tail -3 gpurun_out/bench.log; echo "bench rc=$rc"
+exit $rc

@@ -32,6 +32,17 @@ const char* qie_last_error(void);
 int qie_abi_version(void);
 int qie_device_count(int* count);
 
+/* Device memory plumbing for hosts without their own HIP runtime (ctypes tests,
+ * FFI bindings).  A process should use ONE HIP runtime: PyTorch wheels ship their
+ * own, so Python callers allocate through these rather than torch.cuda. */
+int qie_set_device(int device);
+int qie_malloc(void** ptr, int64_t bytes);
+int qie_free(void* ptr);
+int qie_memcpy_h2d(void* dst, const void* src, int64_t bytes);
+int qie_memcpy_d2h(void* dst, const void* src, int64_t bytes);
+int qie_memset(void* ptr, int value, int64_t bytes);
+int qie_synchronize(void);
+
 /* ---------------------------------------------------------------- tables
  * Replaces precompute_cos_sin (layers/src/include.cpp:5-16, called at
  * utills.cu:36-44).  Fills HOST fp32 tables [n_pos][head_dim/2]: the
@@ -122,6 +133,20 @@ int64_t qie_attention_workspace_bytes(int64_t M, int32_t n_heads, int32_t head_d
 int qie_attention(const void* q, int64_t M, const int32_t* pos, int32_t rows_per_seq,
                   const qie_kv_cache* cache, int32_t layer, int32_t n_heads, void* out,
                   void* ws, void* stream);
+
+/* Decode attention with the q/k post-projection fused in (one launch per layer):
+ * qkv rows [B][(nq + 2 nkv) hd] straight from the QKV projection; applies qk-norm
+ * (q_norm/k_norm non-NULL) and RoPE at pos[m] to q and to the new k, appends the
+ * new K/V row of sequence m at pos[m], and attends over [0, pos[m]].  Splits of 64
+ * keys are combined in-launch by the last-arriving workgroup.  ws must hold
+ * qie_attention_decode_workspace_bytes() and be ZEROED once before first use (it
+ * is left zeroed by every call). */
+int64_t qie_attention_decode_workspace_bytes(int64_t B, int32_t n_heads, int32_t n_kv_heads,
+                                             int32_t head_dim, int32_t max_ctx);
+int qie_attention_decode(const void* qkv, int64_t B, const int32_t* pos, const void* q_norm,
+                         const void* k_norm, const float* rope_cos, const float* rope_sin,
+                         int32_t n_heads, const qie_kv_cache* cache, int32_t layer, float eps,
+                         int32_t numerics, void* out, void* ws, void* stream);
 
 /* ------------------------------------------------------------- elementwise
  * launch_act + launch_elem (helpers.cuh:108-115) and launch_resadd (:116-119)

@@ -82,6 +82,13 @@ SIGNATURES = [
     ("qie_last_error", C.c_char_p, []),
     ("qie_abi_version", C.c_int, []),
     ("qie_device_count", C.c_int, [C.POINTER(C.c_int)]),
+    ("qie_set_device", C.c_int, [C.c_int]),
+    ("qie_malloc", C.c_int, [C.POINTER(_P), _I64]),
+    ("qie_free", C.c_int, [_P]),
+    ("qie_memcpy_h2d", C.c_int, [_P, _P, _I64]),
+    ("qie_memcpy_d2h", C.c_int, [_P, _P, _I64]),
+    ("qie_memset", C.c_int, [_P, C.c_int, _I64]),
+    ("qie_synchronize", C.c_int, []),
     ("qie_rope_table_host", C.c_int, [_PF, _PF, _I32, _I32, _F, _I32]),
     ("qie_embedding", C.c_int, [_P, _P, _P, _I64, _I64, _P]),
     ("qie_rmsnorm", C.c_int, [_P, _P, _P, _I64, _I64, _F, _I32, _P]),
@@ -90,6 +97,9 @@ SIGNATURES = [
                                _I32, _F, _I32, _P, _P]),
     ("qie_attention_workspace_bytes", C.c_int64, [_I64, _I32, _I32, _I32]),
     ("qie_attention", C.c_int, [_P, _I64, _P, _I32, C.POINTER(KvCacheC), _I32, _I32, _P, _P, _P]),
+    ("qie_attention_decode_workspace_bytes", C.c_int64, [_I64, _I32, _I32, _I32, _I32]),
+    ("qie_attention_decode", C.c_int, [_P, _I64, _P, _P, _P, _P, _P, _I32, C.POINTER(KvCacheC), _I32, _F, _I32,
+                                       _P, _P, _P]),
     ("qie_silu_mul", C.c_int, [_P, _P, _P, _I64, _P]),
     ("qie_residual_add", C.c_int, [_P, _P, _I64, _P]),
     ("qie_sample_workspace_bytes", C.c_int64, [_I64, _I64]),

@@ -63,6 +63,7 @@ struct qie_batch {
     uint16_t* h = nullptr;
     uint16_t* logits = nullptr;
     void* attn_ws = nullptr;
+    void* dec_ws = nullptr;     // fused decode attention: split partials + zeroed counters
     void* samp_ws = nullptr;
     std::vector<int32_t> h_pos;
     // prefill scratch
@@ -225,9 +226,8 @@ static int enqueue_layer_decode(qie_batch* b, int l) {
     a.norm_w = L.attn_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
     QIE_TRY(gemv(&a, st));
 
-    QIE_TRY(qie_qkv_post(b->qkv, B, b->d_pos, 1, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, s.n_heads,
-                         &cache, l, s.rms_eps, s.numerics, b->q, st));
-    QIE_TRY(qie_attention(b->q, B, b->d_pos, 1, &cache, l, s.n_heads, b->att, b->attn_ws, st));
+    QIE_TRY(qie_attention_decode(b->qkv, B, b->d_pos, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, s.n_heads,
+                                 &cache, l, s.rms_eps, s.numerics, b->att, b->dec_ws, st));
 
     a = lin_base();
     a.x = b->att; a.ldx = QD;
@@ -517,7 +517,12 @@ int qie_batch_create(qie_engine* e, int32_t batch, int32_t max_ctx, qie_batch** 
     A((void**)&b->logits, batch * (int64_t)s.vocab * 2);
     A(&b->attn_ws, (size_t)qie_attention_workspace_bytes(batch, s.n_heads, s.head_dim, max_ctx));
     A(&b->samp_ws, (size_t)qie_sample_workspace_bytes(batch, s.vocab));
+    const int64_t dec_ws = qie_attention_decode_workspace_bytes(batch, s.n_heads, s.n_kv_heads, s.head_dim, max_ctx);
+    A(&b->dec_ws, (size_t)dec_ws);
     if (!rc) {
+        hipMemsetAsync(b->dec_ws, 0, (size_t)dec_ws, e->stream);
+        hipMemsetAsync(b->kc, 0, (size_t)batch * b->seq_stride * 2, e->stream);
+        hipMemsetAsync(b->vc, 0, (size_t)batch * b->seq_stride * 2, e->stream);
         hipMemsetAsync(b->d_keys, 0, batch * 8, e->stream);
         hipMemsetAsync(b->d_pos, 0, batch * 4, e->stream);
         hipMemsetAsync(b->d_step, 0, batch * 4, e->stream);
@@ -541,7 +546,7 @@ void qie_batch_destroy(qie_batch* b) {
     if (b->e && b->e->stream) hipStreamSynchronize(b->e->stream);
     if (b->gexec) hipGraphExecDestroy(b->gexec);
     void* ps[] = {b->kc, b->vc, b->d_pos, b->d_step, b->d_hist, b->d_ids, b->d_keys, b->x_res, b->qkv, b->q,
-                  b->att, b->h, b->logits, b->attn_ws, b->samp_ws, b->pf_x, b->pf_hn, b->pf_qkv, b->pf_q,
+                  b->att, b->h, b->logits, b->attn_ws, b->dec_ws, b->samp_ws, b->pf_x, b->pf_hn, b->pf_qkv, b->pf_q,
                   b->pf_att, b->pf_h, b->pf_pos, b->pf_ids, b->pf_attn_ws};
     for (void* p : ps)
         if (p) hipFree(p);
@@ -756,7 +761,9 @@ int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* av
     QIE_HIP(hipEventCreate(&t0));
     QIE_HIP(hipEventCreate(&t1));
     auto run = [&]() -> int {
-        if (which == 5) return qie_attention(b->q, B, b->d_pos, 1, &cache, 0, s.n_heads, scratch, b->attn_ws, e->stream);
+        if (which == 5)
+            return qie_attention_decode(b->qkv, B, b->d_pos, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, s.n_heads,
+                                        &cache, 0, s.rms_eps, s.numerics, scratch, b->dec_ws, e->stream);
         return qie_linear(&a, e->stream);
     };
     QIE_TRY(run());   // warm-up

@@ -303,6 +303,43 @@ int qie_device_count(int* count) {
     return 0;
 }
 
+int qie_set_device(int device) {
+    QIE_HIP(hipSetDevice(device));
+    return 0;
+}
+
+int qie_malloc(void** ptr, int64_t bytes) {
+    QIE_REQUIRE(ptr && bytes >= 0, "qie_malloc: bad arguments");
+    QIE_HIP(hipMalloc(ptr, bytes < 16 ? 16 : (size_t)bytes));
+    return 0;
+}
+
+int qie_free(void* ptr) {
+    if (ptr) QIE_HIP(hipFree(ptr));
+    return 0;
+}
+
+int qie_memcpy_h2d(void* dst, const void* src, int64_t bytes) {
+    QIE_HIP(hipMemcpy(dst, src, (size_t)bytes, hipMemcpyHostToDevice));
+    return 0;
+}
+
+int qie_memcpy_d2h(void* dst, const void* src, int64_t bytes) {
+    QIE_HIP(hipDeviceSynchronize());
+    QIE_HIP(hipMemcpy(dst, src, (size_t)bytes, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int qie_memset(void* ptr, int value, int64_t bytes) {
+    QIE_HIP(hipMemset(ptr, value, (size_t)bytes));
+    return 0;
+}
+
+int qie_synchronize(void) {
+    QIE_HIP(hipDeviceSynchronize());
+    return 0;
+}
+
 int qie_rope_table_host(float* cos_out, float* sin_out, int32_t n_pos, int32_t head_dim,
                         float theta, int32_t numerics) {
     QIE_REQUIRE(cos_out && sin_out && n_pos > 0 && head_dim > 0 && head_dim % 2 == 0,

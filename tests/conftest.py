@@ -28,12 +28,5 @@ def qlib():
     return _lib.load()
 
 
-@pytest.fixture(scope="session")
-def torch_cuda():
-    import torch
-    assert torch.cuda.is_available(), "gpu test without a visible GPU"
-    return torch
-
-
 def rng(seed=0):
     return np.random.default_rng(seed)

@@ -1,4 +1,6 @@
-"""Helpers for GPU tests: torch is only device-memory plumbing; all compute is libqie."""
+"""Helpers for GPU tests.  Device memory comes from libqie (qie_malloc & co): a process
+must not host two HIP runtimes, and the PyTorch wheel ships its own (ROCm 7.0) while
+libqie links /opt/rocm (7.2) — so torch.cuda is never touched in-process."""
 import ctypes as C
 
 import numpy as np
@@ -6,39 +8,76 @@ import numpy as np
 from qwen_inference_engine_amd import _lib
 
 
-def torch():
-    import torch as T
-    assert T.cuda.is_available(), "gpu test without a visible GPU"
-    return T
+def L():
+    return _lib.load()
 
 
-def dev(a: np.ndarray):
-    T = torch()
+def check(rc, what=""):
+    _lib.check(rc, what)
+
+
+class DBuf:
+    """A device allocation with a numpy dtype/shape (freed with the object)."""
+
+    def __init__(self, shape, dtype):
+        self.shape = tuple(shape) if isinstance(shape, (tuple, list)) else (int(shape),)
+        self.dtype = np.dtype(dtype)
+        self.nbytes = int(np.prod(self.shape)) * self.dtype.itemsize
+        p = C.c_void_p()
+        check(L().qie_malloc(C.byref(p), self.nbytes), "qie_malloc")
+        self.ptr = p.value
+
+    def upload(self, a: np.ndarray) -> "DBuf":
+        a = np.ascontiguousarray(a, dtype=self.dtype)
+        assert a.nbytes == self.nbytes
+        check(L().qie_memcpy_h2d(self.ptr, a.ctypes.data, self.nbytes), "h2d")
+        return self
+
+    def numpy(self) -> np.ndarray:
+        out = np.empty(self.shape, self.dtype)
+        check(L().qie_memcpy_d2h(out.ctypes.data, self.ptr, self.nbytes), "d2h")
+        return out
+
+    def data_ptr(self) -> int:
+        return self.ptr
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                L().qie_free(self.ptr)
+        except Exception:
+            pass
+
+
+def dev(a: np.ndarray) -> DBuf:
     a = np.ascontiguousarray(a)
-    if a.dtype == np.uint16:
-        return T.from_numpy(a.view(np.int16).copy()).cuda()
-    if a.dtype == np.uint64:
-        return T.from_numpy(a.view(np.int64).copy()).cuda()
-    return T.from_numpy(a.copy()).cuda()
+    return DBuf(a.shape, a.dtype).upload(a)
 
 
-def zeros_bf16(*shape):
-    T = torch()
-    return T.zeros(*shape, dtype=T.int16, device="cuda")
+def zeros(shape, dtype=np.uint16) -> DBuf:
+    b = DBuf(shape, dtype)
+    check(L().qie_memset(b.ptr, 0, b.nbytes), "memset")
+    return b
 
 
-def host_bf16(t) -> np.ndarray:
-    torch().cuda.synchronize()
-    return t.cpu().numpy().view(np.uint16)
+def zeros_bf16(*shape) -> DBuf:
+    return zeros(shape, np.uint16)
 
 
-def host(t) -> np.ndarray:
-    torch().cuda.synchronize()
-    return t.cpu().numpy()
+def zeros_bytes(n) -> DBuf:
+    return zeros((max(int(n), 16),), np.uint8)
+
+
+def host_bf16(t: DBuf) -> np.ndarray:
+    return t.numpy().view(np.uint16)
+
+
+def host(t: DBuf) -> np.ndarray:
+    return t.numpy()
 
 
 def p(t) -> int:
-    return t.data_ptr()
+    return None if t is None else t.ptr
 
 
 def bf(a):
@@ -68,7 +107,3 @@ def assert_sum_close(got, want, abs_scale, rel=1e-5, what=""):
     bad = np.abs(g - w) > tol
     assert not bad.any(), f"{what}: {bad.sum()} / {bad.size} outside tolerance; worst " \
         f"{np.abs(g - w)[bad].max() if bad.any() else 0}"
-
-
-def check(rc, what=""):
-    _lib.check(rc, what)

@@ -1,10 +1,16 @@
 """GPU end-to-end parity: the libqie engine (prefill + hipGraph decode) against the CPU
 oracle's full forward on identical synthetic weights and prompts.
 
-Bar: greedy token ids identical to the oracle's; per-step bf16 logits within a few bf16
-ulps of the oracle's (different fp32 summation orders inside the dot products); engine
-invariants (graph == eager, batch == single, weights.bin == synthetic init, rewind) are
-bit-exact.
+Bar (written per check):
+* logits: every step's bf16 logits within 4 bf16 ulps of the largest |logit| of the
+  oracle's (fp32 summation order differs inside every dot product, 2-80 layers deep);
+* greedy ids: TEACHER-FORCED — at every step the engine's arg-max must equal the
+  oracle's unless the oracle's own logits put the two tokens within that same tolerance
+  (a near-tie, where any fp32 reordering may flip a bf16 arg-max); the oracle's token is
+  then forced into the engine (qie_batch_set_position) so later steps stay comparable.
+  Near-tie flips are counted and bounded;
+* engine invariants (graph == eager, batch == single, weights.bin == synthetic init,
+  device-tensor weights, rewind) are bit-exact.
 """
 import numpy as np
 import pytest
@@ -26,6 +32,7 @@ CONFIGS = {
                       vocab=777 * 2, tie=True, bias=True),
 }
 SYN = W.SynthParams(seed=11, w_scale=0.08, norm_scale=0.25, bias_scale=0.05)
+LOGIT_ULPS = 4
 
 
 def make_pair(spec, oracle, max_ctx=128, use_graph=True, syn=SYN):
@@ -34,10 +41,34 @@ def make_pair(spec, oracle, max_ctx=128, use_graph=True, syn=SYN):
     return eng, hw, oracle.Model(hw, max_ctx)
 
 
+def logit_tol(want):
+    return LOGIT_ULPS * 2.0 ** -7 * max(1.0, float(np.abs(G.bf(want)).max()))
+
+
 def logits_close(got, want, what=""):
     g, w = G.bf(got).astype(np.float64), G.bf(want).astype(np.float64)
-    tol = 4 * 2.0 ** -7 * max(1.0, np.abs(w).max())
-    assert np.abs(g - w).max() <= tol, f"{what}: max |dlogit| {np.abs(g - w).max()} > {tol}"
+    assert np.abs(g - w).max() <= logit_tol(want), f"{what}: max |dlogit| {np.abs(g - w).max()} > {logit_tol(want)}"
+
+
+def forced_compare(oracle, b, om, prompt, n_new, seq=0):
+    """Teacher-forced greedy comparison; returns (oracle ids, near-tie flips)."""
+    lg_o = om.forward(prompt, 0)
+    t_e = b.prefill(seq, prompt)
+    ids, flips = [], 0
+    for i in range(n_new):
+        lg_e = b.logits()[seq]
+        logits_close(lg_e, lg_o, f"step {i}")
+        t_o = oracle.argmax(lg_o)
+        if t_e != t_o:
+            gap = abs(float(G.bf(lg_o[t_o])) - float(G.bf(lg_o[t_e])))
+            assert gap <= logit_tol(lg_o), f"step {i}: engine {t_e} vs oracle {t_o}, oracle gap {gap}"
+            flips += 1
+            b.set_position(seq, len(prompt) + i, t_o)
+        ids.append(t_o)
+        if i + 1 < n_new:
+            t_e = b.decode_step()[seq]
+            lg_o = om.forward([t_o])
+    return ids, flips
 
 
 @pytest.mark.parametrize("name", list(CONFIGS))
@@ -47,16 +78,9 @@ def test_greedy_generation_matches_oracle(oracle, name, num, P):
     spec = CONFIGS[name].with_numerics(num)
     eng, hw, om = make_pair(spec, oracle)
     prompt = list(rng(P).integers(0, spec.vocab, P))
-    n_new = 12
-    want_ids, want_lg = om.generate_greedy(prompt, n_new)
-    b = eng.batch(1, 128)
-    first = b.prefill(0, prompt)
-    logits_close(b.logits()[0], want_lg[0], "prefill")
-    got = [first]
-    for i in range(1, n_new):
-        got.append(b.decode_step()[0])
-        logits_close(b.logits()[0], want_lg[i], f"step {i}")
-    assert got == want_ids
+    n_new = 16
+    ids, flips = forced_compare(oracle, eng.batch(1, 128), om, prompt, n_new)
+    assert flips <= 2, f"{flips} near-tie flips in {n_new} steps"
 
 
 def test_graph_equals_eager_and_batch_equals_single(oracle):
@@ -65,18 +89,21 @@ def test_graph_equals_eager_and_batch_equals_single(oracle):
     outs = {}
     for graph in (True, False):
         eng = Q.Engine(spec, max_ctx=96, use_graph=graph).init_synthetic(SYN)
-        singles = []
+        singles, slog = [], []
         for pr in prompts:
             b = eng.batch(1, 96)
             t0 = b.prefill(0, pr)
             singles.append([t0] + list(b.decode(10)[:, 0]))
+            slog.append(b.logits()[0])
         b3 = eng.batch(3, 96)
         firsts = [b3.prefill(i, pr) for i, pr in enumerate(prompts)]
         rest = b3.decode(10)
         multi = [[firsts[i]] + list(rest[:, i]) for i in range(3)]
         assert multi == singles
-        outs[graph] = singles
-    assert outs[True] == outs[False]
+        assert np.array_equal(b3.logits(), np.stack(slog))
+        outs[graph] = (singles, np.stack(slog))
+    assert outs[True][0] == outs[False][0]
+    assert np.array_equal(outs[True][1], outs[False][1])
 
 
 def test_weights_bin_loader_equals_synthetic(oracle, tmp_path):
@@ -87,22 +114,26 @@ def test_weights_bin_loader_equals_synthetic(oracle, tmp_path):
     e1 = Q.Engine(spec, max_ctx=64).init_synthetic(SYN)
     e2 = Q.Engine(spec, max_ctx=64).load_weights_bin(str(tmp_path / "weights.bin"), str(tmp_path / "meta_data.txt"),
                                                      chunk_bytes=1 << 16)
-    r = []
+    r, lg = [], []
     for e in (e1, e2):
         b = e.batch(1, 64)
         r.append([b.prefill(0, prompt)] + list(b.decode(8)[:, 0]))
+        lg.append(b.logits())
     assert r[0] == r[1]
+    assert np.array_equal(lg[0], lg[1])
 
 
 def test_set_weights_from_device_tensors(oracle):
     spec = CONFIGS["tied-g7"]
     hw = W.HostWeights.synthetic(spec, SYN)
     dev = {n: G.dev(a) for n, a in hw.tensors.items()}
-    e = Q.Engine(spec, max_ctx=64).set_weights({n: t.data_ptr() for n, t in dev.items()}, keepalive=dev)
-    om = oracle.Model(hw, 64)
-    want, _ = om.generate_greedy([5, 4, 3, 2, 1], 8)
-    b = e.batch(1, 64)
-    assert [b.prefill(0, [5, 4, 3, 2, 1])] + list(b.decode(7)[:, 0]) == want
+    e1 = Q.Engine(spec, max_ctx=64).set_weights({n: t.data_ptr() for n, t in dev.items()}, keepalive=dev)
+    e2 = Q.Engine(spec, max_ctx=64).init_synthetic(SYN)
+    r = []
+    for e in (e1, e2):
+        b = e.batch(1, 64)
+        r.append(([b.prefill(0, [5, 4, 3, 2, 1])] + list(b.decode(7)[:, 0]), b.logits()))
+    assert r[0][0] == r[1][0] and np.array_equal(r[0][1], r[1][1])
 
 
 def test_rewind_reproduces(oracle):
@@ -118,35 +149,26 @@ def test_rewind_reproduces(oracle):
     assert list(hist[:len(prompt)]) == prompt and hist[len(prompt)] == t0 and list(hist[len(prompt) + 1:]) == a
 
 
-def test_topk_sampling_matches_oracle(oracle):
-    """Reference sampling schedule: prefill (k=50, T=1.0, seed 1234), decode step s
-    (k=50, T=0.7, seed 1234+s) — qwen_main.cu:241, 381-388."""
+def test_topk_sampling_schedule_on_engine_logits(oracle):
+    """Reference sampling schedule — prefill k=50, T=1.0, seed 1234; decode step s k=50,
+    T=0.7, seed 1234+s (qwen_main.cu:241, 381-388) — applied by the oracle's restated
+    sampler to the ENGINE's own logits must give the engine's token at every step."""
     spec = CONFIGS["qwen2-bias-hd64"]
-    eng, hw, om = make_pair(spec, oracle)
-    prompt = [11, 22, 33, 44, 55, 66, 77]
+    eng = Q.Engine(spec, max_ctx=128).init_synthetic(SYN)
     b = eng.batch(1, 128)
-    got = [b.prefill(0, prompt, Q.Sampling(top_k=50, temperature=1.0, seed=1234))]
-    lg = om.forward(prompt, 0)
-    want = [oracle.sample(lg, 50, 1.0, 1.0, 1234)]
-    for s in range(1, 10):
-        got.append(b.decode_step(Q.Sampling(top_k=50, temperature=0.7, seed=1234))[0])
-        lg = om.forward([want[-1]])
-        want.append(oracle.sample(lg, 50, 0.7, 1.0, 1234 + s))
-        assert got == want
+    prompt = [11, 22, 33, 44, 55, 66, 77]
+    tok = b.prefill(0, prompt, Q.Sampling(top_k=50, temperature=1.0, seed=1234))
+    assert tok == oracle.sample(b.logits()[0], 50, 1.0, 1.0, 1234)
+    for s in range(1, 12):
+        tok = b.decode_step(Q.Sampling(top_k=50, temperature=0.7, seed=1234))[0]
+        assert tok == oracle.sample(b.logits()[0], 50, 0.7, 1.0, 1234 + s), s
 
 
 @pytest.mark.slow
 def test_qwen2_0_5b_config1_greedy_matches_oracle(oracle):
     """BASELINE config 1 shape (Qwen2-0.5B, prompt 16, gen 16, greedy) at full size."""
     spec = S.QWEN2_0_5B
-    syn = W.SynthParams(seed=0)
-    eng, hw, om = make_pair(spec, oracle, max_ctx=64, syn=syn)
+    eng, hw, om = make_pair(spec, oracle, max_ctx=64, syn=W.SynthParams(seed=0))
     prompt = list(rng(1).integers(0, spec.vocab, 16))
-    want, want_lg = om.generate_greedy(prompt, 16)
-    b = eng.batch(1, 64)
-    got = [b.prefill(0, prompt)]
-    logits_close(b.logits()[0], want_lg[0], "prefill")
-    for i in range(1, 16):
-        got.append(b.decode_step()[0])
-        logits_close(b.logits()[0], want_lg[i], f"step {i}")
-    assert got == want
+    ids, flips = forced_compare(oracle, eng.batch(1, 64), om, prompt, 16)
+    assert flips <= 2

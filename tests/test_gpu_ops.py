@@ -134,7 +134,7 @@ def test_linear_fused_norm_and_argmax(oracle, qlib, M, num):
             num=0 if num == "ref" else 1, keys=keys)
     got = G.host_bf16(y)
     G.assert_sum_close(got, want, _abs_scale(oracle, xn, w) * 2, rel=2e-5, what="fused norm")
-    ids = G.torch().zeros(M, dtype=G.torch().int32, device="cuda")
+    ids = G.zeros((M,), np.int32)
     G.check(qlib.qie_keys_to_ids(G.p(keys), M, G.p(ids), None))
     for m in range(M):   # fused arg-max == reference rule on the kernel's own logits
         assert G.host(ids)[m] == oracle.argmax(got[m])
@@ -215,7 +215,7 @@ def test_attention_decode(oracle, qlib, hd, nq, nkv, ctxs):
     q = rand_bf16(oracle, (B, nq * hd), seed=3)
     pos = np.array(ctxs, np.int32) - 1
     ws_bytes = qlib.qie_attention_workspace_bytes(B, nq, hd, maxc)
-    ws = G.torch().zeros(max(ws_bytes, 16), dtype=G.torch().uint8, device="cuda")
+    ws = G.zeros_bytes(ws_bytes)
     kc, vc = G.dev(kc_h), G.dev(vc_h)
     out = G.zeros_bf16(B, nq * hd)
     c = _cache(kc, vc, L, nkv, hd, maxc, seq_stride)
@@ -237,7 +237,7 @@ def test_attention_prefill_causal(oracle, qlib, P):
     q = rand_bf16(oracle, (P, nq * hd), seed=P + 2)
     pos = np.arange(P, dtype=np.int32)
     ws_bytes = qlib.qie_attention_workspace_bytes(P, nq, hd, maxc)
-    ws = G.torch().zeros(max(ws_bytes, 16), dtype=G.torch().uint8, device="cuda")
+    ws = G.zeros_bytes(ws_bytes)
     kc, vc = G.dev(kc_h), G.dev(vc_h)
     out = G.zeros_bf16(P, nq * hd)
     c = _cache(kc, vc, L, nkv, hd, maxc, seq_stride)
@@ -271,8 +271,8 @@ def test_sampling_greedy_topk_and_draw(oracle, qlib, V, kind):
     else:
         lg = oracle.f32_to_bf16((r.standard_normal((M, V)) * 3).astype(np.float32))
     dl = G.dev(lg)
-    ws = G.torch().zeros(qlib.qie_sample_workspace_bytes(M, V), dtype=G.torch().uint8, device="cuda")
-    ids = G.torch().zeros(M, dtype=G.torch().int32, device="cuda")
+    ws = G.zeros_bytes(qlib.qie_sample_workspace_bytes(M, V))
+    ids = G.zeros((M,), np.int32)
     step = G.dev(np.array([0, 1, 7], np.int32))
     for k, T, tp in [(1, 1.0, 1.0), (50, 0.7, 1.0), (50, 1.0, 1.0), (5, 1.3, 1.0), (256, 0.9, 1.0), (50, 0.8, 0.9)]:
         s = SamplingC()
@@ -298,3 +298,56 @@ def test_synthetic_fill_device_equals_host(qlib):
     h2 = np.empty(n, np.uint16)
     G.check(qlib.qie_synthetic_fill_host(h2.ctypes.data, n, 77, 1, 0.25, 1.0))
     assert np.array_equal(G.host_bf16(t), h2)
+
+
+# ------------------------------------------------------ fused decode attention
+@pytest.mark.parametrize("hd", [64, 128])
+@pytest.mark.parametrize("qkn,num", [(False, "ref"), (True, "ref"), (False, "hf"), (True, "hf")])
+@pytest.mark.parametrize("nq,nkv", [(28, 4), (14, 2), (5, 1)])
+def test_attention_decode_fused(oracle, qlib, hd, qkn, num, nq, nkv):
+    """qk-norm + RoPE + KV append + split attention + in-launch combine, one launch,
+    against qknorm/rope/attention of the oracle (and the appended cache rows)."""
+    L, layer, maxc = 2, 1, 700
+    ctxs = [1, 64, 65, 129, 700] if nq == 28 else [3, 200, 640]
+    B = len(ctxs)
+    QD, KD = nq * hd, nkv * hd
+    seq_stride = L * nkv * maxc * hd
+    kc_h = rand_bf16(oracle, (B, L, nkv, maxc, hd), seed=hd + nq)
+    vc_h = rand_bf16(oracle, (B, L, nkv, maxc, hd), seed=hd + nq + 1)
+    qkv = rand_bf16(oracle, (B, QD + 2 * KD), seed=5)
+    pos = np.array(ctxs, np.int32) - 1
+    eps = 1e-4 if num == "ref" else 1e-6
+    qn = oracle.f32_to_bf16((1 + 0.3 * rng(1).standard_normal(hd)).astype(np.float32)) if qkn else None
+    kn = oracle.f32_to_bf16((1 + 0.3 * rng(2).standard_normal(hd)).astype(np.float32)) if qkn else None
+    cs, sn = oracle.rope_table(maxc, hd, 1e6, num)
+    q, k, v = qkv[:, :QD].copy(), qkv[:, QD:QD + KD].copy(), qkv[:, QD + KD:].copy()
+    if qkn:
+        q = oracle.qknorm(q, qn, nq, hd, eps, num)
+        k = oracle.qknorm(k, kn, nkv, hd, eps, num)
+    q = oracle.rope(q, cs, sn, pos, nq, hd, num)
+    k = oracle.rope(k, cs, sn, pos, nkv, hd, num)
+    ws = G.zeros_bytes(qlib.qie_attention_decode_workspace_bytes(B, nq, nkv, hd, maxc))
+    kc, vc = G.dev(kc_h), G.dev(vc_h)
+    out = G.zeros_bf16(B, QD)
+    c = _cache(kc, vc, L, nkv, hd, maxc, seq_stride)
+    dqn, dkn = (G.dev(qn), G.dev(kn)) if qkn else (None, None)
+    dcs, dsn, dqkv, dpos = G.dev(cs), G.dev(sn), G.dev(qkv), G.dev(pos)
+    for rep in range(2):   # second call checks the counters were left zeroed
+        G.check(qlib.qie_attention_decode(G.p(dqkv), B, G.p(dpos), G.p(dqn), G.p(dkn), G.p(dcs), G.p(dsn), nq,
+                                          C.byref(c), layer, eps, 0 if num == "ref" else 1, G.p(out), G.p(ws), None))
+        got = G.host_bf16(out)
+        hk = G.host_bf16(kc).reshape(B, L, nkv, maxc, hd)
+        hv = G.host_bf16(vc).reshape(B, L, nkv, maxc, hd)
+        for b in range(B):
+            p = pos[b]
+            for g in range(nkv):
+                G.assert_bf16_close(hk[b, layer, g, p], k[b, g * hd:(g + 1) * hd], 1, 0.9 if qkn else 1.0, "k")
+                assert np.array_equal(hv[b, layer, g, p], v[b, g * hd:(g + 1) * hd])
+            kk = kc_h[b, layer, :, :p + 1].copy()
+            vv = vc_h[b, layer, :, :p + 1].copy()
+            kk[:, p] = k[b].reshape(nkv, hd)
+            vv[:, p] = v[b].reshape(nkv, hd)
+            want = oracle.attention(q[b:b + 1], kk, vv, nq, nkv, hd, False, 0)
+            d = np.abs(G.bf(got[b]) - G.bf(want[0]))
+            assert d.max() <= 2 ** -7 * max(1.0, np.abs(G.bf(want[0])).max()) * 2, f"ctx {ctxs[b]}: {d.max()}"
+    assert not G.host(ws)[:B * nkv * 4].any()

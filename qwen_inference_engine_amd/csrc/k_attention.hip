@@ -224,27 +224,50 @@ struct DecodeAttnParams {
     uint16_t* out;            // [B][nq * HD]
 };
 
-constexpr int kDecChunk = 64;
+// Splits per (row, kv head): ~16 at long context (>= 64 keys each), more only when
+// a split would exceed 16 keys per thread.  All derived from the live context on
+// device, so a captured graph stays valid as the sequence grows.
+constexpr int kDecMinKeys = 64;
+constexpr int kDecSplits = 16;
+constexpr int kDecNtMax = 16;        // keys per thread per split
+constexpr int kDecMaxSplits = 160;
+
+__host__ __device__ __forceinline__ int dec_tpb(int hd) { return 256 / (hd / 8); }
+__host__ __device__ __forceinline__ int dec_nsplit_target(int ctx, int hd) {
+    const int by_min = (ctx + kDecMinKeys - 1) / kDecMinKeys;
+    const int cap = kDecNtMax * dec_tpb(hd);
+    const int by_cap = (ctx + cap - 1) / cap;
+    const int want = by_cap > kDecSplits ? by_cap : kDecSplits;
+    return by_min < want ? by_min : want;
+}
 
 template <int HD>
 __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnParams a) {
 #pragma clang fp contract(off)
     constexpr int LPT = HD / 8;          // lanes per key row
     constexpr int TPB = 256 / LPT;       // keys per block step (16 or 32)
-    constexpr int NT = kDecChunk / TPB;  // keys per thread
+    constexpr int NTMAX = kDecNtMax;
+    constexpr int CHMAX = NTMAX * TPB;
     __shared__ __attribute__((aligned(16))) float q_s[kMaxGroup][HD];
     __shared__ __attribute__((aligned(16))) uint16_t kv_new[2][HD];
-    __shared__ float red_m[4][kMaxGroup], red_l[4][kMaxGroup];
-    __shared__ float red_o[4][kMaxGroup][HD];
+    __shared__ float p_s[kMaxGroup][CHMAX];
+    __shared__ __attribute__((aligned(16))) float red_o[4][kMaxGroup][HD];
+    __shared__ float stat_m[kMaxGroup], stat_l[kMaxGroup];
+    __shared__ float cw[kMaxGroup][kDecMaxSplits];
     __shared__ int last_flag;
 
     const int64_t m = blockIdx.y;
     const int g = blockIdx.x / a.nsplit_max, s = blockIdx.x % a.nsplit_max;
     const int G = a.nq / a.nkv;
     const int p = a.pos[m], ctx = p + 1;
-    const int nsplit = (ctx + kDecChunk - 1) / kDecChunk;
+    const int nst = dec_nsplit_target(ctx, HD);
+    int chunk = (ctx + nst - 1) / nst;
+    chunk = (chunk + TPB - 1) / TPB * TPB;
+    const int nsplit = (ctx + chunk - 1) / chunk;
     if (s >= nsplit) return;
-    const int t0 = s * kDecChunk, t1 = min(ctx, t0 + kDecChunk);
+    const int t0 = s * chunk, t1 = min(ctx, t0 + chunk);
+    const int ntok = t1 - t0;
+    const int NT = (ntok + TPB - 1) / TPB;
     const bool has_new = (t1 == ctx);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int grp = tid / LPT, dl = tid % LPT;
@@ -323,95 +346,105 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnParams a) {
     }
     __syncthreads();
 
-    // ---------------- K/V loads for this thread's NT keys (all issued up front)
-    uint4 kr[NT], vr[NT];
-    int tt[NT];
+    // ---------------- phase A: all K loads in flight, then scores -> p_s
+    {
+        uint4 kr[NTMAX];
 #pragma unroll
-    for (int i = 0; i < NT; i++) {
-        const int t = t0 + grp + TPB * i;
-        tt[i] = t;
-        const int tc = t < t1 ? t : t0;   // masked slots re-read a written row (never garbage)
-        if (tc == p) {
-            kr[i] = *reinterpret_cast<const uint4*>(&kv_new[0][dl * 8]);
-            vr[i] = *reinterpret_cast<const uint4*>(&kv_new[1][dl * 8]);
-        } else {
-            kr[i] = *reinterpret_cast<const uint4*>(kb + (int64_t)tc * HD + dl * 8);
-            vr[i] = *reinterpret_cast<const uint4*>(vb + (int64_t)tc * HD + dl * 8);
+        for (int i = 0; i < NTMAX; i++) {
+            if (i < NT) {
+                const int t = t0 + grp + TPB * i;
+                const int tc = t < t1 ? t : t0;   // masked slots re-read a written row
+                kr[i] = (tc == p) ? *reinterpret_cast<const uint4*>(&kv_new[0][dl * 8])
+                                  : *reinterpret_cast<const uint4*>(kb + (int64_t)tc * HD + dl * 8);
+            }
+        }
+        float qf[kMaxGroup][8];
+#pragma unroll
+        for (int gi = 0; gi < kMaxGroup; gi++)
+#pragma unroll
+            for (int j = 0; j < 8; j++) qf[gi][j] = gi < G ? q_s[gi][dl * 8 + j] : 0.f;
+        const float scale = sqrtf((float)HD);
+#pragma unroll
+        for (int i = 0; i < NTMAX; i++) {
+            if (i >= NT) continue;
+            float kf[8];
+            uint32_t w[4] = {kr[i].x, kr[i].y, kr[i].z, kr[i].w};
+#pragma unroll
+            for (int j = 0; j < 4; j++) { kf[2 * j] = bf_lo(w[j]); kf[2 * j + 1] = bf_hi(w[j]); }
+            const int tl = grp + TPB * i;
+#pragma unroll
+            for (int gi = 0; gi < kMaxGroup; gi++) {
+                if (gi >= G) continue;
+                float d = 0.f;
+#pragma unroll
+                for (int j = 0; j < 8; j++) d = fmaf(qf[gi][j], kf[j], d);
+#pragma unroll
+                for (int off = LPT / 2; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
+                if (dl == 0 && tl < ntok) p_s[gi][tl] = d / scale;
+            }
         }
     }
-    // ---------------- scores  s = dot(q, k) / sqrtf(hd)
-    const float scale = sqrtf((float)HD);
-    float sc[NT][kMaxGroup];
-#pragma unroll
-    for (int i = 0; i < NT; i++) {
-        float kf[8];
-        uint32_t w[4] = {kr[i].x, kr[i].y, kr[i].z, kr[i].w};
-#pragma unroll
-        for (int j = 0; j < 4; j++) { kf[2 * j] = bf_lo(w[j]); kf[2 * j + 1] = bf_hi(w[j]); }
-#pragma unroll
-        for (int gi = 0; gi < kMaxGroup; gi++) {
-            if (gi >= G) { sc[i][gi] = -INFINITY; continue; }
-            const float4 q0 = *reinterpret_cast<const float4*>(&q_s[gi][dl * 8]);
-            const float4 q1 = *reinterpret_cast<const float4*>(&q_s[gi][dl * 8 + 4]);
-            float d = 0.f;
-            d = fmaf(q0.x, kf[0], d); d = fmaf(q0.y, kf[1], d); d = fmaf(q0.z, kf[2], d); d = fmaf(q0.w, kf[3], d);
-            d = fmaf(q1.x, kf[4], d); d = fmaf(q1.y, kf[5], d); d = fmaf(q1.z, kf[6], d); d = fmaf(q1.w, kf[7], d);
-#pragma unroll
-            for (int off = LPT / 2; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
-            sc[i][gi] = tt[i] < t1 ? d / scale : -INFINITY;
-        }
-    }
-    // ---------------- block max per head
-    float mx[kMaxGroup];
-#pragma unroll
-    for (int gi = 0; gi < kMaxGroup; gi++) {
-        float v = -INFINITY;
-#pragma unroll
-        for (int i = 0; i < NT; i++) v = fmaxf(v, sc[i][gi]);
-#pragma unroll
-        for (int off = LPT; off < 64; off <<= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
-        mx[gi] = v;
-    }
-    if (lane == 0)
-#pragma unroll
-        for (int gi = 0; gi < kMaxGroup; gi++) red_m[wave][gi] = mx[gi];
     __syncthreads();
+    // ---------------- phase B: per-head max, p = exp(s - max), l = sum p
+    for (int gi = wave; gi < G; gi += 4) {
+        float mx = -INFINITY;
+        for (int j = lane; j < ntok; j += 64) mx = fmaxf(mx, p_s[gi][j]);
+        mx = wave_max(mx);
+        float sum = 0.f;
+        for (int j = lane; j < ntok; j += 64) {
+            const float e = expf(p_s[gi][j] - mx);
+            p_s[gi][j] = e;
+            sum += e;
+        }
+        sum = wave_sum(sum);
+        if (lane == 0) {
+            stat_m[gi] = mx;
+            stat_l[gi] = sum;
+        }
+    }
+    __syncthreads();
+    // ---------------- phase C: all V loads in flight, o = sum p v
+    float o[kMaxGroup][8];
 #pragma unroll
     for (int gi = 0; gi < kMaxGroup; gi++)
-        mx[gi] = fmaxf(fmaxf(red_m[0][gi], red_m[1][gi]), fmaxf(red_m[2][gi], red_m[3][gi]));
-    // ---------------- p = exp(s - max), l = sum p, o = sum p v
-    float l[kMaxGroup], o[kMaxGroup][8];
-#pragma unroll
-    for (int gi = 0; gi < kMaxGroup; gi++) {
-        l[gi] = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; j++) o[gi][j] = 0.f;
-    }
+    {
+        uint4 vr[NTMAX];
 #pragma unroll
-    for (int i = 0; i < NT; i++) {
-        float vf[8];
-        uint32_t w[4] = {vr[i].x, vr[i].y, vr[i].z, vr[i].w};
+        for (int i = 0; i < NTMAX; i++) {
+            if (i < NT) {
+                const int t = t0 + grp + TPB * i;
+                const int tc = t < t1 ? t : t0;
+                vr[i] = (tc == p) ? *reinterpret_cast<const uint4*>(&kv_new[1][dl * 8])
+                                  : *reinterpret_cast<const uint4*>(vb + (int64_t)tc * HD + dl * 8);
+            }
+        }
 #pragma unroll
-        for (int j = 0; j < 4; j++) { vf[2 * j] = bf_lo(w[j]); vf[2 * j + 1] = bf_hi(w[j]); }
+        for (int i = 0; i < NTMAX; i++) {
+            if (i >= NT) continue;
+            const int tl = grp + TPB * i;
+            if (tl >= ntok) continue;
+            float vf[8];
+            uint32_t w[4] = {vr[i].x, vr[i].y, vr[i].z, vr[i].w};
 #pragma unroll
-        for (int gi = 0; gi < kMaxGroup; gi++) {
-            if (gi >= G) continue;
-            const float e = tt[i] < t1 ? expf(sc[i][gi] - mx[gi]) : 0.f;
-            l[gi] += e;
+            for (int j = 0; j < 4; j++) { vf[2 * j] = bf_lo(w[j]); vf[2 * j + 1] = bf_hi(w[j]); }
 #pragma unroll
-            for (int j = 0; j < 8; j++) o[gi][j] = fmaf(e, vf[j], o[gi][j]);
+            for (int gi = 0; gi < kMaxGroup; gi++) {
+                if (gi >= G) continue;
+                const float e = p_s[gi][tl];
+#pragma unroll
+                for (int j = 0; j < 8; j++) o[gi][j] = fmaf(e, vf[j], o[gi][j]);
+            }
         }
     }
-    // reduce over the key slots of the wave, then over waves via LDS
 #pragma unroll
     for (int gi = 0; gi < kMaxGroup; gi++) {
         if (gi >= G) continue;
 #pragma unroll
-        for (int off = LPT; off < 64; off <<= 1) {
-            l[gi] += __shfl_xor(l[gi], off, 64);
+        for (int off = LPT; off < 64; off <<= 1)
 #pragma unroll
             for (int j = 0; j < 8; j++) o[gi][j] += __shfl_xor(o[gi][j], off, 64);
-        }
     }
     if (lane < LPT) {
 #pragma unroll
@@ -419,7 +452,6 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnParams a) {
             if (gi >= G) continue;
 #pragma unroll
             for (int j = 0; j < 8; j++) red_o[wave][gi][dl * 8 + j] = o[gi][j];
-            if (dl == 0) red_l[wave][gi] = l[gi];
         }
     }
     __syncthreads();
@@ -428,8 +460,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnParams a) {
         for (int idx = tid; idx < G * HD; idx += 256) {
             const int gi = idx / HD, d = idx % HD;
             const float ov = red_o[0][gi][d] + red_o[1][gi][d] + red_o[2][gi][d] + red_o[3][gi][d];
-            const float lv = red_l[0][gi] + red_l[1][gi] + red_l[2][gi] + red_l[3][gi];
-            a.out[m * (int64_t)nq * HD + (int64_t)(g * G + gi) * HD + d] = f2bf(ov / lv);
+            a.out[m * (int64_t)nq * HD + (int64_t)(g * G + gi) * HD + d] = f2bf(ov / stat_l[gi]);
         }
         return;
     }
@@ -438,11 +469,11 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnParams a) {
         const int64_t pi = (m * nq + g * G + gi) * (int64_t)a.nsplit_max + s;
         a.part_o[pi * HD + d] = red_o[0][gi][d] + red_o[1][gi][d] + red_o[2][gi][d] + red_o[3][gi][d];
         if (d == 0) {
-            a.part_ml[pi * 2] = mx[gi];
-            a.part_ml[pi * 2 + 1] = red_l[0][gi] + red_l[1][gi] + red_l[2][gi] + red_l[3][gi];
+            a.part_ml[pi * 2] = stat_m[gi];
+            a.part_ml[pi * 2 + 1] = stat_l[gi];
         }
     }
-    // ---------------- publish this split, last arriver combines (release / acquire)
+    // ---------------- publish this split; the last arriver combines (release / acquire)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     unsigned* cnt = a.counters + m * a.nkv + g;
@@ -457,20 +488,247 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnParams a) {
     if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    for (int idx = tid; idx < G * HD; idx += 256) {
-        const int gi = idx / HD, d = idx % HD;
+    // combine weights: cw[gi][j] = exp(m_j - M) / sum_j l_j exp(m_j - M)
+    for (int idx = tid; idx < G * nsplit; idx += 256) {
+        const int gi = idx / nsplit, j = idx % nsplit;
+        cw[gi][j] = a.part_ml[((m * nq + g * G + gi) * (int64_t)a.nsplit_max + j) * 2];
+    }
+    __syncthreads();
+    if (tid < G) {
+        const int gi = tid;
         const int64_t base = (m * nq + g * G + gi) * (int64_t)a.nsplit_max;
         float mm = -INFINITY;
-        for (int j = 0; j < nsplit; j++) mm = fmaxf(mm, a.part_ml[(base + j) * 2]);
-        float lv = 0.f, ov = 0.f;
+        for (int j = 0; j < nsplit; j++) mm = fmaxf(mm, cw[gi][j]);
+        float lv = 0.f;
         for (int j = 0; j < nsplit; j++) {
-            const float c = expf(a.part_ml[(base + j) * 2] - mm);
+            const float c = expf(cw[gi][j] - mm);
+            cw[gi][j] = c;
             lv += a.part_ml[(base + j) * 2 + 1] * c;
-            ov += a.part_o[(base + j) * HD + d] * c;
         }
-        a.out[m * (int64_t)nq * HD + (int64_t)(g * G + gi) * HD + d] = f2bf(ov / lv);
+        const float inv = 1.0f / lv;
+        for (int j = 0; j < nsplit; j++) cw[gi][j] *= inv;
+    }
+    __syncthreads();
+    for (int idx = tid; idx < G * (HD / 4); idx += 256) {
+        const int gi = idx / (HD / 4), d4 = idx % (HD / 4);
+        const float4* src = reinterpret_cast<const float4*>(a.part_o) +
+                            ((m * nq + g * G + gi) * (int64_t)a.nsplit_max) * (HD / 4) + d4;
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int j0 = 0; j0 < nsplit; j0 += 16) {
+            float4 v[16];
+#pragma unroll
+            for (int jj = 0; jj < 16; jj++)
+                if (j0 + jj < nsplit) v[jj] = src[(int64_t)(j0 + jj) * (HD / 4)];
+#pragma unroll
+            for (int jj = 0; jj < 16; jj++) {
+                if (j0 + jj >= nsplit) continue;
+                const float c = cw[gi][j0 + jj];
+                acc.x = fmaf(c, v[jj].x, acc.x);
+                acc.y = fmaf(c, v[jj].y, acc.y);
+                acc.z = fmaf(c, v[jj].z, acc.z);
+                acc.w = fmaf(c, v[jj].w, acc.w);
+            }
+        }
+        uint16_t* dst = a.out + m * (int64_t)nq * HD + (int64_t)(g * G + gi) * HD + d4 * 4;
+        *reinterpret_cast<uint2*>(dst) = make_uint2(pack2(acc.x, acc.y), pack2(acc.z, acc.w));
     }
     if (tid == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---------------------------------------------------------------------------
+// Prefill: causal flash attention on MFMA (v_mfma_f32_16x16x32_bf16).
+// Workgroup = 4 waves = 64 query rows of ONE q head (16 rows per wave); K/V
+// tiles of 64 keys staged in LDS (double-buffered, register prefetch).
+//   S^T = K . Q^T  — A = K tile (row = key, k = d) from an XOR-swizzled LDS image,
+//                    B = Q^T from registers (lane: q = lane & 15, 8 contiguous d);
+//                    so each lane holds 4 keys x 4 key-tiles of ONE query row and
+//                    the softmax row statistics need only lanes l, l^16, l^32, l^48.
+//   O  += P . V    — A = P straight from the S^T accumulators (bf16), k permuted as
+//                    key(j) = 32c + 4g + j (j < 4), 32c + 16 + 4g + (j - 4);
+//                    B = V with the SAME key permutation, read by two
+//                    ds_read_b64_tr_b16 per fragment from a row-major V image.
+// Scores: dot / sqrtf(hd) (fp32), masked keys (> query position) get -inf (the
+// reference's -1e9, self_attension.cu:88-92, underflows to the same 0).
+struct PrefillAttnParams {
+    const uint16_t* q;       // [M][nq*HD]
+    const int32_t* pos;      // [M]; non-decreasing within each sequence's rows
+    int rows_per_seq;
+    const uint16_t* kc;
+    const uint16_t* vc;
+    int64_t seq_stride;
+    int layer, nkv, nq, max_ctx;
+    int64_t M;
+    uint16_t* out;
+};
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef short i16x4_t __attribute__((ext_vector_type(4)));
+
+template <int HD>
+__global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(PrefillAttnParams a) {
+    constexpr int KT = 64;                 // keys per tile
+    constexpr int CPR = HD / 8;            // 16-byte chunks per row
+    constexpr int KSTEPS = HD / 32;        // MFMA k-steps over d for S
+    constexpr int DT = HD / 16;            // output d tiles
+    constexpr int CHUNKS = KT * CPR;       // per tile per operand
+    constexpr int LPT = CHUNKS / 256;      // chunk loads per thread per operand
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint16_t* Ks = reinterpret_cast<uint16_t*>(smem);                  // [2][KT][HD] swizzled
+    uint16_t* Vs = reinterpret_cast<uint16_t*>(smem + 2 * KT * HD * 2);  // [2][KT][HD] plain
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int fr = lane & 15, g = lane >> 4;
+    const int h = blockIdx.y, seq = blockIdx.z;
+    const int ntiles_q = (a.rows_per_seq + 63) / 64;
+    const int qt = ntiles_q - 1 - (int)blockIdx.x;         // heaviest (latest) rows first
+    const int64_t row0 = (int64_t)seq * a.rows_per_seq;
+    const int rlo = qt * 64, rhi = min(a.rows_per_seq, rlo + 64);
+    const int G = a.nq / a.nkv, kvh = h / G;
+    const int64_t head_off = (((int64_t)a.layer * a.nkv + kvh) * a.max_ctx) * HD;
+    const uint16_t* kb = a.kc + seq * a.seq_stride + head_off;
+    const uint16_t* vb = a.vc + seq * a.seq_stride + head_off;
+    const int kmax = a.pos[row0 + rhi - 1];                // last key any row of the block needs
+    const int nkt = kmax / KT + 1;
+
+    // this lane's query row (B operand column) and its position
+    const int qrow = min(rlo + wave * 16 + fr, rhi - 1);
+    const int qpos = a.pos[row0 + qrow];
+    bf16x8_t qf[KSTEPS];
+    {
+        const uint16_t* qp = a.q + (row0 + qrow) * (int64_t)a.nq * HD + (int64_t)h * HD;
+#pragma unroll
+        for (int ks = 0; ks < KSTEPS; ks++) qf[ks] = *reinterpret_cast<const bf16x8_t*>(qp + ks * 32 + g * 8);
+    }
+
+    uint4 rk[LPT], rv[LPT];
+    auto gload = [&](int kt) {
+#pragma unroll
+        for (int i = 0; i < LPT; i++) {
+            const int c = tid + 256 * i;
+            const int key = min(kt * KT + c / CPR, kmax);
+            const int ch = c % CPR;
+            rk[i] = *reinterpret_cast<const uint4*>(kb + (int64_t)key * HD + ch * 8);
+            rv[i] = *reinterpret_cast<const uint4*>(vb + (int64_t)key * HD + ch * 8);
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < LPT; i++) {
+            const int c = tid + 256 * i;
+            const int r = c / CPR, ch = c % CPR;
+            *reinterpret_cast<uint4*>(Ks + buf * KT * HD + r * HD + ((ch ^ (r & (CPR - 1))) * 8)) = rk[i];
+            *reinterpret_cast<uint4*>(Vs + buf * KT * HD + r * HD + ch * 8) = rv[i];
+        }
+    };
+
+    f32x4_t oacc[DT];
+#pragma unroll
+    for (int d = 0; d < DT; d++) oacc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    float m_run = -INFINITY, l_run = 0.f;
+    const float scale = sqrtf((float)HD);
+
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    int cur = 0;
+    for (int kt = 0; kt < nkt; kt++) {
+        if (kt + 1 < nkt) gload(kt + 1);
+        const uint16_t* K = Ks + cur * KT * HD;
+        const uint16_t* Vt = Vs + cur * KT * HD;
+        // ---- S^T = K . Q^T   (4 key tiles of 16)
+        f32x4_t sacc[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            sacc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+            const int r = t * 16 + fr;
+#pragma unroll
+            for (int ks = 0; ks < KSTEPS; ks++) {
+                const int ch = ks * 4 + g;
+                const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(K + r * HD + ((ch ^ (r & (CPR - 1))) * 8));
+                sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], sacc[t], 0, 0, 0);
+            }
+        }
+        // ---- online softmax over this tile (row = this lane's query)
+        float sv[4][4];
+        float mt = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int key = kt * KT + t * 16 + g * 4 + r;
+                const float sc = key <= qpos ? sacc[t][r] / scale : -INFINITY;
+                sv[t][r] = sc;
+                mt = fmaxf(mt, sc);
+            }
+        mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+        mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+        const float m_new = fmaxf(m_run, mt);
+        const float alpha = expf(m_run - m_new);   // 0 on the first tile
+        float ls = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const float e = expf(sv[t][r] - m_new);
+                sv[t][r] = e;
+                ls += e;
+            }
+        ls += __shfl_xor(ls, 16, 64);
+        ls += __shfl_xor(ls, 32, 64);
+        l_run = l_run * alpha + ls;
+        m_run = m_new;
+        // ---- rescale O rows (q = 4g + r) by their alpha
+        float ar[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) ar[r] = __shfl(alpha, g * 4 + r, 64);
+#pragma unroll
+        for (int d = 0; d < DT; d++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) oacc[d][r] *= ar[r];
+        // ---- O += P . V
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+            bf16x8_t pa;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                pa[j] = (__bf16)sv[2 * c][j];
+                pa[4 + j] = (__bf16)sv[2 * c + 1][j];
+            }
+            const int q4 = fr >> 2, p4 = fr & 3;
+#pragma unroll
+            for (int d = 0; d < DT; d++) {
+                const uint16_t* a0 = Vt + (32 * c + 4 * g + q4) * HD + 16 * d + 4 * p4;
+                const uint16_t* a1 = a0 + 16 * HD;
+                i16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (__attribute__((address_space(3))) i16x4_t*)(a0));
+                i16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (__attribute__((address_space(3))) i16x4_t*)(a1));
+                bf16x8_t vb8;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    vb8[j] = __builtin_bit_cast(__bf16, v0[j]);
+                    vb8[4 + j] = __builtin_bit_cast(__bf16, v1[j]);
+                }
+                oacc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb8, oacc[d], 0, 0, 0);
+            }
+        }
+        if (kt + 1 < nkt) lstore(cur ^ 1);
+        __syncthreads();
+        cur ^= 1;
+    }
+    // ---- normalise and store rows q = 4g + r of this wave
+    float lr[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) lr[r] = __shfl(l_run, g * 4 + r, 64);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int row = rlo + wave * 16 + g * 4 + r;
+        if (row >= rhi) continue;
+        uint16_t* orow = a.out + (row0 + row) * (int64_t)a.nq * HD + (int64_t)h * HD;
+#pragma unroll
+        for (int d = 0; d < DT; d++) orow[16 * d + fr] = f2bf(oacc[d][r] / lr[r]);
+    }
 }
 
 static int attn_nsplit(int64_t M, int32_t max_ctx) {
@@ -507,6 +765,29 @@ int qie_attention(const void* q, int64_t M, const int32_t* pos, int32_t rows_per
                 "qie_attention: n_heads/n_kv_heads must be an integer <= %d", kMaxGroup);
     QIE_REQUIRE(layer >= 0 && layer < cache->n_layers, "qie_attention: bad layer");
     if (M == 0) return 0;
+    if (rows_per_seq >= 32 && M % rows_per_seq == 0 && !getenv("QIE_ATTN_NO_MFMA")) {
+        PrefillAttnParams pa;
+        pa.q = (const uint16_t*)q;
+        pa.pos = pos;
+        pa.rows_per_seq = rows_per_seq;
+        pa.kc = (const uint16_t*)cache->k;
+        pa.vc = (const uint16_t*)cache->v;
+        pa.seq_stride = cache->seq_stride;
+        pa.layer = layer;
+        pa.nkv = cache->n_kv_heads;
+        pa.nq = n_heads;
+        pa.max_ctx = cache->max_ctx;
+        pa.M = M;
+        pa.out = (uint16_t*)out;
+        dim3 grid((unsigned)((rows_per_seq + 63) / 64), (unsigned)n_heads, (unsigned)(M / rows_per_seq));
+        const size_t shm = (size_t)2 * 2 * 64 * cache->head_dim * 2;
+        if (cache->head_dim == 128)
+            hipLaunchKernelGGL(attn_prefill_mfma_kernel<128>, grid, dim3(256), shm, (hipStream_t)stream, pa);
+        else
+            hipLaunchKernelGGL(attn_prefill_mfma_kernel<64>, grid, dim3(256), shm, (hipStream_t)stream, pa);
+        QIE_LAUNCH_CHECK();
+        return 0;
+    }
     AttnParams a;
     a.q = (const uint16_t*)q;
     a.pos = pos;
@@ -541,7 +822,7 @@ int qie_attention(const void* q, int64_t M, const int32_t* pos, int32_t rows_per
 
 int64_t qie_attention_decode_workspace_bytes(int64_t B, int32_t n_heads, int32_t n_kv_heads, int32_t head_dim,
                                              int32_t max_ctx) {
-    const int64_t ns = (max_ctx + kDecChunk - 1) / kDecChunk;
+    const int64_t ns = dec_nsplit_target(max_ctx, head_dim);
     const int64_t cnt = ((B * n_kv_heads * 4 + 255) / 256) * 256;
     return cnt + B * n_heads * ns * (head_dim + 2) * 4;
 }
@@ -570,7 +851,8 @@ int qie_attention_decode(const void* qkv, int64_t B, const int32_t* pos, const v
     a.nkv = cache->n_kv_heads;
     a.nq = n_heads;
     a.max_ctx = cache->max_ctx;
-    a.nsplit_max = (cache->max_ctx + kDecChunk - 1) / kDecChunk;
+    a.nsplit_max = dec_nsplit_target(cache->max_ctx, cache->head_dim);
+    QIE_REQUIRE(a.nsplit_max <= kDecMaxSplits, "qie_attention_decode: max_ctx %d too long", cache->max_ctx);
     a.eps = eps;
     a.numerics = numerics;
     const int64_t cnt = ((B * a.nkv * 4 + 255) / 256) * 256;

@@ -28,5 +28,12 @@ def qlib():
     return _lib.load()
 
 
+@pytest.fixture(autouse=True)
+def _release_device_buffers():
+    yield
+    import gpu_util
+    gpu_util.release_all()
+
+
 def rng(seed=0):
     return np.random.default_rng(seed)

@@ -49,14 +49,27 @@ class DBuf:
             pass
 
 
+# Every buffer made by dev()/zeros() stays alive until release_all() (called after each
+# test): `p(dev(x))` would otherwise free the allocation before the kernel runs and let
+# the next allocation reuse its address.
+_LIVE = []
+
+
+def release_all():
+    _LIVE.clear()
+
+
 def dev(a: np.ndarray) -> DBuf:
     a = np.ascontiguousarray(a)
-    return DBuf(a.shape, a.dtype).upload(a)
+    b = DBuf(a.shape, a.dtype).upload(a)
+    _LIVE.append(b)
+    return b
 
 
 def zeros(shape, dtype=np.uint16) -> DBuf:
     b = DBuf(shape, dtype)
     check(L().qie_memset(b.ptr, 0, b.nbytes), "memset")
+    _LIVE.append(b)
     return b
 
 

@@ -44,7 +44,7 @@ def test_rmsnorm(oracle, qlib, rows, H, num):
     y = G.zeros_bf16(rows, H)
     dx, dw = G.dev(x), G.dev(w)
     G.check(qlib.qie_rmsnorm(G.p(dx), G.p(dw), G.p(y), rows, H, eps, 0 if num == "ref" else 1, None))
-    G.assert_bf16_close(G.host_bf16(y), want, max_ulp=1, min_exact=0.98, what="rmsnorm")
+    G.assert_bf16_close(G.host_bf16(y), want, max_ulp=1 if num == "ref" else 2, min_exact=0.98, what="rmsnorm")
 
 
 # --------------------------------------------------------------------------- linear
@@ -99,9 +99,14 @@ def test_linear_residual(oracle, qlib, M, K, N):
     y = G.dev(res)
     _linear(qlib, G.dev(x), [(G.dev(w), N)], [], M, K, N, y, _lib.QIE_EPI_RESIDUAL)
     got = G.host_bf16(y)
-    # residual adds one more rounding on top of the bf16(acc) that may differ by 1 ulp
-    d = G.ulp_diff(got, want)
-    assert (d <= 1).mean() > 0.995 and d.max() <= 2, f"max {d.max()}"
+    # y = bf16(res + bf16(acc)): the inner bf16(acc) may differ by 1 ulp of |acc| (fp32
+    # summation order), then one more rounding at |y| — absolute bound, since res + acc
+    # can cancel to far below either operand.
+    acc = G.bf(oracle.matmul(x, w)).astype(np.float64)
+    tol = 2.0 ** -8 * np.abs(acc) + 2.0 ** -8 * np.abs(G.bf(want)) + 1e-5 * _abs_scale(oracle, x, w)
+    err = np.abs(G.bf(got).astype(np.float64) - G.bf(want))
+    assert (err <= tol).all(), f"worst {(err - tol).max()}"
+    assert (G.ulp_diff(got, want) == 0).mean() > 0.99
 
 
 @pytest.mark.parametrize("M", [1, 2, 8, 17, 128])
@@ -115,7 +120,13 @@ def test_linear_swiglu(oracle, qlib, M, K, I):
     _linear(qlib, G.dev(x), [(G.dev(wg), I), (G.dev(wu), I)], [], M, K, I, y, _lib.QIE_EPI_SWIGLU)
     got = G.host_bf16(y)
     d = G.ulp_diff(got, want)
-    assert (d == 0).mean() > 0.97 and d.max() <= 3, f"max {d.max()}"
+    assert (d == 0).mean() > 0.97
+    # elements off by > 2 ulps must be ill-conditioned: a gate/up sum that cancels to
+    # < 1 % of sum|x*w|, where fp32 summation order alone moves many bf16 ulps
+    g = np.abs(G.bf(oracle.matmul(x, wg)).astype(np.float64))
+    u = np.abs(G.bf(oracle.matmul(x, wu)).astype(np.float64))
+    ill = (g < 1e-2 * _abs_scale(oracle, x, wg)) | (u < 1e-2 * _abs_scale(oracle, x, wu))
+    assert not ((d > 2) & ~ill).any(), f"well-conditioned element off by {d[~ill].max()} ulps"
 
 
 @pytest.mark.parametrize("M", [1, 3, 8])
@@ -133,7 +144,8 @@ def test_linear_fused_norm_and_argmax(oracle, qlib, M, num):
     _linear(qlib, G.dev(x), [(G.dev(w), N)], [], M, K, N, y, _lib.QIE_EPI_STORE, norm_w=G.dev(nw), eps=eps,
             num=0 if num == "ref" else 1, keys=keys)
     got = G.host_bf16(y)
-    G.assert_sum_close(got, want, _abs_scale(oracle, xn, w) * 2, rel=2e-5, what="fused norm")
+    # the fused RMSNorm may round a few normalised activations 1 ulp differently (sum order)
+    G.assert_sum_close(got, want, _abs_scale(oracle, xn, w), rel=1e-4, what="fused norm")
     ids = G.zeros((M,), np.int32)
     G.check(qlib.qie_keys_to_ids(G.p(keys), M, G.p(ids), None))
     for m in range(M):   # fused arg-max == reference rule on the kernel's own logits

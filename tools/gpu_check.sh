@@ -16,4 +16,12 @@ rc=$?; tail -2 gpurun_out/smoke.log; echo "smoke rc=$rc"
 [ "${SKIP_BENCH:-0}" = "1" ] && exit 0
 timeout -k 10 ${BENCH_TIMEOUT:-600} python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
 rc=$?; tail -3 gpurun_out/bench.log; echo "bench rc=$rc"
+[ $rc -eq 0 ] || exit $rc
+if [ "${PROFILE:-0}" = "1" ]; then
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof" \
+      -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 64 --warmup 4 --prefill-iters 1 --no-cpu-baseline \
+      > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1
+  rc=$?; echo "rocprof rc=$rc"; cd "$GRAFT_REPO_ROOT"
+fi
 exit $rc

@@ -216,6 +216,8 @@ struct DecodeAttnParams {
     uint16_t* vc;
     int64_t seq_stride;
     int layer, nkv, nq, max_ctx, nsplit_max;
+    int splits_target;        // ~splits per (row, kv head) at long context
+    int dbg;                  // timing experiments only (QIE_DEC_DBG): 1 no combine, 2 no release, 4 no acquire
     float eps;
     int numerics;
     float* part_o;            // [B][nq][nsplit_max][HD]
@@ -233,12 +235,18 @@ constexpr int kDecNtMax = 16;        // keys per thread per split
 constexpr int kDecMaxSplits = 160;
 
 __host__ __device__ __forceinline__ int dec_tpb(int hd) { return 256 / (hd / 8); }
-__host__ __device__ __forceinline__ int dec_nsplit_target(int ctx, int hd) {
+__host__ __device__ __forceinline__ int dec_nsplit_target(int ctx, int hd, int splits = kDecSplits) {
     const int by_min = (ctx + kDecMinKeys - 1) / kDecMinKeys;
     const int cap = kDecNtMax * dec_tpb(hd);
     const int by_cap = (ctx + cap - 1) / cap;
-    const int want = by_cap > kDecSplits ? by_cap : kDecSplits;
+    const int want = by_cap > splits ? by_cap : splits;
     return by_min < want ? by_min : want;
+}
+
+static int dec_splits_env() {
+    const char* e = getenv("QIE_DEC_SPLITS");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : kDecSplits;
 }
 
 template <int HD>
@@ -260,7 +268,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnParams a) {
     const int g = blockIdx.x / a.nsplit_max, s = blockIdx.x % a.nsplit_max;
     const int G = a.nq / a.nkv;
     const int p = a.pos[m], ctx = p + 1;
-    const int nst = dec_nsplit_target(ctx, HD);
+    const int nst = dec_nsplit_target(ctx, HD, a.splits_target);
     int chunk = (ctx + nst - 1) / nst;
     chunk = (chunk + TPB - 1) / TPB * TPB;
     const int nsplit = (ctx + chunk - 1) / chunk;
@@ -476,16 +484,17 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnParams a) {
     // ---------------- publish this split; the last arriver combines (release / acquire)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (a.dbg & 1) return;
     unsigned* cnt = a.counters + m * a.nkv + g;
     if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (!(a.dbg & 2)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         last_flag = (old == (unsigned)nsplit - 1) ? 1 : 0;
     }
     __syncthreads();
     if (!last_flag) return;
-    if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (tid == 0 && !(a.dbg & 4)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     // combine weights: cw[gi][j] = exp(m_j - M) / sum_j l_j exp(m_j - M)
@@ -559,6 +568,7 @@ struct PrefillAttnParams {
     int layer, nkv, nq, max_ctx;
     int64_t M;
     uint16_t* out;
+    int no_tr;               // diagnostics (QIE_ATTN_NO_TR): V fragments by scalar LDS reads
 };
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -700,15 +710,23 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(PrefillAttnParam
             for (int d = 0; d < DT; d++) {
                 const uint16_t* a0 = Vt + (32 * c + 4 * g + q4) * HD + 16 * d + 4 * p4;
                 const uint16_t* a1 = a0 + 16 * HD;
-                i16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                    (__attribute__((address_space(3))) i16x4_t*)(a0));
-                i16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                    (__attribute__((address_space(3))) i16x4_t*)(a1));
                 bf16x8_t vb8;
+                if (a.no_tr) {
 #pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    vb8[j] = __builtin_bit_cast(__bf16, v0[j]);
-                    vb8[4 + j] = __builtin_bit_cast(__bf16, v1[j]);
+                    for (int j = 0; j < 4; j++) {
+                        vb8[j] = __builtin_bit_cast(__bf16, Vt[(32 * c + 4 * g + j) * HD + 16 * d + fr]);
+                        vb8[4 + j] = __builtin_bit_cast(__bf16, Vt[(32 * c + 16 + 4 * g + j) * HD + 16 * d + fr]);
+                    }
+                } else {
+                    i16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (__attribute__((address_space(3))) i16x4_t*)(a0));
+                    i16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (__attribute__((address_space(3))) i16x4_t*)(a1));
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        vb8[j] = __builtin_bit_cast(__bf16, v0[j]);
+                        vb8[4 + j] = __builtin_bit_cast(__bf16, v1[j]);
+                    }
                 }
                 oacc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb8, oacc[d], 0, 0, 0);
             }
@@ -779,6 +797,7 @@ int qie_attention(const void* q, int64_t M, const int32_t* pos, int32_t rows_per
         pa.max_ctx = cache->max_ctx;
         pa.M = M;
         pa.out = (uint16_t*)out;
+        pa.no_tr = getenv("QIE_ATTN_NO_TR") ? 1 : 0;
         dim3 grid((unsigned)((rows_per_seq + 63) / 64), (unsigned)n_heads, (unsigned)(M / rows_per_seq));
         const size_t shm = (size_t)2 * 2 * 64 * cache->head_dim * 2;
         if (cache->head_dim == 128)
@@ -822,7 +841,7 @@ int qie_attention(const void* q, int64_t M, const int32_t* pos, int32_t rows_per
 
 int64_t qie_attention_decode_workspace_bytes(int64_t B, int32_t n_heads, int32_t n_kv_heads, int32_t head_dim,
                                              int32_t max_ctx) {
-    const int64_t ns = dec_nsplit_target(max_ctx, head_dim);
+    const int64_t ns = kDecMaxSplits;   // any splits_target fits
     const int64_t cnt = ((B * n_kv_heads * 4 + 255) / 256) * 256;
     return cnt + B * n_heads * ns * (head_dim + 2) * 4;
 }
@@ -851,7 +870,9 @@ int qie_attention_decode(const void* qkv, int64_t B, const int32_t* pos, const v
     a.nkv = cache->n_kv_heads;
     a.nq = n_heads;
     a.max_ctx = cache->max_ctx;
-    a.nsplit_max = dec_nsplit_target(cache->max_ctx, cache->head_dim);
+    a.splits_target = dec_splits_env();
+    a.dbg = getenv("QIE_DEC_DBG") ? atoi(getenv("QIE_DEC_DBG")) : 0;
+    a.nsplit_max = dec_nsplit_target(cache->max_ctx, cache->head_dim, a.splits_target);
     QIE_REQUIRE(a.nsplit_max <= kDecMaxSplits, "qie_attention_decode: max_ctx %d too long", cache->max_ctx);
     a.eps = eps;
     a.numerics = numerics;

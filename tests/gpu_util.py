@@ -112,10 +112,10 @@ def assert_bf16_close(got, want, max_ulp=1, min_exact=0.98, what=""):
         f"{what}: max ulp {d.max()}, exact fraction {exact:.4f}"
 
 
-def assert_sum_close(got, want, abs_scale, rel=1e-5, what=""):
-    """|got - want| <= max(1 bf16 ulp of want, rel * sum|a*w|) element-wise."""
+def assert_sum_close(got, want, abs_scale, rel=1e-5, ulps=1, what=""):
+    """|got - want| <= max(ulps bf16 ulps of want, rel * sum|a*w|) element-wise."""
     g, w = bf(got).astype(np.float64), bf(want).astype(np.float64)
-    ulp = np.maximum(np.abs(w), 1e-30) * 2.0 ** -7
+    ulp = ulps * np.maximum(np.abs(w), 1e-30) * 2.0 ** -7
     tol = np.maximum(ulp, rel * abs_scale)
     bad = np.abs(g - w) > tol
     assert not bad.any(), f"{what}: {bad.sum()} / {bad.size} outside tolerance; worst " \

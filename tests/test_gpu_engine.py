@@ -172,3 +172,15 @@ def test_qwen2_0_5b_config1_greedy_matches_oracle(oracle):
     prompt = list(rng(1).integers(0, spec.vocab, 16))
     ids, flips = forced_compare(oracle, eng.batch(1, 64), om, prompt, 16)
     assert flips <= 2
+
+
+@pytest.mark.slow
+def test_qwen2_7b_widths_two_layers_match_oracle(oracle):
+    """Full Qwen2-7B widths (H 3584, I 18944, 28/4 heads, V 152064), 2 layers: any
+    7B-shape-specific kernel bug shows here at the tight tolerance, independent of the
+    drift that 28 layers of fp32 reordering accumulate in the full model."""
+    spec = S.QWEN2_7B.replace(n_layers=2)
+    eng, hw, om = make_pair(spec, oracle, max_ctx=64, syn=W.SynthParams(seed=0))
+    prompt = list(rng(2).integers(0, spec.vocab, 24))
+    ids, flips = forced_compare(oracle, eng.batch(1, 64), om, prompt, 6)
+    assert flips <= 2

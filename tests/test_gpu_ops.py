@@ -103,7 +103,7 @@ def test_linear_residual(oracle, qlib, M, K, N):
     # summation order), then one more rounding at |y| — absolute bound, since res + acc
     # can cancel to far below either operand.
     acc = G.bf(oracle.matmul(x, w)).astype(np.float64)
-    tol = 2.0 ** -8 * np.abs(acc) + 2.0 ** -8 * np.abs(G.bf(want)) + 1e-5 * _abs_scale(oracle, x, w)
+    tol = 2.0 ** -7 * (np.abs(acc) + np.abs(G.bf(want))) + 1e-5 * _abs_scale(oracle, x, w)
     err = np.abs(G.bf(got).astype(np.float64) - G.bf(want))
     assert (err <= tol).all(), f"worst {(err - tol).max()}"
     assert (G.ulp_diff(got, want) == 0).mean() > 0.99
@@ -122,10 +122,12 @@ def test_linear_swiglu(oracle, qlib, M, K, I):
     d = G.ulp_diff(got, want)
     assert (d == 0).mean() > 0.97
     # elements off by > 2 ulps must be ill-conditioned: a gate/up sum that cancels to
-    # < 1 % of sum|x*w|, where fp32 summation order alone moves many bf16 ulps
-    g = np.abs(G.bf(oracle.matmul(x, wg)).astype(np.float64))
+    # < 1 % of sum|x*w| (fp32 summation order alone moves many bf16 ulps), or a gate
+    # g < -4 where silu(g) = g*sigmoid(g) amplifies a relative error of g by |1 + g(1-sig)|
+    gs = G.bf(oracle.matmul(x, wg)).astype(np.float64)
+    g = np.abs(gs)
     u = np.abs(G.bf(oracle.matmul(x, wu)).astype(np.float64))
-    ill = (g < 1e-2 * _abs_scale(oracle, x, wg)) | (u < 1e-2 * _abs_scale(oracle, x, wu))
+    ill = (g < 1e-2 * _abs_scale(oracle, x, wg)) | (u < 1e-2 * _abs_scale(oracle, x, wu)) | (gs < -4)
     assert not ((d > 2) & ~ill).any(), f"well-conditioned element off by {d[~ill].max()} ulps"
 
 
@@ -144,8 +146,10 @@ def test_linear_fused_norm_and_argmax(oracle, qlib, M, num):
     _linear(qlib, G.dev(x), [(G.dev(w), N)], [], M, K, N, y, _lib.QIE_EPI_STORE, norm_w=G.dev(nw), eps=eps,
             num=0 if num == "ref" else 1, keys=keys)
     got = G.host_bf16(y)
-    # the fused RMSNorm may round a few normalised activations 1 ulp differently (sum order)
-    G.assert_sum_close(got, want, _abs_scale(oracle, xn, w), rel=1e-4, what="fused norm")
+    # the fused RMSNorm may round a few normalised activations 1 ulp differently (sum order);
+    # HF numerics round twice (bf16(w * bf16(x/rms))), so allow 2 output ulps there
+    G.assert_sum_close(got, want, _abs_scale(oracle, xn, w), rel=1e-4, ulps=1 if num == "ref" else 2,
+                       what="fused norm")
     ids = G.zeros((M,), np.int32)
     G.check(qlib.qie_keys_to_ids(G.p(keys), M, G.p(ids), None))
     for m in range(M):   # fused arg-max == reference rule on the kernel's own logits
@@ -353,7 +357,9 @@ def test_attention_decode_fused(oracle, qlib, hd, qkn, num, nq, nkv):
         for b in range(B):
             p = pos[b]
             for g in range(nkv):
-                G.assert_bf16_close(hk[b, layer, g, p], k[b, g * hd:(g + 1) * hd], 1, 0.9 if qkn else 1.0, "k")
+                # qk-norm sum order may flip one rounding; HF rounds twice (2 ulps)
+                G.assert_bf16_close(hk[b, layer, g, p], k[b, g * hd:(g + 1) * hd], 1 if num == "ref" else 2,
+                                    0.9 if qkn else 1.0, "k")
                 assert np.array_equal(hv[b, layer, g, p], v[b, g * hd:(g + 1) * hd])
             kk = kc_h[b, layer, :, :p + 1].copy()
             vv = vc_h[b, layer, :, :p + 1].copy()

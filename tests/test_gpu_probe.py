@@ -1,0 +1,72 @@
+"""GPU structure probes for the MFMA flash-attention prefill kernel: inputs chosen so each
+stage (P.V, Q.K^T + softmax) is checked in isolation against closed forms."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+import gpu_util as G
+
+from qwen_inference_engine_amd._lib import KvCacheC
+
+pytestmark = pytest.mark.gpu
+
+
+def run_prefill_attn(qlib, q, k, v, hd, nq, nkv):
+    P = q.shape[0]
+    maxc = max(64, P)
+    kc = np.zeros((1, 1, nkv, maxc, hd), np.uint16)
+    vc = np.zeros_like(kc)
+    kc[0, 0, :, :P] = k
+    vc[0, 0, :, :P] = v
+    dk, dv = G.dev(kc), G.dev(vc)
+    c = KvCacheC()
+    c.k, c.v, c.seq_stride = dk.ptr, dv.ptr, nkv * maxc * hd
+    c.n_layers, c.n_kv_heads, c.head_dim, c.max_ctx = 1, nkv, hd, maxc
+    out = G.zeros_bf16(P, nq * hd)
+    ws = G.zeros_bytes(qlib.qie_attention_workspace_bytes(P, nq, hd, maxc))
+    G.check(qlib.qie_attention(G.p(G.dev(q)), P, G.p(G.dev(np.arange(P, dtype=np.int32))), P, C.byref(c), 0, nq,
+                               G.p(out), G.p(ws), None))
+    return G.bf(G.host_bf16(out))
+
+
+@pytest.mark.parametrize("no_tr", [False, True])
+@pytest.mark.parametrize("hd", [64, 128])
+def test_flash_pv_uniform(oracle, qlib, no_tr, hd, monkeypatch):
+    """Q = 0: every score is 0, so O[q] = mean(V[0..q])."""
+    if no_tr:
+        monkeypatch.setenv("QIE_ATTN_NO_TR", "1")
+    P = 64
+    rng = np.random.default_rng(0)
+    v = oracle.f32_to_bf16(rng.standard_normal((1, P, hd)).astype(np.float32))
+    q = np.zeros((P, hd), np.uint16)
+    k = oracle.f32_to_bf16(rng.standard_normal((1, P, hd)).astype(np.float32))
+    got = run_prefill_attn(qlib, q, k, v, hd, 1, 1)
+    vf = G.bf(v[0]).astype(np.float64)
+    want = np.cumsum(vf, 0) / np.arange(1, P + 1)[:, None]
+    err = np.abs(got - want)
+    rows = np.where(err.max(1) > 2e-2)[0]
+    assert not len(rows), f"rows {rows[:10]} wrong; first bad row err {err[rows[0]].max() if len(rows) else 0}"
+
+
+@pytest.mark.parametrize("no_tr", [False, True])
+def test_flash_probabilities_onehot_v(oracle, qlib, no_tr, monkeypatch):
+    """V[key] = e_key (hd = 64 >= P): O[q][d] = softmax probability of key d for query q."""
+    if no_tr:
+        monkeypatch.setenv("QIE_ATTN_NO_TR", "1")
+    P, hd = 48, 64
+    rng = np.random.default_rng(1)
+    q = oracle.f32_to_bf16(rng.standard_normal((P, hd)).astype(np.float32))
+    k = oracle.f32_to_bf16(rng.standard_normal((1, P, hd)).astype(np.float32))
+    v = np.zeros((1, P, hd), np.uint16)
+    for t in range(P):
+        v[0, t, t] = 0x3F80   # 1.0
+    got = run_prefill_attn(qlib, q, k, v, hd, 1, 1)
+    s = G.bf(q).astype(np.float64) @ G.bf(k[0]).astype(np.float64).T / np.sqrt(hd)
+    s[np.triu_indices(P, 1)] = -np.inf
+    p = np.exp(s - s.max(1, keepdims=True))
+    p /= p.sum(1, keepdims=True)
+    err = np.abs(got[:, :P] - p)
+    bad = np.argwhere(err > 1e-2)
+    assert not len(bad), f"{len(bad)} bad (q, key) entries, e.g. {bad[:8].tolist()}"

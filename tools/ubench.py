@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Kernel A/B micro-benchmarks on the real Qwen2-7B decode state (one process, interleaved
+rounds, cdna_hip_programming.md §5.4 rule 24).  Prints one JSON line per measurement."""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import qwen_inference_engine_amd as Q  # noqa: E402
+from qwen_inference_engine_amd import spec as S, weights as W  # noqa: E402
+
+NAMES = {0: "gate_up", 1: "down", 2: "qkv", 3: "o", 4: "lm_head", 5: "attn"}
+
+
+def main():
+    spec = S.PRESETS[os.environ.get("UB_MODEL", "Qwen2-7B")]
+    P = int(os.environ.get("UB_P", "2048"))
+    eng = Q.Engine(spec, max_ctx=P + 528).init_synthetic(W.SynthParams(seed=0))
+    b = eng.batch(1, P + 528)
+    ids = np.random.default_rng(1).integers(0, spec.vocab, P)
+    b.prefill(0, ids)
+    b.decode(256, want_ids=False)          # ctx ~2300
+    variants = [
+        ("attn", 5, {}), ("attn", 5, {"QIE_DEC_SPLITS": "4"}), ("attn", 5, {"QIE_DEC_SPLITS": "8"}),
+        ("attn", 5, {"QIE_DEC_SPLITS": "32"}), ("attn", 5, {"QIE_DEC_SPLITS": "64"}),
+        ("attn", 5, {"QIE_DEC_DBG": "1"}), ("attn", 5, {"QIE_DEC_DBG": "2"}), ("attn", 5, {"QIE_DEC_DBG": "4"}),
+        ("attn", 5, {"QIE_DEC_DBG": "6"}),
+    ]
+    for which in (0, 1, 2, 3):
+        for bpc in ("2", "4", "8"):
+            for rpw in ("2", "4"):
+                variants.append((NAMES[which], which, {"QIE_GEMV_BLOCKS_PER_CU": bpc, "QIE_GEMV_RPW": rpw}))
+    res = {}
+    for rnd in range(3):
+        for name, which, env in variants:
+            saved = {k: os.environ.get(k) for k in env}
+            os.environ.update(env)
+            us, by = b.time_kernel(which, 100)
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+            key = (name, json.dumps(env, sort_keys=True))
+            res.setdefault(key, []).append(us)
+    for (name, env), v in res.items():
+        print(json.dumps({"kernel": name, "env": json.loads(env), "us_median": round(float(np.median(v)), 3),
+                          "us_min": round(float(np.min(v)), 3)}))
+
+
+if __name__ == "__main__":
+    main()

@@ -148,6 +148,11 @@ int qie_attention_decode(const void* qkv, int64_t B, const int32_t* pos, const v
                          int32_t n_heads, const qie_kv_cache* cache, int32_t layer, float eps,
                          int32_t numerics, void* out, void* ws, void* stream);
 
+/* Diagnostics: one wave, lane l reads 8 bytes at element 4*l of an LDS array whose
+ * element i holds i, through ds_read_b64_tr_b16; out_dev[l*4 + e] receives element e
+ * of lane l (pins the transposed-read lane mapping the prefill attention relies on). */
+int qie_debug_tr16_probe(int32_t* out_dev);
+
 /* ------------------------------------------------------------- elementwise
  * launch_act + launch_elem (helpers.cuh:108-115) and launch_resadd (:116-119)
  * for callers that do not use the fused linear epilogues. */

@@ -100,6 +100,7 @@ SIGNATURES = [
     ("qie_attention_decode_workspace_bytes", C.c_int64, [_I64, _I32, _I32, _I32, _I32]),
     ("qie_attention_decode", C.c_int, [_P, _I64, _P, _P, _P, _P, _P, _I32, C.POINTER(KvCacheC), _I32, _F, _I32,
                                        _P, _P, _P]),
+    ("qie_debug_tr16_probe", C.c_int, [_P]),
     ("qie_silu_mul", C.c_int, [_P, _P, _P, _I64, _P]),
     ("qie_residual_add", C.c_int, [_P, _P, _I64, _P]),
     ("qie_sample_workspace_bytes", C.c_int64, [_I64, _I64]),

@@ -356,15 +356,18 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnParams a) {
 
     // ---------------- phase A: all K loads in flight, then scores -> p_s
     {
+        // Unconditional, index-clamped loads + branch-free select of the new row: a
+        // load under a wave-uniform runtime condition makes hipcc branch around it and
+        // wait vmcnt(0) per element (cdna_hip_programming.md §5, trap (c)).
         uint4 kr[NTMAX];
+        const uint4 knew = *reinterpret_cast<const uint4*>(&kv_new[0][dl * 8]);
 #pragma unroll
         for (int i = 0; i < NTMAX; i++) {
-            if (i < NT) {
-                const int t = t0 + grp + TPB * i;
-                const int tc = t < t1 ? t : t0;   // masked slots re-read a written row
-                kr[i] = (tc == p) ? *reinterpret_cast<const uint4*>(&kv_new[0][dl * 8])
-                                  : *reinterpret_cast<const uint4*>(kb + (int64_t)tc * HD + dl * 8);
-            }
+            const int t = t0 + grp + TPB * i;
+            const int tc = t < t1 ? t : t0;   // masked slots re-read a written row
+            const uint4 ld = *reinterpret_cast<const uint4*>(kb + (int64_t)tc * HD + dl * 8);
+            const bool nw = tc == p;
+            kr[i] = make_uint4(nw ? knew.x : ld.x, nw ? knew.y : ld.y, nw ? knew.z : ld.z, nw ? knew.w : ld.w);
         }
         float qf[kMaxGroup][8];
 #pragma unroll
@@ -419,14 +422,14 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnParams a) {
         for (int j = 0; j < 8; j++) o[gi][j] = 0.f;
     {
         uint4 vr[NTMAX];
+        const uint4 vnew = *reinterpret_cast<const uint4*>(&kv_new[1][dl * 8]);
 #pragma unroll
         for (int i = 0; i < NTMAX; i++) {
-            if (i < NT) {
-                const int t = t0 + grp + TPB * i;
-                const int tc = t < t1 ? t : t0;
-                vr[i] = (tc == p) ? *reinterpret_cast<const uint4*>(&kv_new[1][dl * 8])
-                                  : *reinterpret_cast<const uint4*>(vb + (int64_t)tc * HD + dl * 8);
-            }
+            const int t = t0 + grp + TPB * i;
+            const int tc = t < t1 ? t : t0;
+            const uint4 ld = *reinterpret_cast<const uint4*>(vb + (int64_t)tc * HD + dl * 8);
+            const bool nw = tc == p;
+            vr[i] = make_uint4(nw ? vnew.x : ld.x, nw ? vnew.y : ld.y, nw ? vnew.z : ld.z, nw ? vnew.w : ld.w);
         }
 #pragma unroll
         for (int i = 0; i < NTMAX; i++) {
@@ -749,6 +752,16 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(PrefillAttnParam
     }
 }
 
+// Diagnostics: lane l reads the 8 bytes at element 4*l of an LDS array holding
+// value == element index; out[l][e] = what ds_read_b64_tr_b16 delivered.
+__global__ void tr16_probe_kernel(int32_t* out) {
+    __shared__ __attribute__((aligned(16))) uint16_t lds[512];
+    for (int i = threadIdx.x; i < 512; i += 64) lds[i] = (uint16_t)i;
+    __syncthreads();
+    i16x4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4_t*)(lds + 4 * threadIdx.x));
+    for (int e = 0; e < 4; e++) out[threadIdx.x * 4 + e] = (uint16_t)v[e];
+}
+
 static int attn_nsplit(int64_t M, int32_t max_ctx) {
     const char* e = getenv("QIE_ATTN_SPLIT_TOKENS");
     int per = e ? atoi(e) : 0;
@@ -835,6 +848,13 @@ int qie_attention(const void* q, int64_t M, const int32_t* pos, int32_t rows_per
         QIE_LAUNCH_CHECK();
         if (a.nsplit > 1) hipLaunchKernelGGL(attn_combine_kernel<64>, dim3(n_heads, (unsigned)M), dim3(64), 0, st, a);
     }
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+
+int qie_debug_tr16_probe(int32_t* out_dev) {
+    QIE_REQUIRE(out_dev, "qie_debug_tr16_probe: null");
+    hipLaunchKernelGGL(tr16_probe_kernel, dim3(1), dim3(64), 0, nullptr, out_dev);
     QIE_LAUNCH_CHECK();
     return 0;
 }

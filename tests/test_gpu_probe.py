@@ -31,6 +31,28 @@ def run_prefill_attn(qlib, q, k, v, hd, nq, nkv):
     return G.bf(G.host_bf16(out))
 
 
+def test_tr16_lane_mapping(qlib):
+    """Records what ds_read_b64_tr_b16 delivers per lane (written to gpurun_out/) and
+    checks the mapping the flash kernel assumes: within each 16-lane group, lane
+    4q + p supplies row q / columns 4p..4p+3 of a 4 x 16 block and lane i receives
+    column i of the 4 rows (element q = row q)."""
+    out = G.zeros((64 * 4,), np.int32)
+    G.check(qlib.qie_debug_tr16_probe(G.p(out)))
+    got = G.host(out).reshape(64, 4)
+    os.makedirs("gpurun_out", exist_ok=True)
+    np.savetxt("gpurun_out/tr16_probe.txt", got, fmt="%d")
+    # element index held by LDS at (lane L, e) is 4L + e; under the assumed mapping lane
+    # i of group g receives, for element q, the value loaded by lane 16g + 4q + i//4 at
+    # position i % 4.
+    want = np.zeros_like(got)
+    for lane in range(64):
+        gq, i = lane // 16, lane % 16
+        for q in range(4):
+            src = 16 * gq + 4 * q + i // 4
+            want[lane, q] = 4 * src + i % 4
+    assert np.array_equal(got, want), "tr16 mapping differs; see gpurun_out/tr16_probe.txt"
+
+
 @pytest.mark.parametrize("no_tr", [False, True])
 @pytest.mark.parametrize("hd", [64, 128])
 def test_flash_pv_uniform(oracle, qlib, no_tr, hd, monkeypatch):

@@ -23,16 +23,13 @@ def main():
     ids = np.random.default_rng(1).integers(0, spec.vocab, P)
     b.prefill(0, ids)
     b.decode(256, want_ids=False)          # ctx ~2300
-    variants = [
-        ("attn", 5, {}), ("attn", 5, {"QIE_DEC_SPLITS": "4"}), ("attn", 5, {"QIE_DEC_SPLITS": "8"}),
-        ("attn", 5, {"QIE_DEC_SPLITS": "32"}), ("attn", 5, {"QIE_DEC_SPLITS": "64"}),
-        ("attn", 5, {"QIE_DEC_DBG": "1"}), ("attn", 5, {"QIE_DEC_DBG": "2"}), ("attn", 5, {"QIE_DEC_DBG": "4"}),
-        ("attn", 5, {"QIE_DEC_DBG": "6"}),
-    ]
-    for which in (0, 1, 2, 3):
-        for bpc in ("2", "4", "8"):
-            for rpw in ("2", "4"):
-                variants.append((NAMES[which], which, {"QIE_GEMV_BLOCKS_PER_CU": bpc, "QIE_GEMV_RPW": rpw}))
+    variants = [("attn", 5, {})]
+    for sp in ("4", "8", "12", "24", "32"):
+        variants.append(("attn", 5, {"QIE_DEC_SPLITS": sp}))
+    variants += [("attn", 5, {"QIE_DEC_DBG": "1"}), ("attn", 5, {"QIE_DEC_DBG": "6"})]
+    for which in (0, 1, 2, 3, 4):
+        variants.append((NAMES[which], which, {}))
+        variants.append((NAMES[which], which, {"QIE_GEMV_BLOCKS_PER_CU": "16"}))
     res = {}
     for rnd in range(3):
         for name, which, env in variants:

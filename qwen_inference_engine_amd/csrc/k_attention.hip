@@ -721,15 +721,14 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(PrefillAttnParam
                         vb8[4 + j] = __builtin_bit_cast(__bf16, Vt[(32 * c + 16 + 4 * g + j) * HD + 16 * d + fr]);
                     }
                 } else {
-                    i16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    const i16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                         (__attribute__((address_space(3))) i16x4_t*)(a0));
-                    i16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    const i16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                         (__attribute__((address_space(3))) i16x4_t*)(a1));
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        vb8[j] = __builtin_bit_cast(__bf16, v0[j]);
-                        vb8[4 + j] = __builtin_bit_cast(__bf16, v1[j]);
-                    }
+                    // whole-vector reinterpretation: a per-element short->__bf16 bit_cast
+                    // here was lowered (ROCm 7.2) to a v_perm_b32 that duplicated the low
+                    // half of each dword (caught by tests/test_gpu_probe.py)
+                    vb8 = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
                 }
                 oacc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb8, oacc[d], 0, 0, 0);
             }

@@ -305,8 +305,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnParams a) {
                     float ss = 0.f;
 #pragma unroll
                     for (int j = 0; j < 8; j++) ss += x[j] * x[j];
-#pragma unroll
-                    for (int off = LPT / 2; off > 0; off >>= 1) ss += __shfl_xor(ss, off, 64);
+                    ss = group_sum<LPT>(ss);
                     const float rms = sqrtf((ss / (float)HD) + a.eps);
 #pragma unroll
                     for (int j = 0; j < 8; j++) {
@@ -389,8 +388,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnParams a) {
                 float d = 0.f;
 #pragma unroll
                 for (int j = 0; j < 8; j++) d = fmaf(qf[gi][j], kf[j], d);
-#pragma unroll
-                for (int off = LPT / 2; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
+                d = group_sum<LPT>(d);
                 if (dl == 0 && tl < ntok) p_s[gi][tl] = d / scale;
             }
         }
@@ -453,9 +451,11 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnParams a) {
     for (int gi = 0; gi < kMaxGroup; gi++) {
         if (gi >= G) continue;
 #pragma unroll
-        for (int off = LPT; off < 64; off <<= 1)
-#pragma unroll
-            for (int j = 0; j < 8; j++) o[gi][j] += __shfl_xor(o[gi][j], off, 64);
+        for (int j = 0; j < 8; j++) {
+            float v = o[gi][j];
+            if constexpr (LPT == 8) v += dpp_f<0x128>(v);   // row_ror:8 == lane ^ 8
+            o[gi][j] = xor32_sum(xor16_sum(v));
+        }
     }
     if (lane < LPT) {
 #pragma unroll
@@ -674,8 +674,7 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(PrefillAttnParam
                 sv[t][r] = sc;
                 mt = fmaxf(mt, sc);
             }
-        mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
-        mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+        mt = xor32_max(xor16_max(mt));
         const float m_new = fmaxf(m_run, mt);
         const float alpha = expf(m_run - m_new);   // 0 on the first tile
         float ls = 0.f;
@@ -687,8 +686,7 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(PrefillAttnParam
                 sv[t][r] = e;
                 ls += e;
             }
-        ls += __shfl_xor(ls, 16, 64);
-        ls += __shfl_xor(ls, 32, 64);
+        ls = xor32_sum(xor16_sum(ls));
         l_run = l_run * alpha + ls;
         m_run = m_new;
         // ---- rescale O rows (q = 4g + r) by their alpha

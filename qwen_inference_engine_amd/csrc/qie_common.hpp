@@ -53,16 +53,59 @@ __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
     return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
 }
 
-template <typename T>
-__device__ __forceinline__ T wave_sum(T v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// ------------------------------------------------------ cross-lane reductions
+// __shfl_xor lowers to ds_bpermute_b32 (an LDS round trip, ~100 cycles); chains of
+// them serialised the decode attention.  These use DPP row ops (folded into the
+// VALU op, e.g. v_add_f32_dpp) within 16-lane rows and gfx950's
+// v_permlane16/32_swap across rows — no LDS traffic.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+// every lane gets op over the N-lane aligned group it belongs to (N in 2,4,8,16):
+// xor 1, xor 2 (quad_perm), then mirrored halves (row_half_mirror) and rows (row_mirror).
+template <int N>
+__device__ __forceinline__ float group_sum(float v) {
+    if constexpr (N >= 2) v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+    if constexpr (N >= 4) v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+    if constexpr (N >= 8) v += dpp_f<0x141>(v);  // row_half_mirror
+    if constexpr (N >= 16) v += dpp_f<0x140>(v); // row_mirror
     return v;
 }
-template <typename T>
-__device__ __forceinline__ T wave_max(T v) {
+template <int N>
+__device__ __forceinline__ float group_max(float v) {
+    if constexpr (N >= 2) v = fmaxf(v, dpp_f<0xB1>(v));
+    if constexpr (N >= 4) v = fmaxf(v, dpp_f<0x4E>(v));
+    if constexpr (N >= 8) v = fmaxf(v, dpp_f<0x141>(v));
+    if constexpr (N >= 16) v = fmaxf(v, dpp_f<0x140>(v));
+    return v;
+}
+// op with lane ^ 16 / lane ^ 32 (v_permlane16_swap / v_permlane32_swap on two copies)
+__device__ __forceinline__ float xor16_sum(float v) {
+    auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false, false);
+    return __builtin_bit_cast(float, r[0]) + __builtin_bit_cast(float, r[1]);
+}
+__device__ __forceinline__ float xor32_sum(float v) {
+    auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false, false);
+    return __builtin_bit_cast(float, r[0]) + __builtin_bit_cast(float, r[1]);
+}
+__device__ __forceinline__ float xor16_max(float v) {
+    auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false, false);
+    return fmaxf(__builtin_bit_cast(float, r[0]), __builtin_bit_cast(float, r[1]));
+}
+__device__ __forceinline__ float xor32_max(float v) {
+    auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false, false);
+    return fmaxf(__builtin_bit_cast(float, r[0]), __builtin_bit_cast(float, r[1]));
+}
+__device__ __forceinline__ float wave_sum(float v) { return xor32_sum(xor16_sum(group_sum<16>(v))); }
+__device__ __forceinline__ float wave_max(float v) { return xor32_max(xor16_max(group_max<16>(v))); }
+// 64-bit max (selection keys) keeps the generic shuffle path (rare, end of kernels).
+__device__ __forceinline__ unsigned long long wave_max(unsigned long long v) {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    for (int o = 32; o > 0; o >>= 1) {
+        unsigned long long t = __shfl_xor(v, o, 64);
+        v = t > v ? t : v;
+    }
     return v;
 }
 

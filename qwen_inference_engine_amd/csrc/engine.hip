@@ -717,7 +717,8 @@ int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* av
     const int64_t I = s.ffn, B = b->B;
     // scratch output so timing never disturbs the sequence state
     uint16_t* scratch = nullptr;
-    QIE_TRY(dmalloc((void**)&scratch, (size_t)B * std::max<int64_t>(std::max(I, (int64_t)s.vocab), QD + 2 * KD) * 2));
+    QIE_TRY(dmalloc((void**)&scratch,
+                    (size_t)B * std::max<int64_t>(std::max(I, (int64_t)s.vocab), QD + 2 * KD) * 2 + B * 8 + 64));
     qie_linear_args a = lin_base();
     double by = 0;
     if (which == 0) {
@@ -744,6 +745,7 @@ int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* av
         a.x = b->x_res; a.ldx = H; a.w[0] = e->w.lm_head; a.seg_rows[0] = s.vocab;
         a.M = B; a.K = H; a.N = s.vocab; a.y = scratch; a.ldy = s.vocab; a.epilogue = QIE_EPI_STORE;
         a.norm_w = e->w.final_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
+        a.argmax_keys = (uint64_t*)(((uintptr_t)(scratch + B * (int64_t)s.vocab) + 7) & ~(uintptr_t)7);   // as the greedy step runs it
         by = (double)s.vocab * H * 2 + B * H * 2 + B * (double)s.vocab * 2;
     } else if (which != 5) {
         hipFree(scratch);

@@ -227,12 +227,12 @@ struct DecodeAttnParams {
 };
 
 // Splits per (row, kv head): ~16 at long context (>= 64 keys each), more only when
-// a split would exceed 16 keys per thread.  All derived from the live context on
+// a split would exceed kDecNtMax keys per thread.  All derived from the live context on
 // device, so a captured graph stays valid as the sequence grows.
 constexpr int kDecMinKeys = 64;
 constexpr int kDecSplits = 16;
-constexpr int kDecNtMax = 16;        // keys per thread per split
-constexpr int kDecMaxSplits = 160;
+constexpr int kDecNtMax = 8;         // keys per thread per split (K and V both held in VGPRs)
+constexpr int kDecMaxSplits = 512;   // 64k keys at head_dim 128, 128k at 64
 
 __host__ __device__ __forceinline__ int dec_tpb(int hd) { return 256 / (hd / 8); }
 __host__ __device__ __forceinline__ int dec_nsplit_target(int ctx, int hd, int splits = kDecSplits) {
@@ -246,27 +246,42 @@ __host__ __device__ __forceinline__ int dec_nsplit_target(int ctx, int hd, int s
 static int dec_splits_env() {
     const char* e = getenv("QIE_DEC_SPLITS");
     const int v = e ? atoi(e) : 0;
-    return v > 0 ? v : kDecSplits;
+    return v > 0 ? std::min(v, kDecMaxSplits) : kDecSplits;
 }
 
-template <int HD>
+__device__ __forceinline__ void unpack_bf8(const uint4& r, float* f) {
+    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int j = 0; j < 4; j++) { f[2 * j] = bf_lo(w[j]); f[2 * j + 1] = bf_hi(w[j]); }
+}
+__device__ __forceinline__ uint4 sel4(bool c, const uint4& a, const uint4& b) {
+    return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
+}
+
+// Latency structure (B = 1 decode is a chain of dependent memory round trips, not a
+// bandwidth problem): one scalar load of pos, then EVERY global load of the split —
+// the new token's q/k/v slice, norm weights, RoPE row, the split's K rows and V rows —
+// is issued before any arithmetic, so the body costs one HBM round trip; the combine
+// costs one more (partials) plus the ticket atomic.
+// G (q heads per kv head) is a template parameter: a runtime group size made hipcc
+// emit a branch per (key, head) and 12k lines of ISA.
+template <int HD, int G>
 __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnParams a) {
 #pragma clang fp contract(off)
     constexpr int LPT = HD / 8;          // lanes per key row
     constexpr int TPB = 256 / LPT;       // keys per block step (16 or 32)
     constexpr int NTMAX = kDecNtMax;
     constexpr int CHMAX = NTMAX * TPB;
-    __shared__ __attribute__((aligned(16))) float q_s[kMaxGroup][HD];
+    __shared__ __attribute__((aligned(16))) float q_s[G][HD];
     __shared__ __attribute__((aligned(16))) uint16_t kv_new[2][HD];
-    __shared__ float p_s[kMaxGroup][CHMAX];
-    __shared__ __attribute__((aligned(16))) float red_o[4][kMaxGroup][HD];
-    __shared__ float stat_m[kMaxGroup], stat_l[kMaxGroup];
-    __shared__ float cw[kMaxGroup][kDecMaxSplits];
+    __shared__ float p_s[G][CHMAX];
+    __shared__ __attribute__((aligned(16))) float red_o[4][G][HD];
+    __shared__ float stat_m[G], stat_l[G];
+    __shared__ float cw[G][kDecMaxSplits];
     __shared__ int last_flag;
 
     const int64_t m = blockIdx.y;
     const int g = blockIdx.x / a.nsplit_max, s = blockIdx.x % a.nsplit_max;
-    const int G = a.nq / a.nkv;
     const int p = a.pos[m], ctx = p + 1;
     const int nst = dec_nsplit_target(ctx, HD, a.splits_target);
     int chunk = (ctx + nst - 1) / nst;
@@ -275,7 +290,6 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnParams a) {
     if (s >= nsplit) return;
     const int t0 = s * chunk, t1 = min(ctx, t0 + chunk);
     const int ntok = t1 - t0;
-    const int NT = (ntok + TPB - 1) / TPB;
     const bool has_new = (t1 == ctx);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int grp = tid / LPT, dl = tid % LPT;
@@ -286,161 +300,154 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnParams a) {
     uint16_t* kb = a.kc + m * a.seq_stride + head_off;
     uint16_t* vb = a.vc + m * a.seq_stride + head_off;
 
-    // ---------------- prologue: q heads (norm + RoPE), new K (norm + RoPE), new V
-    if (grp < G + 2) {
-        const bool is_q = grp < G, is_k = grp == G, is_v = grp == G + 1;
-        if (is_q || ((is_k || is_v) && has_new)) {
-            const uint16_t* src = is_q ? row + (g * G + grp) * HD
-                                       : (is_k ? row + a.nq * HD + g * HD : row + (a.nq + a.nkv) * HD + g * HD);
-            uint4 raw = *reinterpret_cast<const uint4*>(src + dl * 8);
-            float x[8];
-            {
-                uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
+    // ---------------- issue all loads.  Prologue operands first (vmcnt retires in
+    // order, so waiting for them does not wait for the K/V rows).  Groups past G + 1
+    // and the k/v groups of splits without the new token load valid dummies.
+    const bool is_q = grp < G, is_k = grp == G, is_v = grp == G + 1;
+    const bool pro = is_q || ((is_k || is_v) && has_new);
+    const uint16_t* src = is_q ? row + (g * G + grp) * HD
+                               : (is_k ? row + a.nq * HD + g * HD : row + (a.nq + a.nkv) * HD + g * HD);
+    if (!(is_q || is_k || is_v)) src = row;
+    const uint4 raw = *reinterpret_cast<const uint4*>(src + dl * 8);
+    const uint16_t* nwp = is_q ? a.q_norm : a.k_norm;
+    const uint4 nraw = *reinterpret_cast<const uint4*>((nwp ? nwp : row) + dl * 8);
+    // RoPE row: interleaved pairs (dl*4 .. dl*4+3) or rotate_half (dl*8 % (HD/2) .. +7)
+    const float* cp = a.cs + (int64_t)p * (HD / 2);
+    const float* sp = a.sn + (int64_t)p * (HD / 2);
+    const int rb = hf ? (dl * 8) % (HD / 2) : dl * 4;
+    const float4 c0 = *reinterpret_cast<const float4*>(cp + rb);
+    const float4 s0 = *reinterpret_cast<const float4*>(sp + rb);
+    const int rb2 = hf ? rb + 4 : rb;   // unconditional load (a load under a uniform
+    const float4 c1 = *reinterpret_cast<const float4*>(cp + rb2);   // condition serialises)
+    const float4 s1 = *reinterpret_cast<const float4*>(sp + rb2);
+
+    uint4 kr[NTMAX], vr[NTMAX];
 #pragma unroll
-                for (int j = 0; j < 4; j++) { x[2 * j] = bf_lo(w[j]); x[2 * j + 1] = bf_hi(w[j]); }
-            }
-            if (!is_v) {
-                const uint16_t* nw = is_q ? a.q_norm : a.k_norm;
-                if (nw) {   // qk_norm.cu:43-79 (per-head RMSNorm)
-                    float ss = 0.f;
+    for (int i = 0; i < NTMAX; i++) {
+        const int t = t0 + grp + TPB * i;
+        const int tc = t < t1 ? t : t0;   // masked slots re-read a valid row
+        kr[i] = *reinterpret_cast<const uint4*>(kb + (int64_t)tc * HD + dl * 8);
+        vr[i] = *reinterpret_cast<const uint4*>(vb + (int64_t)tc * HD + dl * 8);
+    }
+    __builtin_amdgcn_sched_barrier(0);   // keep prologue math from interleaving (and waiting) mid-issue
+
+    // ---------------- prologue: q heads (norm + RoPE), new K (norm + RoPE), new V.
+    // Computed branch-free by every group (only the stores are predicated): hipcc sinks a
+    // load into the conditional block that consumes it, which would put the norm/RoPE
+    // loads behind the K/V rows in the vmcnt queue.
+    {
+        const bool nrm = nwp != nullptr && !is_v;
+        float x[8], wv[8];
+        unpack_bf8(raw, x);
+        unpack_bf8(nraw, wv);
+        // qk_norm.cu:43-79 (per-head RMSNorm)
+        float ss = 0.f;
 #pragma unroll
-                    for (int j = 0; j < 8; j++) ss += x[j] * x[j];
-                    ss = group_sum<LPT>(ss);
-                    const float rms = sqrtf((ss / (float)HD) + a.eps);
+        for (int j = 0; j < 8; j++) ss += x[j] * x[j];
+        ss = group_sum<LPT>(ss);
+        const float rms = sqrtf((ss / (float)HD) + a.eps);
 #pragma unroll
-                    for (int j = 0; j < 8; j++) {
-                        const float wv = bf2f(nw[dl * 8 + j]);
-                        x[j] = hf ? rbf(wv * rbf(x[j] * (1.0f / rms))) : rbf((x[j] / rms) * wv);
-                    }
-                }
-                // RoPE at position p (RoPE.cu:6-22 interleaved / HF rotate_half)
-                const float* c = a.cs + (int64_t)p * (HD / 2);
-                const float* sn = a.sn + (int64_t)p * (HD / 2);
-                float y[8];
-                if (hf) {
-                    float o[8];
+        for (int j = 0; j < 8; j++) {
+            const float xn = hf ? rbf(wv[j] * rbf(x[j] * (1.0f / rms))) : rbf((x[j] / rms) * wv[j]);
+            x[j] = nrm ? xn : x[j];
+        }
+        // RoPE at position p (RoPE.cu:6-22 interleaved / HF rotate_half)
+        const float cv[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+        const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        float o[8], y[8];
 #pragma unroll
-                    for (int j = 0; j < 8; j++) o[j] = __shfl_xor(x[j], LPT / 2, 64);
-                    const bool first = dl < LPT / 2;
+        for (int j = 0; j < 8; j++) o[j] = __shfl_xor(x[j], LPT / 2, 64);
+        const bool first = dl < LPT / 2;
 #pragma unroll
-                    for (int j = 0; j < 8; j++) {
-                        const int ti = (dl * 8 + j) % (HD / 2);
-                        y[j] = first ? rbf(rbf(x[j] * c[ti]) + rbf(-o[j] * sn[ti]))
-                                     : rbf(rbf(x[j] * c[ti]) + rbf(o[j] * sn[ti]));
-                    }
-                } else {
+        for (int j = 0; j < 8; j += 2) {
+            const float ya = rbf(x[j] * cv[j / 2] - x[j + 1] * sv[j / 2]);
+            const float yb = rbf(x[j + 1] * cv[j / 2] + x[j] * sv[j / 2]);
+            const float ha = first ? rbf(rbf(x[j] * cv[j]) + rbf(-o[j] * sv[j])) : rbf(rbf(x[j] * cv[j]) + rbf(o[j] * sv[j]));
+            const float hb = first ? rbf(rbf(x[j + 1] * cv[j + 1]) + rbf(-o[j + 1] * sv[j + 1]))
+                                   : rbf(rbf(x[j + 1] * cv[j + 1]) + rbf(o[j + 1] * sv[j + 1]));
+            y[j] = hf ? ha : ya;
+            y[j + 1] = hf ? hb : yb;
+        }
 #pragma unroll
-                    for (int j = 0; j < 8; j += 2) {
-                        const int ti = dl * 4 + j / 2;
-                        y[j] = rbf(x[j] * c[ti] - x[j + 1] * sn[ti]);
-                        y[j + 1] = rbf(x[j + 1] * c[ti] + x[j] * sn[ti]);
-                    }
-                }
+        for (int j = 0; j < 8; j++) x[j] = is_v ? x[j] : y[j];
+        if (is_q) {
 #pragma unroll
-                for (int j = 0; j < 8; j++) x[j] = y[j];
-            }
-            if (is_q) {
-#pragma unroll
-                for (int j = 0; j < 8; j++) q_s[grp][dl * 8 + j] = x[j];
-            } else {
-                const uint4 packed = make_uint4(pack2(x[0], x[1]), pack2(x[2], x[3]), pack2(x[4], x[5]),
-                                                pack2(x[6], x[7]));
-                uint16_t* dst = (is_k ? kb : vb) + (int64_t)p * HD + dl * 8;
-                *reinterpret_cast<uint4*>(dst) = packed;
-                *reinterpret_cast<uint4*>(&kv_new[is_k ? 0 : 1][dl * 8]) = packed;
-            }
+            for (int j = 0; j < 8; j++) q_s[grp][dl * 8 + j] = x[j];
+        } else if (pro) {
+            const uint4 packed = make_uint4(pack2(x[0], x[1]), pack2(x[2], x[3]), pack2(x[4], x[5]),
+                                            pack2(x[6], x[7]));
+            uint16_t* dst = (is_k ? kb : vb) + (int64_t)p * HD + dl * 8;
+            *reinterpret_cast<uint4*>(dst) = packed;
+            *reinterpret_cast<uint4*>(&kv_new[is_k ? 0 : 1][dl * 8]) = packed;
         }
     }
     __syncthreads();
 
-    // ---------------- phase A: all K loads in flight, then scores -> p_s
+    // ---------------- phase A: raw scores q.k -> p_s (scaled in phase B)
     {
-        // Unconditional, index-clamped loads + branch-free select of the new row: a
-        // load under a wave-uniform runtime condition makes hipcc branch around it and
-        // wait vmcnt(0) per element (cdna_hip_programming.md §5, trap (c)).
-        uint4 kr[NTMAX];
         const uint4 knew = *reinterpret_cast<const uint4*>(&kv_new[0][dl * 8]);
+        float qf[G][8];
+#pragma unroll
+        for (int gi = 0; gi < G; gi++)
+#pragma unroll
+            for (int j = 0; j < 8; j++) qf[gi][j] = q_s[gi][dl * 8 + j];
 #pragma unroll
         for (int i = 0; i < NTMAX; i++) {
-            const int t = t0 + grp + TPB * i;
-            const int tc = t < t1 ? t : t0;   // masked slots re-read a written row
-            const uint4 ld = *reinterpret_cast<const uint4*>(kb + (int64_t)tc * HD + dl * 8);
-            const bool nw = tc == p;
-            kr[i] = make_uint4(nw ? knew.x : ld.x, nw ? knew.y : ld.y, nw ? knew.z : ld.z, nw ? knew.w : ld.w);
-        }
-        float qf[kMaxGroup][8];
-#pragma unroll
-        for (int gi = 0; gi < kMaxGroup; gi++)
-#pragma unroll
-            for (int j = 0; j < 8; j++) qf[gi][j] = gi < G ? q_s[gi][dl * 8 + j] : 0.f;
-        const float scale = sqrtf((float)HD);
-#pragma unroll
-        for (int i = 0; i < NTMAX; i++) {
-            if (i >= NT) continue;
-            float kf[8];
-            uint32_t w[4] = {kr[i].x, kr[i].y, kr[i].z, kr[i].w};
-#pragma unroll
-            for (int j = 0; j < 4; j++) { kf[2 * j] = bf_lo(w[j]); kf[2 * j + 1] = bf_hi(w[j]); }
             const int tl = grp + TPB * i;
+            float kf[8];
+            unpack_bf8(sel4(t0 + tl == p, knew, kr[i]), kf);
 #pragma unroll
-            for (int gi = 0; gi < kMaxGroup; gi++) {
-                if (gi >= G) continue;
+            for (int gi = 0; gi < G; gi++) {
                 float d = 0.f;
 #pragma unroll
                 for (int j = 0; j < 8; j++) d = fmaf(qf[gi][j], kf[j], d);
                 d = group_sum<LPT>(d);
-                if (dl == 0 && tl < ntok) p_s[gi][tl] = d / scale;
+                if (dl == 0 && tl < ntok) p_s[gi][tl] = d;
             }
         }
     }
     __syncthreads();
-    // ---------------- phase B: per-head max, p = exp(s - max), l = sum p
-    for (int gi = wave; gi < G; gi += 4) {
-        float mx = -INFINITY;
-        for (int j = lane; j < ntok; j += 64) mx = fmaxf(mx, p_s[gi][j]);
-        mx = wave_max(mx);
-        float sum = 0.f;
-        for (int j = lane; j < ntok; j += 64) {
-            const float e = expf(p_s[gi][j] - mx);
-            p_s[gi][j] = e;
-            sum += e;
-        }
-        sum = wave_sum(sum);
-        if (lane == 0) {
-            stat_m[gi] = mx;
-            stat_l[gi] = sum;
+    // ---------------- phase B: s = dot / sqrt(hd); per-head max, p = exp(s - max), l = sum p
+    {
+        const float scale = sqrtf((float)HD);
+        for (int gi = wave; gi < G; gi += 4) {
+            float mx = -INFINITY;
+            for (int j = lane; j < ntok; j += 64) {
+                const float sc = p_s[gi][j] / scale;
+                p_s[gi][j] = sc;
+                mx = fmaxf(mx, sc);
+            }
+            mx = wave_max(mx);
+            float sum = 0.f;
+            for (int j = lane; j < ntok; j += 64) {
+                const float e = expf(p_s[gi][j] - mx);
+                p_s[gi][j] = e;
+                sum += e;
+            }
+            sum = wave_sum(sum);
+            if (lane == 0) {
+                stat_m[gi] = mx;
+                stat_l[gi] = sum;
+            }
         }
     }
     __syncthreads();
-    // ---------------- phase C: all V loads in flight, o = sum p v
-    float o[kMaxGroup][8];
+    // ---------------- phase C: o = sum p v (V rows already in registers)
+    float o[G][8];
 #pragma unroll
-    for (int gi = 0; gi < kMaxGroup; gi++)
+    for (int gi = 0; gi < G; gi++)
 #pragma unroll
         for (int j = 0; j < 8; j++) o[gi][j] = 0.f;
     {
-        uint4 vr[NTMAX];
         const uint4 vnew = *reinterpret_cast<const uint4*>(&kv_new[1][dl * 8]);
 #pragma unroll
         for (int i = 0; i < NTMAX; i++) {
-            const int t = t0 + grp + TPB * i;
-            const int tc = t < t1 ? t : t0;
-            const uint4 ld = *reinterpret_cast<const uint4*>(vb + (int64_t)tc * HD + dl * 8);
-            const bool nw = tc == p;
-            vr[i] = make_uint4(nw ? vnew.x : ld.x, nw ? vnew.y : ld.y, nw ? vnew.z : ld.z, nw ? vnew.w : ld.w);
-        }
-#pragma unroll
-        for (int i = 0; i < NTMAX; i++) {
-            if (i >= NT) continue;
             const int tl = grp + TPB * i;
-            if (tl >= ntok) continue;
+            if (tl >= ntok) continue;   // divergent only in the split's last step
             float vf[8];
-            uint32_t w[4] = {vr[i].x, vr[i].y, vr[i].z, vr[i].w};
+            unpack_bf8(sel4(t0 + tl == p, vnew, vr[i]), vf);
 #pragma unroll
-            for (int j = 0; j < 4; j++) { vf[2 * j] = bf_lo(w[j]); vf[2 * j + 1] = bf_hi(w[j]); }
-#pragma unroll
-            for (int gi = 0; gi < kMaxGroup; gi++) {
-                if (gi >= G) continue;
+            for (int gi = 0; gi < G; gi++) {
                 const float e = p_s[gi][tl];
 #pragma unroll
                 for (int j = 0; j < 8; j++) o[gi][j] = fmaf(e, vf[j], o[gi][j]);
@@ -448,8 +455,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnParams a) {
         }
     }
 #pragma unroll
-    for (int gi = 0; gi < kMaxGroup; gi++) {
-        if (gi >= G) continue;
+    for (int gi = 0; gi < G; gi++) {
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             float v = o[gi][j];
@@ -459,11 +465,9 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnParams a) {
     }
     if (lane < LPT) {
 #pragma unroll
-        for (int gi = 0; gi < kMaxGroup; gi++) {
-            if (gi >= G) continue;
+        for (int gi = 0; gi < G; gi++)
 #pragma unroll
             for (int j = 0; j < 8; j++) red_o[wave][gi][dl * 8 + j] = o[gi][j];
-        }
     }
     __syncthreads();
     const int nq = a.nq;
@@ -500,41 +504,40 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnParams a) {
     if (tid == 0 && !(a.dbg & 4)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    // combine weights: cw[gi][j] = exp(m_j - M) / sum_j l_j exp(m_j - M)
-    for (int idx = tid; idx < G * nsplit; idx += 256) {
-        const int gi = idx / nsplit, j = idx % nsplit;
-        cw[gi][j] = a.part_ml[((m * nq + g * G + gi) * (int64_t)a.nsplit_max + j) * 2];
-    }
-    __syncthreads();
-    if (tid < G) {
-        const int gi = tid;
+    // combine weights cw[gi][j] = exp(m_j - M) / sum_j l_j exp(m_j - M): one wave per head
+    for (int gi = wave; gi < G; gi += 4) {
         const int64_t base = (m * nq + g * G + gi) * (int64_t)a.nsplit_max;
         float mm = -INFINITY;
-        for (int j = 0; j < nsplit; j++) mm = fmaxf(mm, cw[gi][j]);
+        for (int j = lane; j < nsplit; j += 64) {
+            const float mj = a.part_ml[(base + j) * 2];
+            cw[gi][j] = mj;
+            mm = fmaxf(mm, mj);
+        }
+        mm = wave_max(mm);
         float lv = 0.f;
-        for (int j = 0; j < nsplit; j++) {
+        for (int j = lane; j < nsplit; j += 64) {
             const float c = expf(cw[gi][j] - mm);
             cw[gi][j] = c;
             lv += a.part_ml[(base + j) * 2 + 1] * c;
         }
+        lv = wave_sum(lv);
         const float inv = 1.0f / lv;
-        for (int j = 0; j < nsplit; j++) cw[gi][j] *= inv;
+        for (int j = lane; j < nsplit; j += 64) cw[gi][j] *= inv;
     }
     __syncthreads();
     for (int idx = tid; idx < G * (HD / 4); idx += 256) {
         const int gi = idx / (HD / 4), d4 = idx % (HD / 4);
-        const float4* src = reinterpret_cast<const float4*>(a.part_o) +
-                            ((m * nq + g * G + gi) * (int64_t)a.nsplit_max) * (HD / 4) + d4;
+        const float4* src4 = reinterpret_cast<const float4*>(a.part_o) +
+                             ((m * nq + g * G + gi) * (int64_t)a.nsplit_max) * (HD / 4) + d4;
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
         for (int j0 = 0; j0 < nsplit; j0 += 16) {
             float4 v[16];
 #pragma unroll
             for (int jj = 0; jj < 16; jj++)
-                if (j0 + jj < nsplit) v[jj] = src[(int64_t)(j0 + jj) * (HD / 4)];
+                v[jj] = src4[(int64_t)min(j0 + jj, nsplit - 1) * (HD / 4)];
 #pragma unroll
             for (int jj = 0; jj < 16; jj++) {
-                if (j0 + jj >= nsplit) continue;
-                const float c = cw[gi][j0 + jj];
+                const float c = j0 + jj < nsplit ? cw[gi][j0 + jj] : 0.f;
                 acc.x = fmaf(c, v[jj].x, acc.x);
                 acc.y = fmaf(c, v[jj].y, acc.y);
                 acc.z = fmaf(c, v[jj].z, acc.z);
@@ -858,7 +861,8 @@ int qie_debug_tr16_probe(int32_t* out_dev) {
 
 int64_t qie_attention_decode_workspace_bytes(int64_t B, int32_t n_heads, int32_t n_kv_heads, int32_t head_dim,
                                              int32_t max_ctx) {
-    const int64_t ns = kDecMaxSplits;   // any splits_target fits
+    // an upper bound for every splits_target <= kDecMaxSplits (monotone in it)
+    const int64_t ns = dec_nsplit_target(max_ctx, head_dim, kDecMaxSplits);
     const int64_t cnt = ((B * n_kv_heads * 4 + 255) / 256) * 256;
     return cnt + B * n_heads * ns * (head_dim + 2) * 4;
 }
@@ -899,10 +903,17 @@ int qie_attention_decode(const void* qkv, int64_t B, const int32_t* pos, const v
     a.part_ml = a.part_o + B * n_heads * (int64_t)a.nsplit_max * cache->head_dim;
     a.out = (uint16_t*)out;
     dim3 grid((unsigned)(a.nkv * a.nsplit_max), (unsigned)B);
-    if (cache->head_dim == 128)
-        hipLaunchKernelGGL(attn_decode_kernel<128>, grid, dim3(256), 0, (hipStream_t)stream, a);
-    else
-        hipLaunchKernelGGL(attn_decode_kernel<64>, grid, dim3(256), 0, (hipStream_t)stream, a);
+    const int G = n_heads / cache->n_kv_heads;
+    using K = void (*)(DecodeAttnParams);
+    static const K k128[kMaxGroup] = {attn_decode_kernel<128, 1>, attn_decode_kernel<128, 2>,
+                                      attn_decode_kernel<128, 3>, attn_decode_kernel<128, 4>,
+                                      attn_decode_kernel<128, 5>, attn_decode_kernel<128, 6>,
+                                      attn_decode_kernel<128, 7>, attn_decode_kernel<128, 8>};
+    static const K k64[kMaxGroup] = {attn_decode_kernel<64, 1>, attn_decode_kernel<64, 2>,
+                                     attn_decode_kernel<64, 3>, attn_decode_kernel<64, 4>,
+                                     attn_decode_kernel<64, 5>, attn_decode_kernel<64, 6>,
+                                     attn_decode_kernel<64, 7>, attn_decode_kernel<64, 8>};
+    hipLaunchKernelGGL((cache->head_dim == 128 ? k128 : k64)[G - 1], grid, dim3(256), 0, (hipStream_t)stream, a);
     QIE_LAUNCH_CHECK();
     return 0;
 }

@@ -80,23 +80,21 @@ __device__ __forceinline__ float group_max(float v) {
     if constexpr (N >= 16) v = fmaxf(v, dpp_f<0x140>(v));
     return v;
 }
-// op with lane ^ 16 / lane ^ 32 (v_permlane16_swap / v_permlane32_swap on two copies)
-__device__ __forceinline__ float xor16_sum(float v) {
-    auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false, false);
-    return __builtin_bit_cast(float, r[0]) + __builtin_bit_cast(float, r[1]);
+// op with lane ^ 16 / lane ^ 32 (v_permlane16_swap / v_permlane32_swap on two copies).
+// Inline asm: the __builtin_amdgcn_permlane*_swap builtins with both operands equal are
+// miscompiled by this toolchain (both results read from the same register).  The s_nops
+// cover the VALU-write -> permlane-read hazard and the result read after it.
+template <int W>
+__device__ __forceinline__ void lane_swap(float& a, float& b) {
+    if constexpr (W == 16)
+        asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+    else
+        asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
 }
-__device__ __forceinline__ float xor32_sum(float v) {
-    auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false, false);
-    return __builtin_bit_cast(float, r[0]) + __builtin_bit_cast(float, r[1]);
-}
-__device__ __forceinline__ float xor16_max(float v) {
-    auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false, false);
-    return fmaxf(__builtin_bit_cast(float, r[0]), __builtin_bit_cast(float, r[1]));
-}
-__device__ __forceinline__ float xor32_max(float v) {
-    auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false, false);
-    return fmaxf(__builtin_bit_cast(float, r[0]), __builtin_bit_cast(float, r[1]));
-}
+__device__ __forceinline__ float xor16_sum(float v) { float a = v, b = v; lane_swap<16>(a, b); return a + b; }
+__device__ __forceinline__ float xor32_sum(float v) { float a = v, b = v; lane_swap<32>(a, b); return a + b; }
+__device__ __forceinline__ float xor16_max(float v) { float a = v, b = v; lane_swap<16>(a, b); return fmaxf(a, b); }
+__device__ __forceinline__ float xor32_max(float v) { float a = v, b = v; lane_swap<32>(a, b); return fmaxf(a, b); }
 __device__ __forceinline__ float wave_sum(float v) { return xor32_sum(xor16_sum(group_sum<16>(v))); }
 __device__ __forceinline__ float wave_max(float v) { return xor32_max(xor16_max(group_max<16>(v))); }
 // 64-bit max (selection keys) keeps the generic shuffle path (rare, end of kernels).

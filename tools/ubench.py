@@ -24,7 +24,7 @@ def main():
     b.prefill(0, ids)
     b.decode(256, want_ids=False)          # ctx ~2300
     variants = [("attn", 5, {})]
-    for sp in ("4", "8", "12", "24", "32"):
+    for sp in ("8", "24", "32", "48", "64"):
         variants.append(("attn", 5, {"QIE_DEC_SPLITS": sp}))
     variants += [("attn", 5, {"QIE_DEC_DBG": "1"}), ("attn", 5, {"QIE_DEC_DBG": "6"})]
     for which in (0, 1, 2, 3, 4):

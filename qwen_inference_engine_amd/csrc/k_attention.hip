@@ -217,7 +217,8 @@ struct DecodeAttnParams {
     int64_t seq_stride;
     int layer, nkv, nq, max_ctx, nsplit_max;
     int splits_target;        // ~splits per (row, kv head) at long context
-    int dbg;                  // timing experiments only (QIE_DEC_DBG): 1 no combine, 2 no release, 4 no acquire
+    int dbg;                  // timing experiments only (QIE_DEC_DBG): 1 no combine, 2 no release, 4 no acquire,
+                              // 8/16/32 stop after prologue / phase A / phase B, 64 exit at once
     float eps;
     int numerics;
     float* part_o;            // [B][nq][nsplit_max][HD]
@@ -243,12 +244,6 @@ __host__ __device__ __forceinline__ int dec_nsplit_target(int ctx, int hd, int s
     return by_min < want ? by_min : want;
 }
 
-static int dec_splits_env() {
-    const char* e = getenv("QIE_DEC_SPLITS");
-    const int v = e ? atoi(e) : 0;
-    return v > 0 ? std::min(v, kDecMaxSplits) : kDecSplits;
-}
-
 __device__ __forceinline__ void unpack_bf8(const uint4& r, float* f) {
     const uint32_t w[4] = {r.x, r.y, r.z, r.w};
 #pragma unroll
@@ -256,6 +251,14 @@ __device__ __forceinline__ void unpack_bf8(const uint4& r, float* f) {
 }
 __device__ __forceinline__ uint4 sel4(bool c, const uint4& a, const uint4& b) {
     return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
+}
+// Opaque register pass-through: math on the value cannot be hoisted above this point,
+// so the wait for its load lands here (after the K/V loads were issued), not before them.
+__device__ __forceinline__ void pin4(uint4& v) {
+    asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+}
+__device__ __forceinline__ void pin4(float4& v) {
+    asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
 }
 
 // Latency structure (B = 1 decode is a chain of dependent memory round trips, not a
@@ -287,7 +290,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnParams a) {
     int chunk = (ctx + nst - 1) / nst;
     chunk = (chunk + TPB - 1) / TPB * TPB;
     const int nsplit = (ctx + chunk - 1) / chunk;
-    if (s >= nsplit) return;
+    if (s >= nsplit || (a.dbg & 64)) return;
     const int t0 = s * chunk, t1 = min(ctx, t0 + chunk);
     const int ntok = t1 - t0;
     const bool has_new = (t1 == ctx);
@@ -382,6 +385,10 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnParams a) {
         }
     }
     __syncthreads();
+    if (a.dbg & 8) {   // timing: loads + prologue only
+        if (tid == 0) a.out[m] = (uint16_t)(kr[0].x + vr[NTMAX - 1].y + kr[NTMAX - 1].z + vr[0].w);
+        return;
+    }
 
     // ---------------- phase A: raw scores q.k -> p_s (scaled in phase B)
     {
@@ -407,6 +414,10 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnParams a) {
         }
     }
     __syncthreads();
+    if (a.dbg & 16) {
+        if (tid == 0) a.out[m] = (uint16_t)(p_s[0][1] + vr[NTMAX - 1].y + vr[0].w);
+        return;
+    }
     // ---------------- phase B: s = dot / sqrt(hd); per-head max, p = exp(s - max), l = sum p
     {
         const float scale = sqrtf((float)HD);
@@ -432,6 +443,10 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnParams a) {
         }
     }
     __syncthreads();
+    if (a.dbg & 32) {
+        if (tid == 0) a.out[m] = (uint16_t)(p_s[0][1] + vr[NTMAX - 1].y + vr[0].w);
+        return;
+    }
     // ---------------- phase C: o = sum p v (V rows already in registers)
     float o[G][8];
 #pragma unroll
@@ -752,6 +767,357 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(PrefillAttnParam
     }
 }
 
+// ---------------------------------------------------------------------------
+// Decode attention on MFMA (default decode path).  The q heads of one kv head
+// (G <= 8, padded to 16) play the role of the 16 "query rows" of the prefill
+// kernel above, so GQA decode is a 16 x 32 x HD flash step per wave:
+//   S^T = K . Q^T : A = K rows straight from HBM into registers (lane: key l&15,
+//                   8 contiguous d), B = Q^T from LDS (bf16 after norm + RoPE);
+//   O  += P . V   : A = P from the S^T accumulators, split into bf16 hi + lo parts
+//                   (two MFMAs) so the fp32 probabilities keep ~16 mantissa bits;
+//                   B = V through a per-wave LDS slot read with ds_read_b64_tr_b16.
+// Block = (kv head, split) x 4 waves; a block step covers 128 keys (32 per wave);
+// waves run an online softmax, are merged in LDS, and the splits are merged by
+// the last-arriving block (release / acquire, as the VALU kernel).  The VALU
+// kernel spent ~7 us of ~11 in dot products and cross-lane reductions here.
+constexpr int kDecMStep = 128;      // keys per block step (4 waves x 32)
+constexpr int kDecMSplits = 32;     // default split target
+
+__host__ __device__ __forceinline__ int decm_chunk(int ctx, int target) {
+    const int per = kDecMStep * target;
+    const int steps = (ctx + per - 1) / per;
+    return kDecMStep * (steps < 1 ? 1 : steps);
+}
+
+template <int HD>
+__global__ __launch_bounds__(256) void attn_decode_mfma_kernel(DecodeAttnParams a) {
+#pragma clang fp contract(off)
+    constexpr int LPT = HD / 8;          // prologue: lanes per head row
+    constexpr int KSTEPS = HD / 32;      // MFMA k-steps over d for S
+    constexpr int DT = HD / 16;          // output d tiles
+    constexpr int CPR = HD / 8;          // 16-byte chunks per row
+    constexpr int VCH = 32 * CPR / 64;   // V chunks per lane per wave step
+    __shared__ __attribute__((aligned(16))) uint16_t q_s[16][HD];
+    __shared__ __attribute__((aligned(16))) uint16_t kv_new[2][HD];
+    __shared__ __attribute__((aligned(16))) uint16_t v_s[4][32 * HD];
+    __shared__ float red_m[4][16], red_l[4][16];
+    __shared__ __attribute__((aligned(16))) float red_o[4][kMaxGroup][HD];
+    __shared__ float cw[kMaxGroup][kDecMaxSplits];
+    __shared__ int last_flag;
+
+    const int64_t m = blockIdx.y;
+    const int g = blockIdx.x / a.nsplit_max, s = blockIdx.x % a.nsplit_max;
+    const int G = a.nq / a.nkv;
+    const int p = a.pos[m], ctx = p + 1;
+    const int chunk = decm_chunk(ctx, a.splits_target);
+    const int nsplit = (ctx + chunk - 1) / chunk;
+    if (s >= nsplit || (a.dbg & 64)) return;
+    const int t0 = s * chunk, t1 = min(ctx, t0 + chunk);
+    const int nstep = (t1 - t0 + kDecMStep - 1) / kDecMStep;
+    const bool has_new = (t1 == ctx);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int fr = lane & 15, gq = lane >> 4;
+    const int grp = tid / LPT, dl = tid % LPT;
+    const int QKVD = (a.nq + 2 * a.nkv) * HD;
+    const uint16_t* row = a.qkv + m * (int64_t)QKVD;
+    const bool hf = a.numerics == QIE_NUMERICS_HF;
+    const int64_t head_off = (((int64_t)a.layer * a.nkv + g) * a.max_ctx) * HD;
+    uint16_t* kb = a.kc + m * a.seq_stride + head_off;
+    uint16_t* vb = a.vc + m * a.seq_stride + head_off;
+
+    // ---------------- issue all loads: prologue operands first, then step 0's K/V
+    const bool is_q = grp < G, is_k = grp == G, is_v = grp == G + 1;
+    const bool pro = is_q || ((is_k || is_v) && has_new);
+    const uint16_t* src = is_q ? row + (g * G + grp) * HD
+                               : (is_k ? row + a.nq * HD + g * HD : row + (a.nq + a.nkv) * HD + g * HD);
+    if (!(is_q || is_k || is_v)) src = row;
+    uint4 raw = *reinterpret_cast<const uint4*>(src + dl * 8);
+    const uint16_t* nwp = is_q ? a.q_norm : a.k_norm;
+    uint4 nraw = *reinterpret_cast<const uint4*>((nwp ? nwp : row) + dl * 8);
+    const float* cp = a.cs + (int64_t)p * (HD / 2);
+    const float* sp = a.sn + (int64_t)p * (HD / 2);
+    const int rb = hf ? (dl * 8) % (HD / 2) : dl * 4;
+    const int rb2 = hf ? rb + 4 : rb;
+    float4 c0 = *reinterpret_cast<const float4*>(cp + rb);
+    float4 s0 = *reinterpret_cast<const float4*>(sp + rb);
+    float4 c1 = *reinterpret_cast<const float4*>(cp + rb2);
+    float4 s1 = *reinterpret_cast<const float4*>(sp + rb2);
+    __builtin_amdgcn_sched_barrier(0);   // prologue operands ahead of K/V in the vmcnt queue
+
+    uint4 kf[2][KSTEPS], vr[VCH];
+    auto load_step = [&](int st) {
+        const int kbase = t0 + st * kDecMStep + wave * 32;
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+            const int key = min(kbase + 16 * t + fr, t1 - 1);
+#pragma unroll
+            for (int ks = 0; ks < KSTEPS; ks++)
+                kf[t][ks] = *reinterpret_cast<const uint4*>(kb + (int64_t)key * HD + 32 * ks + 8 * gq);
+        }
+#pragma unroll
+        for (int i = 0; i < VCH; i++) {
+            const int c = lane + 64 * i;
+            const int key = min(kbase + c / CPR, t1 - 1);
+            vr[i] = *reinterpret_cast<const uint4*>(vb + (int64_t)key * HD + (c % CPR) * 8);
+        }
+    };
+    load_step(0);
+    pin4(raw); pin4(nraw); pin4(c0); pin4(s0); pin4(c1); pin4(s1);
+
+    // ---------------- prologue (branch-free; see attn_decode_kernel)
+    {
+        const bool nrm = nwp != nullptr && !is_v;
+        float x[8], wv[8];
+        unpack_bf8(raw, x);
+        unpack_bf8(nraw, wv);
+        float ss = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; j++) ss += x[j] * x[j];
+        ss = group_sum<LPT>(ss);
+        const float rms = sqrtf((ss / (float)HD) + a.eps);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const float xn = hf ? rbf(wv[j] * rbf(x[j] * (1.0f / rms))) : rbf((x[j] / rms) * wv[j]);
+            x[j] = nrm ? xn : x[j];
+        }
+        const float cv[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+        const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        float o[8], y[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) o[j] = __shfl_xor(x[j], LPT / 2, 64);
+        const bool first = dl < LPT / 2;
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+            const float ya = rbf(x[j] * cv[j / 2] - x[j + 1] * sv[j / 2]);
+            const float yb = rbf(x[j + 1] * cv[j / 2] + x[j] * sv[j / 2]);
+            const float ha = first ? rbf(rbf(x[j] * cv[j]) + rbf(-o[j] * sv[j])) : rbf(rbf(x[j] * cv[j]) + rbf(o[j] * sv[j]));
+            const float hb = first ? rbf(rbf(x[j + 1] * cv[j + 1]) + rbf(-o[j + 1] * sv[j + 1]))
+                                   : rbf(rbf(x[j + 1] * cv[j + 1]) + rbf(o[j + 1] * sv[j + 1]));
+            y[j] = hf ? ha : ya;
+            y[j + 1] = hf ? hb : yb;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) x[j] = is_v ? x[j] : y[j];
+        const uint4 packed = make_uint4(pack2(x[0], x[1]), pack2(x[2], x[3]), pack2(x[4], x[5]), pack2(x[6], x[7]));
+        if (is_q) {
+            *reinterpret_cast<uint4*>(&q_s[grp][dl * 8]) = packed;
+        } else if (pro) {
+            uint16_t* dst = (is_k ? kb : vb) + (int64_t)p * HD + dl * 8;
+            *reinterpret_cast<uint4*>(dst) = packed;
+            *reinterpret_cast<uint4*>(&kv_new[is_k ? 0 : 1][dl * 8]) = packed;
+        }
+        for (int idx = tid; idx < (16 - G) * CPR; idx += 256)   // padded q rows
+            *reinterpret_cast<uint4*>(&q_s[G + idx / CPR][(idx % CPR) * 8]) = make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+    if (a.dbg & 8) {   // timing: loads + prologue only
+        if (tid == 0) a.out[m] = (uint16_t)(kf[0][0].x + vr[VCH - 1].y + kf[1][KSTEPS - 1].z);
+        return;
+    }
+
+    bf16x8_t qb[KSTEPS];
+    uint4 knew[KSTEPS];
+#pragma unroll
+    for (int ks = 0; ks < KSTEPS; ks++) {
+        qb[ks] = *reinterpret_cast<const bf16x8_t*>(&q_s[fr][32 * ks + 8 * gq]);
+        knew[ks] = *reinterpret_cast<const uint4*>(&kv_new[0][32 * ks + 8 * gq]);
+    }
+    const float scale = sqrtf((float)HD);
+    float m_run = -INFINITY, l_run = 0.f;
+    f32x4_t oacc[DT];
+#pragma unroll
+    for (int d = 0; d < DT; d++) oacc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    uint16_t* vw = &v_s[wave][0];
+    const int q4 = fr >> 2, p4 = fr & 3;
+
+    for (int st = 0; st < nstep; st++) {
+        const int kbase = t0 + st * kDecMStep + wave * 32;
+        // ---- S^T = K . Q^T over this wave's two 16-key tiles
+        f32x4_t sacc[2];
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+            sacc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+            const bool nw = kbase + 16 * t + fr == p;
+#pragma unroll
+            for (int ks = 0; ks < KSTEPS; ks++)
+                sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                    __builtin_bit_cast(bf16x8_t, sel4(nw, knew[ks], kf[t][ks])), qb[ks], sacc[t], 0, 0, 0);
+        }
+        // ---- V rows -> this wave's LDS slot (the new token's row from kv_new)
+#pragma unroll
+        for (int i = 0; i < VCH; i++) {
+            const int c = lane + 64 * i;
+            const int r = c / CPR, ch = c % CPR;
+            const uint4 vn = *reinterpret_cast<const uint4*>(&kv_new[1][ch * 8]);
+            *reinterpret_cast<uint4*>(vw + r * HD + ch * 8) = sel4(kbase + r == p, vn, vr[i]);
+        }
+        if (st + 1 < nstep) load_step(st + 1);
+        // ---- online softmax (lane: head fr; keys 4 gq + r of tiles 0 and 1)
+        float e[2][4];
+        float mt = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < 2; t++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int key = kbase + 16 * t + 4 * gq + r;
+                const float sc = key < t1 ? sacc[t][r] / scale : -INFINITY;
+                e[t][r] = sc;
+                mt = fmaxf(mt, sc);
+            }
+        mt = xor32_max(xor16_max(mt));
+        const float m_new = fmaxf(m_run, mt);
+        const float m_use = m_new == -INFINITY ? 0.f : m_new;   // a wave with no live key yet
+        const float alpha = expf(m_run - m_use);
+        float ls = 0.f;
+#pragma unroll
+        for (int t = 0; t < 2; t++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                e[t][r] = expf(e[t][r] - m_use);
+                ls += e[t][r];
+            }
+        ls = xor32_sum(xor16_sum(ls));
+        l_run = l_run * alpha + ls;
+        m_run = m_new;
+        float ar[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) ar[r] = __shfl(alpha, gq * 4 + r, 64);
+#pragma unroll
+        for (int d = 0; d < DT; d++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) oacc[d][r] *= ar[r];
+        // ---- O += P . V, P = hi + lo (k slot 8 gq + j <-> key j < 4 ? 4 gq + j : 16 + 4 gq + j - 4)
+        bf16x8_t ph, pl;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            ph[j] = (__bf16)e[0][j];
+            ph[4 + j] = (__bf16)e[1][j];
+            pl[j] = (__bf16)(e[0][j] - (float)ph[j]);
+            pl[4 + j] = (__bf16)(e[1][j] - (float)ph[4 + j]);
+        }
+        __syncthreads();   // V slot written
+#pragma unroll
+        for (int d = 0; d < DT; d++) {
+            const uint16_t* a0 = vw + (4 * gq + q4) * HD + 16 * d + 4 * p4;
+            const i16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4_t*)(a0));
+            const i16x4_t v1 =
+                __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4_t*)(a0 + 16 * HD));
+            const bf16x8_t vb8 = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+            oacc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph, vb8, oacc[d], 0, 0, 0);
+            oacc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pl, vb8, oacc[d], 0, 0, 0);
+        }
+        __syncthreads();   // slot free for the next step
+    }
+    if (a.dbg & 16) {
+        if (tid == 0) a.out[m] = (uint16_t)(oacc[0][0] + m_run);
+        return;
+    }
+
+    // ---------------- merge the 4 waves (rows = heads 4 gq + r of this lane)
+    if (gq == 0) {
+        red_m[wave][fr] = m_run;
+        red_l[wave][fr] = l_run;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int h = 4 * gq + r;
+        if (h >= G) continue;
+        const float M = fmaxf(fmaxf(red_m[0][h], red_m[1][h]), fmaxf(red_m[2][h], red_m[3][h]));
+        const float mw = red_m[wave][h];
+        const float sc = mw == -INFINITY ? 0.f : expf(mw - M);
+#pragma unroll
+        for (int d = 0; d < DT; d++) red_o[wave][h][16 * d + fr] = oacc[d][r] * sc;
+    }
+    __syncthreads();
+    const int nq = a.nq;
+    for (int idx = tid; idx < G * HD; idx += 256) {
+        const int h = idx / HD, d = idx % HD;
+        const float M = fmaxf(fmaxf(red_m[0][h], red_m[1][h]), fmaxf(red_m[2][h], red_m[3][h]));
+        float L = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; w++)
+            if (red_m[w][h] != -INFINITY) L += red_l[w][h] * expf(red_m[w][h] - M);
+        const float ov = red_o[0][h][d] + red_o[1][h][d] + red_o[2][h][d] + red_o[3][h][d];
+        if (nsplit == 1) {
+            a.out[m * (int64_t)nq * HD + (int64_t)(g * G + h) * HD + d] = f2bf(ov / L);
+        } else {
+            const int64_t pi = (m * nq + g * G + h) * (int64_t)a.nsplit_max + s;
+            a.part_o[pi * HD + d] = ov;
+            if (d == 0) {
+                a.part_ml[pi * 2] = M;
+                a.part_ml[pi * 2 + 1] = L;
+            }
+        }
+    }
+    if (nsplit == 1) return;
+    // ---------------- publish this split; the last arriver combines (release / acquire)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (a.dbg & 1) return;
+    unsigned* cnt = a.counters + m * a.nkv + g;
+    if (tid == 0) {
+        if (!(a.dbg & 2)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_flag = (old == (unsigned)nsplit - 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (!last_flag) return;
+    if (tid == 0 && !(a.dbg & 4)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // each (head, d4) item issues its first 16 partial loads together with the m / l loads
+    const bool has_item = tid < G * (HD / 4);
+    const int gi = has_item ? tid / (HD / 4) : 0, d4 = tid % (HD / 4);
+    const float4* src4 =
+        reinterpret_cast<const float4*>(a.part_o) + ((m * nq + g * G + gi) * (int64_t)a.nsplit_max) * (HD / 4) + d4;
+    float4 v[16];
+#pragma unroll
+    for (int jj = 0; jj < 16; jj++) v[jj] = src4[(int64_t)min(jj, nsplit - 1) * (HD / 4)];
+    __builtin_amdgcn_sched_barrier(0);
+    for (int gh = wave; gh < G; gh += 4) {   // cw[h][j] = exp(m_j - M) / sum_j l_j exp(m_j - M)
+        const int64_t base = (m * nq + g * G + gh) * (int64_t)a.nsplit_max;
+        float mm = -INFINITY;
+        for (int j = lane; j < nsplit; j += 64) {
+            const float mj = a.part_ml[(base + j) * 2];
+            cw[gh][j] = mj;
+            mm = fmaxf(mm, mj);
+        }
+        mm = wave_max(mm);
+        float lv = 0.f;
+        for (int j = lane; j < nsplit; j += 64) {
+            const float c = expf(cw[gh][j] - mm);
+            cw[gh][j] = c;
+            lv += a.part_ml[(base + j) * 2 + 1] * c;
+        }
+        lv = wave_sum(lv);
+        const float inv = 1.0f / lv;
+        for (int j = lane; j < nsplit; j += 64) cw[gh][j] *= inv;
+    }
+    __syncthreads();
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int j0 = 0; j0 < nsplit; j0 += 16) {
+        if (j0 > 0) {
+#pragma unroll
+            for (int jj = 0; jj < 16; jj++) v[jj] = src4[(int64_t)min(j0 + jj, nsplit - 1) * (HD / 4)];
+        }
+#pragma unroll
+        for (int jj = 0; jj < 16; jj++) {
+            const float c = j0 + jj < nsplit ? cw[gi][j0 + jj] : 0.f;
+            acc.x = fmaf(c, v[jj].x, acc.x);
+            acc.y = fmaf(c, v[jj].y, acc.y);
+            acc.z = fmaf(c, v[jj].z, acc.z);
+            acc.w = fmaf(c, v[jj].w, acc.w);
+        }
+    }
+    if (has_item) {
+        uint16_t* dst = a.out + m * (int64_t)nq * HD + (int64_t)(g * G + gi) * HD + d4 * 4;
+        *reinterpret_cast<uint2*>(dst) = make_uint2(pack2(acc.x, acc.y), pack2(acc.z, acc.w));
+    }
+    if (tid == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Diagnostics: lane l reads the 8 bytes at element 4*l of an LDS array holding
 // value == element index; out[l][e] = what ds_read_b64_tr_b16 delivered.
 __global__ void tr16_probe_kernel(int32_t* out) {
@@ -891,9 +1257,13 @@ int qie_attention_decode(const void* qkv, int64_t B, const int32_t* pos, const v
     a.nkv = cache->n_kv_heads;
     a.nq = n_heads;
     a.max_ctx = cache->max_ctx;
-    a.splits_target = dec_splits_env();
+    const bool valu = getenv("QIE_DEC_VALU") && atoi(getenv("QIE_DEC_VALU")) != 0;   // A/B timing only
+    const char* se = getenv("QIE_DEC_SPLITS");
+    const int senv = se ? std::min(atoi(se), kDecMaxSplits) : 0;
+    a.splits_target = senv > 0 ? senv : (valu ? kDecSplits : kDecMSplits);
     a.dbg = getenv("QIE_DEC_DBG") ? atoi(getenv("QIE_DEC_DBG")) : 0;
-    a.nsplit_max = dec_nsplit_target(cache->max_ctx, cache->head_dim, a.splits_target);
+    a.nsplit_max = valu ? dec_nsplit_target(cache->max_ctx, cache->head_dim, a.splits_target)
+                        : std::min(a.splits_target, (cache->max_ctx + kDecMStep - 1) / kDecMStep);
     QIE_REQUIRE(a.nsplit_max <= kDecMaxSplits, "qie_attention_decode: max_ctx %d too long", cache->max_ctx);
     a.eps = eps;
     a.numerics = numerics;
@@ -913,7 +1283,14 @@ int qie_attention_decode(const void* qkv, int64_t B, const int32_t* pos, const v
                                      attn_decode_kernel<64, 3>, attn_decode_kernel<64, 4>,
                                      attn_decode_kernel<64, 5>, attn_decode_kernel<64, 6>,
                                      attn_decode_kernel<64, 7>, attn_decode_kernel<64, 8>};
-    hipLaunchKernelGGL((cache->head_dim == 128 ? k128 : k64)[G - 1], grid, dim3(256), 0, (hipStream_t)stream, a);
+    if (!valu) {
+        if (cache->head_dim == 128)
+            hipLaunchKernelGGL(attn_decode_mfma_kernel<128>, grid, dim3(256), 0, (hipStream_t)stream, a);
+        else
+            hipLaunchKernelGGL(attn_decode_mfma_kernel<64>, grid, dim3(256), 0, (hipStream_t)stream, a);
+    } else {
+        hipLaunchKernelGGL((cache->head_dim == 128 ? k128 : k64)[G - 1], grid, dim3(256), 0, (hipStream_t)stream, a);
+    }
     QIE_LAUNCH_CHECK();
     return 0;
 }

@@ -63,13 +63,85 @@ __device__ __forceinline__ void unpack8(u32x4 v, float* f) {
     f[6] = bf_lo(v.w); f[7] = bf_hi(v.w);
 }
 
-template <int MT, int RPW, int EPI, int U>
+template <int MT, int RPW, int EPI, int U, bool PF>
 __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint16_t* xs = reinterpret_cast<uint16_t*>(smem);
     float* red = reinterpret_cast<float*>(smem + (p.xlds ? (size_t)MT * p.K * 2 : 0));
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t K = p.K;
+
+    // ---------------- task -> weight rows / output columns
+    auto task_ptrs = [&](int64_t task, const u32x4* (&wr)[RPW]) {
+        if constexpr (EPI == QIE_EPI_SWIGLU) {
+            constexpr int P2 = RPW / 2;
+#pragma unroll
+            for (int i = 0; i < P2; i++) {
+                int64_t j = task * P2 + i;
+                if (j >= p.N) j = p.N - 1;
+                wr[i] = reinterpret_cast<const u32x4*>(p.w0 + j * K);
+                wr[P2 + i] = reinterpret_cast<const u32x4*>(p.w1 + j * K);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < RPW; i++) {
+                int64_t r = task * RPW + i;
+                if (r >= p.N) r = p.N - 1;
+                const uint16_t* base;
+                if (r < p.n0) base = p.w0 + r * K;
+                else if (r < p.n01) base = p.w1 + (r - p.n0) * K;
+                else base = p.w2 + (r - p.n01) * K;
+                wr[i] = reinterpret_cast<const u32x4*>(base);
+            }
+        }
+    };
+    auto task_cols = [&](int64_t task, int64_t (&col)[RPW]) {
+        if constexpr (EPI == QIE_EPI_SWIGLU) {
+            constexpr int P2 = RPW / 2;
+#pragma unroll
+            for (int i = 0; i < P2; i++) col[i] = col[P2 + i] = task * P2 + i;
+        } else {
+#pragma unroll
+            for (int i = 0; i < RPW; i++) col[i] = task * RPW + i;
+        }
+    };
+    auto load_chunk = [&](const u32x4* const (&wr)[RPW], int64_t k0, u32x4 (&wv)[U][RPW]) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int64_t k = k0 + u * 512;
+#pragma unroll
+            for (int i = 0; i < RPW; i++)
+                wv[u][i] = (k < K) ? __builtin_nontemporal_load(wr[i] + (k >> 3)) : u32x4{0u, 0u, 0u, 0u};
+        }
+    };
+    auto compute_chunk = [&](int64_t k0, const u32x4 (&wv)[U][RPW], float (&acc)[MT][RPW]) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int64_t k = k0 + u * 512;
+            if (k < K) {
+#pragma unroll
+                for (int m = 0; m < MT; m++) {
+                    uint4 xv = p.xlds ? *reinterpret_cast<const uint4*>(xs + (int64_t)m * K + k)
+                                      : (m < p.M ? *reinterpret_cast<const uint4*>(p.x + (int64_t)m * p.ldx + k)
+                                                 : make_uint4(0, 0, 0, 0));
+                    float xf[8];
+                    unpack8(u32x4{xv.x, xv.y, xv.z, xv.w}, xf);
+#pragma unroll
+                    for (int i = 0; i < RPW; i++) fma8(acc[m][i], xf, wv[u][i]);
+                }
+            }
+        }
+    };
+
+    const int64_t tstride = (int64_t)gridDim.x * 4;
+    const int64_t task0 = (int64_t)blockIdx.x * 4 + wave;
+    const u32x4* wr[RPW];
+    u32x4 wv[U][RPW];
+    if (PF && task0 < p.n_tasks) {
+        task_ptrs(task0, wr);
+        load_chunk(wr, (int64_t)lane * 8, wv);
+    }
+    __builtin_amdgcn_sched_barrier(0);
 
     // ---------------- prologue: activation rows -> LDS (optionally RMS-normed)
     if (p.xlds) {
@@ -135,68 +207,30 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
 #pragma unroll
     for (int m = 0; m < MT; m++) kbest[m] = 0ull;
 
-    // ---------------- main loop over row tasks
-    for (int64_t task = (int64_t)blockIdx.x * 4 + wave; task < p.n_tasks;
-         task += (int64_t)gridDim.x * 4) {
-        const u32x4* wr[RPW];
+    // ---------------- main loop over row tasks.  Software-pipelined across tasks: the
+    // first weight chunk of a wave's NEXT task is issued before this task's reduction
+    // and epilogue (and the first task's before the prologue above), so a wave with one
+    // or two tasks — every small decode GEMV — pays one HBM round trip, not three.
+    for (int64_t task = task0; task < p.n_tasks; task += tstride) {
         int64_t col[RPW];
-        if constexpr (EPI == QIE_EPI_SWIGLU) {
-            constexpr int P2 = RPW / 2;
-#pragma unroll
-            for (int i = 0; i < P2; i++) {
-                int64_t j = task * P2 + i;
-                col[i] = col[P2 + i] = j;
-                if (j >= p.N) j = p.N - 1;
-                wr[i] = reinterpret_cast<const u32x4*>(p.w0 + j * K);
-                wr[P2 + i] = reinterpret_cast<const u32x4*>(p.w1 + j * K);
-            }
-        } else {
-#pragma unroll
-            for (int i = 0; i < RPW; i++) {
-                int64_t r = task * RPW + i;
-                col[i] = r;
-                if (r >= p.N) r = p.N - 1;
-                const uint16_t* base;
-                if (r < p.n0) base = p.w0 + r * K;
-                else if (r < p.n01) base = p.w1 + (r - p.n0) * K;
-                else base = p.w2 + (r - p.n01) * K;
-                wr[i] = reinterpret_cast<const u32x4*>(base);
-            }
+        task_cols(task, col);
+        if constexpr (!PF) {
+            task_ptrs(task, wr);
+            load_chunk(wr, (int64_t)lane * 8, wv);
         }
-
         float acc[MT][RPW];
 #pragma unroll
         for (int m = 0; m < MT; m++)
 #pragma unroll
             for (int i = 0; i < RPW; i++) acc[m][i] = 0.f;
-
-        for (int64_t k0 = (int64_t)lane * 8; k0 < K; k0 += 512 * U) {
-            u32x4 wv[U][RPW];
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                const int64_t k = k0 + u * 512;
-#pragma unroll
-                for (int i = 0; i < RPW; i++)
-                    wv[u][i] = (k < K) ? __builtin_nontemporal_load(wr[i] + (k >> 3))
-                                       : u32x4{0u, 0u, 0u, 0u};
-            }
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                const int64_t k = k0 + u * 512;
-                if (k < K) {
-#pragma unroll
-                    for (int m = 0; m < MT; m++) {
-                        uint4 xv = p.xlds ? *reinterpret_cast<const uint4*>(xs + (int64_t)m * K + k)
-                                          : (m < p.M ? *reinterpret_cast<const uint4*>(
-                                                           p.x + (int64_t)m * p.ldx + k)
-                                                     : make_uint4(0, 0, 0, 0));
-                        float xf[8];
-                        unpack8(u32x4{xv.x, xv.y, xv.z, xv.w}, xf);
-#pragma unroll
-                        for (int i = 0; i < RPW; i++) fma8(acc[m][i], xf, wv[u][i]);
-                    }
-                }
-            }
+        compute_chunk((int64_t)lane * 8, wv, acc);
+        for (int64_t k0 = (int64_t)lane * 8 + 512 * U; k0 < K; k0 += 512 * U) {
+            load_chunk(wr, k0, wv);
+            compute_chunk(k0, wv, acc);
+        }
+        if (PF && task + tstride < p.n_tasks) {
+            task_ptrs(task + tstride, wr);
+            load_chunk(wr, (int64_t)lane * 8, wv);
         }
 #pragma unroll
         for (int m = 0; m < MT; m++)
@@ -268,7 +302,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
     }
 }
 
-template <int MT, int RPW, int EPI>
+template <int MT, int RPW, int EPI, bool PF>
 static int launch_gemv_t(const GemvParams& p, hipStream_t st, int blocks_per_cu) {
     constexpr int U = (RPW >= 4) ? 4 : 8;
     const int64_t n_blocks_needed = (p.n_tasks + 3) / 4;
@@ -278,27 +312,31 @@ static int launch_gemv_t(const GemvParams& p, hipStream_t st, int blocks_per_cu)
     if (shm > 65536) {
         static bool raised = false;   // per instantiation
         if (!raised) {
-            QIE_HIP(hipFuncSetAttribute((const void*)gemv_kernel<MT, RPW, EPI, U>,
+            QIE_HIP(hipFuncSetAttribute((const void*)gemv_kernel<MT, RPW, EPI, U, PF>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
             raised = true;
         }
     }
-    hipLaunchKernelGGL((gemv_kernel<MT, RPW, EPI, U>), dim3(grid), dim3(256), shm, st, p);
+    hipLaunchKernelGGL((gemv_kernel<MT, RPW, EPI, U, PF>), dim3(grid), dim3(256), shm, st, p);
     QIE_LAUNCH_CHECK();
     return 0;
 }
 
-template <int MT>
+template <int MT, bool PF>
 static int launch_gemv_m(const GemvParams& p, int rpw, int epi, hipStream_t st, int bpc) {
     if (epi == QIE_EPI_SWIGLU) {
-        return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_SWIGLU>(p, st, bpc)
-                        : launch_gemv_t<MT, 2, QIE_EPI_SWIGLU>(p, st, bpc);
+        return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_SWIGLU, PF>(p, st, bpc)
+                        : launch_gemv_t<MT, 2, QIE_EPI_SWIGLU, PF>(p, st, bpc);
     } else if (epi == QIE_EPI_RESIDUAL) {
-        return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_RESIDUAL>(p, st, bpc)
-                        : launch_gemv_t<MT, 2, QIE_EPI_RESIDUAL>(p, st, bpc);
+        return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_RESIDUAL, PF>(p, st, bpc)
+                        : launch_gemv_t<MT, 2, QIE_EPI_RESIDUAL, PF>(p, st, bpc);
     }
-    return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_STORE>(p, st, bpc)
-                    : launch_gemv_t<MT, 2, QIE_EPI_STORE>(p, st, bpc);
+    return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_STORE, PF>(p, st, bpc)
+                    : launch_gemv_t<MT, 2, QIE_EPI_STORE, PF>(p, st, bpc);
+}
+template <int MT>
+static int launch_gemv_pf(const GemvParams& p, int rpw, int epi, hipStream_t st, int bpc, bool pf) {
+    return pf ? launch_gemv_m<MT, true>(p, rpw, epi, st, bpc) : launch_gemv_m<MT, false>(p, rpw, epi, st, bpc);
 }
 
 static int env_int(const char* name, int dflt) {
@@ -344,11 +382,15 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
     (void)cus;
     p.n_tasks = (rows + rpw - 1) / rpw;
     const int bpc = std::max(1, env_int("QIE_GEMV_BLOCKS_PER_CU", 8));
+    // Cross-task weight prefetch (QIE_GEMV_PREFETCH=1) measured slower on every Qwen2-7B
+    // decode GEMV (qkv 11.4 vs 9.4 us): the prologue's x loads queue behind the prefetched
+    // weights (vmcnt retires in order) and occupancy drops 4 -> 3 waves/SIMD.
+    const bool pf = env_int("QIE_GEMV_PREFETCH", 0) != 0;
     switch (MT) {
-        case 1: return launch_gemv_m<1>(p, rpw, a->epilogue, st, bpc);
-        case 2: return launch_gemv_m<2>(p, rpw, a->epilogue, st, bpc);
-        case 4: return launch_gemv_m<4>(p, rpw, a->epilogue, st, bpc);
-        default: return launch_gemv_m<8>(p, rpw, a->epilogue, st, bpc);
+        case 1: return launch_gemv_pf<1>(p, rpw, a->epilogue, st, bpc, pf);
+        case 2: return launch_gemv_pf<2>(p, rpw, a->epilogue, st, bpc, pf);
+        case 4: return launch_gemv_pf<4>(p, rpw, a->epilogue, st, bpc, pf);
+        default: return launch_gemv_pf<8>(p, rpw, a->epilogue, st, bpc, pf);
     }
 }
 

@@ -105,6 +105,7 @@ def main():
         us, by = batch.time_kernel(which, 50)
         kern[name] = {"avg_us": round(us, 3), "bytes": by, "GBps": round(by / us / 1e3, 1)}
     dom = kern["gate_up_gemv"]
+    traffic, traffic_src = pmc_traffic("gate_up") if spec.name == "Qwen2-7B" and B == 1 else (None, None)
     avg_ctx = P + (a.steps + 1) / 2.0
     step_bytes = spec.decode_weight_bytes() + B * spec.kv_bytes_per_position() * avg_ctx
     step_gbs = step_bytes / (ms_step * 1e-3) / 1e9
@@ -129,7 +130,8 @@ def main():
         "prefill_ms": round(t_prefill * 1e3, 3),
         "roofline": {"bound": "hbm", "kernel": "gate_up_gemv (rms + gate/up GEMV + SwiGLU, layer 0)",
                      "achieved": dom["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(dom["GBps"] / HBM_PEAK_GBS, 4), "traffic": None},
+                     "frac": round(dom["GBps"] / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "algorithmic_bytes": dom["bytes"], "traffic_source": traffic_src},
         "step_roofline": {"bytes_per_step": step_bytes, "achieved_GBps": round(step_gbs, 1),
                           "frac": round(step_gbs / HBM_PEAK_GBS, 4),
                           "roofline_tok_s": round(HBM_PEAK_GBS * 1e9 / step_bytes * B * world, 1)},
@@ -140,6 +142,22 @@ def main():
         out["cpu_baseline"] = cpu_baseline(spec, a, batch, eng)
     if rank == 0:
         print(json.dumps(out), flush=True)
+
+
+def pmc_traffic(kernel="gate_up"):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/rNN_pmc_traffic.json: rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes over
+    tools/pmc_probe.py, same model / layer / shapes; gfx950 FETCH_SIZE correction applied
+    by tools/pmc_summary.py).  Counters cannot be read from inside this process."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    doc = json.load(open(files[-1]))
+    for k in doc["kernels"]:
+        if k["kernel"] == kernel:
+            return k["hbm_bytes"], os.path.relpath(files[-1], ROOT)
+    return None, None
 
 
 def cpu_baseline(spec, a, batch, eng):
@@ -165,14 +183,22 @@ def cpu_baseline(spec, a, batch, eng):
         lgs.append(m.forward([ids[-1]]))
         ids.append(O.argmax(lgs[-1]))
     t_dec = time.perf_counter() - t0
-    del hw, m
+    # order-sensitivity of the reference algorithm itself at full depth: the same forward
+    # with another (equally valid) matmul summation order, teacher-forced on the same ids
+    O.set_sum_order(1)
+    m1 = O.Model(hw, a.cpu_prompt + a.cpu_decode + 4, nthreads=threads)
+    lgs1 = [m1.forward(prompt, 0)] + [m1.forward([t]) for t in ids[:-1]]
+    O.set_sum_order(0)
+    del hw, m, m1
     # GPU, teacher-forced on the oracle's ids
     bf = lambda v: (np.asarray(v, np.uint16).astype(np.uint32) << 16).view(np.float32).astype(np.float64)
     t_e = batch.prefill(0, prompt)
-    max_err, tol_max, flips, hard = 0.0, 0.0, 0, 0
+    max_err, tol_max, spread_max, flips, hard = 0.0, 0.0, 0.0, 0, 0
     for i, lg in enumerate(lgs):
         ge = batch.logits()[0]
-        tol = 4 * 2.0 ** -7 * max(1.0, float(np.abs(bf(lg)).max()))
+        spread = float(np.abs(bf(lgs1[i]) - bf(lg)).max())
+        spread_max = max(spread_max, spread)
+        tol = max(4 * 2.0 ** -7 * max(1.0, float(np.abs(bf(lg)).max())), 2.0 * spread)
         max_err = max(max_err, float(np.abs(bf(ge) - bf(lg)).max()))
         tol_max = max(tol_max, tol)
         if t_e != ids[i]:
@@ -189,6 +215,8 @@ def cpu_baseline(spec, a, batch, eng):
                       f"({t_dec:.2f} s); weights generated in {t_gen:.1f} s",
             "prefill_tok_s": round(a.cpu_prompt / t_pf, 3),
             "gpu_parity": {"steps": len(lgs), "max_abs_dlogit": max_err, "tol": tol_max,
+                           "oracle_order_spread": spread_max,
+                           "tol_rule": "max(4 bf16 ulps of max|logit|, 2 x oracle order spread)",
                            "near_tie_flips": flips, "hard_mismatches": hard,
                            "ok": max_err <= tol_max and hard == 0}}
 

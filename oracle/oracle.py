@@ -50,6 +50,7 @@ def lib():
             "or_argmax_ref": (C.c_int, [P, I64]),
             "or_sample_ref": (C.c_int, [P, I64, C.c_int, F, F, C.c_uint64]),
             "or_curand_uniform_first": (F, [C.c_uint64]),
+            "or_set_sum_order": (None, [C.c_int]),
             "or_forward": (C.c_int, [C.POINTER(qlib.ModelSpecC), C.POINTER(qlib.ModelWeightsC), P, P,
                                      C.c_int, P, C.c_int, C.c_int, P, P, C.c_int]),
         }
@@ -152,6 +153,11 @@ def topk(logits, k):
     val = np.zeros(256, np.float32)
     n = lib().or_topk_ref(_p(logits), logits.size, k, _p(idx), _p(val))
     return idx[:n], val[:n]
+
+
+def set_sum_order(v: int) -> None:
+    """Matmul summation-order variant (0 default, 1 alternative; see or_set_sum_order)."""
+    lib().or_set_sum_order(int(v))
 
 
 def argmax(logits) -> int:

@@ -159,6 +159,15 @@ void or_rmsnorm(const bf16_t* x, const bf16_t* w, bf16_t* y, int64_t rows, int64
  * oracle fixes its own order: 16 fp32 partial sums over k, combined in double.)
  * Bias (Qwen2, absent in the reference): C = bf16(float(sum) + b[n]).
  */
+static int g_sum_order = 0;
+/* Summation-order variant for the matmul inner products (test infrastructure only):
+ * 0 = the order above; 1 = 64 interleaved fp32 partials over 8-element blocks
+ * (k / 8 mod 64), combined by a float pairwise tree — another order the reference's
+ * unspecified WMMA accumulation could take.  The logit spread between the two at full
+ * depth is the reference algorithm's own order sensitivity, which sizes the full-depth
+ * parity tolerance (bench.py cpu_baseline, DESIGN.md "Parity"). */
+void or_set_sum_order(int v) { g_sum_order = v; }
+
 void or_matmul(const bf16_t* A, const bf16_t* W, const bf16_t* bias, bf16_t* C,
                int64_t M, int64_t K, int64_t N, int nthreads) {
     std::vector<float> Af((size_t)M * K);
@@ -173,6 +182,17 @@ void or_matmul(const bf16_t* A, const bf16_t* W, const bf16_t* bias, bf16_t* C,
             for (int64_t k = 0; k < K; k++) wf[k] = bf2f(wr[k]);
             for (int64_t m = 0; m < M; m++) {
                 const float* ar = Af.data() + m * K;
+                if (g_sum_order == 1) {
+                    float part[64];
+                    for (int j = 0; j < 64; j++) part[j] = 0.f;
+                    for (int64_t k = 0; k < K; k++) part[(k >> 3) & 63] += ar[k] * wf[k];
+                    for (int w = 32; w > 0; w >>= 1)
+                        for (int j = 0; j < w; j++) part[j] += part[j + w];
+                    float f = part[0];
+                    if (bias) f = f + bf2f(bias[n]);
+                    C[m * N + n] = f2bf(f);
+                    continue;
+                }
                 float acc[16];
                 for (int j = 0; j < 16; j++) acc[j] = 0.f;
                 int64_t k = 0;

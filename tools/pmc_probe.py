@@ -1,0 +1,40 @@
+#!/usr/bin/env python3
+"""Fixed launch sequence for rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE): each decode
+kernel of the Qwen2-7B step (layer 0 weights, context 2048) launched ITERS times in
+isolation through qie_batch_time_kernel, in the order gate_up, down, qkv, o, lm_head,
+attention.  tools/pmc_summary.py turns the per-dispatch counters into HBM bytes per
+launch (profiles/)."""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import qwen_inference_engine_amd as Q  # noqa: E402
+from qwen_inference_engine_amd import spec as S, weights as W  # noqa: E402
+
+ITERS = int(os.environ.get("PMC_ITERS", "8"))
+ORDER = [(0, "gate_up"), (1, "down"), (2, "qkv"), (3, "o"), (4, "lm_head"), (5, "attn")]
+
+
+def main():
+    spec = S.PRESETS["Qwen2-7B"]
+    P = 2048
+    eng = Q.Engine(spec, max_ctx=P + 64).init_synthetic(W.SynthParams(seed=0))
+    b = eng.batch(1, P + 64)
+    b.prefill(0, np.random.default_rng(1).integers(0, spec.vocab, P))
+    meta = []
+    for which, name in ORDER:
+        us, by = b.time_kernel(which, ITERS)   # 1 warm-up + ITERS launches
+        meta.append({"kernel": name, "which": which, "launches": ITERS + 1, "algorithmic_bytes": by, "avg_us": us})
+    out = os.path.join(ROOT, "gpurun_out", "pmc_probe_meta.json")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    with open(out, "w") as f:
+        json.dump({"iters": ITERS, "order": meta}, f, indent=1)
+    print(json.dumps(meta))
+
+
+if __name__ == "__main__":
+    main()

@@ -30,6 +30,7 @@ extern "C" {
 #endif
 
 typedef struct qie_engine qie_engine;
+typedef struct qie_comm qie_comm;
 typedef struct qie_batch qie_batch;
 typedef struct qie_index qie_index;
 
@@ -48,12 +49,29 @@ int qie_index_write_meta(const qie_index* idx, const char* path);
 void qie_index_destroy(qie_index* idx);
 
 /* ----------------------------------------------------------------- engine */
+/* ------------------------------------------------------ tensor parallelism
+ * One communicator per rank.  RCCL: rank 0 calls qie_comm_unique_id() and ships the
+ * QIE_COMM_ID_BYTES bytes to every rank (any host channel), then every rank calls
+ * qie_comm_create_rccl() with its device (blocks until all ranks joined).  Local:
+ * qie_comm_create_local(world, out[world]) makes `world` ranks of ONE process on one
+ * device, driven by one host thread each (test backend; engines on it run without
+ * hipGraphs).  Pass the handle as qie_engine_opts.tp_comm; the engine then holds
+ * only its shard and every collective call of a step must be made by
+ * all ranks (prefill, decode, qie_batch_logits). */
+#define QIE_COMM_ID_BYTES 128
+int qie_comm_unique_id(void* id_out);
+int qie_comm_create_rccl(const void* id, int32_t world, int32_t rank, int32_t device, qie_comm** out);
+int qie_comm_create_local(int32_t world, qie_comm** out);
+int qie_comm_rank(const qie_comm* c, int32_t* world, int32_t* rank);
+int qie_comm_allreduce_sum_f32(qie_comm* c, float* buf, int64_t n, void* stream);
+void qie_comm_destroy(qie_comm* c);
+
 typedef struct qie_engine_opts {
     int32_t device;          /* HIP device ordinal                                   */
     int32_t max_ctx;         /* RoPE table rows (reference CONTEXT_SIZE = 32786)     */
     int32_t use_graph;       /* 1: decode steps replay a captured hipGraph           */
-    int32_t tp_rank, tp_size;/* tensor parallel (1 = off)                            */
-    void* tp_comm;           /* ncclComm_t for tp_size > 1 (RCCL over xGMI)          */
+    int32_t tp_rank, tp_size;/* informational; taken from tp_comm when it is set     */
+    void* tp_comm;           /* qie_comm* (tensor parallel over its ranks) or NULL   */
     int32_t reserved[8];
 } qie_engine_opts;
 

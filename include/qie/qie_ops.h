@@ -72,8 +72,10 @@ int qie_rmsnorm(const void* x, const void* w, void* y, int64_t rows, int64_t H, 
 enum {
     QIE_EPI_STORE = 0,     /* y = bf16(acc [+ bias])                                  */
     QIE_EPI_RESIDUAL = 1,  /* y = bf16(y + bf16(acc))   (launch_resadd fused)          */
-    QIE_EPI_SWIGLU = 2     /* segs (gate, up): y[m, j] = bf16(bf16(up) * bf16(silu(bf16(gate))))
+    QIE_EPI_SWIGLU = 2,    /* segs (gate, up): y[m, j] = bf16(bf16(up) * bf16(silu(bf16(gate))))
                               (SiLU.cu:10-23 + element_add.cu:4-12 fused); N = I      */
+    QIE_EPI_F32 = 3        /* y is float [M, N]: y = acc, unrounded (tensor-parallel
+                              partial sums, reduced across ranks before the rounding) */
 };
 
 typedef struct qie_linear_args {
@@ -93,6 +95,8 @@ typedef struct qie_linear_args {
     uint64_t* argmax_keys;  /* optional [M] selection keys, atomically max-merged
                                (fused greedy arg-max, logit_decode.cu:15-33); caller
                                zeroes them before the launch                            */
+    int64_t key_col0;       /* global index of output column 0 in the keys (vocab-
+                               parallel lm_head shard offset; 0 otherwise)              */
 } qie_linear_args;
 
 int qie_linear(const qie_linear_args* args, void* stream);
@@ -158,6 +162,10 @@ int qie_debug_tr16_probe(int32_t* out_dev);
  * for callers that do not use the fused linear epilogues. */
 int qie_silu_mul(const void* gate, const void* up, void* h, int64_t n, void* stream);
 int qie_residual_add(void* x, const void* y, int64_t n, void* stream);
+/* Tensor-parallel residual: x = bf16(x + bf16(sum)) with sum the fp32 all-reduced
+ * partials of the row-parallel O / down projection (same rounding as the fused
+ * QIE_EPI_RESIDUAL epilogue on one GPU). */
+int qie_residual_add_f32(void* x, const float* sum, int64_t n, void* stream);
 
 /* ---------------------------------------------------------------- sampling
  * Replaces sample_topk_bf16 / topk_temperature_softmax_sampling_kernel_bf16
@@ -182,6 +190,11 @@ int qie_synthetic_fill(void* dev, int64_t n, uint32_t tensor_id, uint64_t seed, 
                        float offset, void* stream);
 int qie_synthetic_fill_host(void* host, int64_t n, uint32_t tensor_id, uint64_t seed,
                             float scale, float offset);
+/* Tensor-parallel shard of the same synthetic tensor: dev[i][j] = element
+ * (row0 + i) * full_cols + col0 + j of the full tensor, rows x cols, row-major. */
+int qie_synthetic_fill_slice(void* dev, int64_t rows, int64_t cols, int64_t full_cols, int64_t row0,
+                             int64_t col0, uint32_t tensor_id, uint64_t seed, float scale, float offset,
+                             void* stream);
 
 #ifdef __cplusplus
 }

@@ -7,6 +7,6 @@ thin Python layer.  See DESIGN.md.
 """
 from .spec import ModelSpec, PRESETS, QWEN2_0_5B, QWEN2_7B, QWEN2_72B, QWEN3_14B, tiny  # noqa: F401
 from .weights import HostWeights, SynthParams, synthetic_index, parse_meta, format_meta  # noqa: F401
-from .engine import Engine, Batch, Sampling, GREEDY  # noqa: F401
+from .engine import Engine, Batch, Comm, Sampling, GREEDY  # noqa: F401
 
 __version__ = "0.1.0"

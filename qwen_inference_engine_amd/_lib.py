@@ -19,6 +19,8 @@ QIE_NUMERICS_HF = 1
 QIE_EPI_STORE = 0
 QIE_EPI_RESIDUAL = 1
 QIE_EPI_SWIGLU = 2
+QIE_EPI_F32 = 3
+QIE_COMM_ID_BYTES = 128
 
 
 class ModelSpecC(C.Structure):
@@ -53,7 +55,7 @@ class LinearArgsC(C.Structure):
         ("seg_rows", C.c_int64 * 3), ("M", C.c_int64), ("K", C.c_int64), ("N", C.c_int64),
         ("y", C.c_void_p), ("ldy", C.c_int64), ("epilogue", C.c_int32), ("numerics", C.c_int32),
         ("norm_w", C.c_void_p), ("norm_eps", C.c_float), ("flags", C.c_int32),
-        ("argmax_keys", C.c_void_p),
+        ("argmax_keys", C.c_void_p), ("key_col0", C.c_int64),
     ]
 
 
@@ -103,13 +105,21 @@ SIGNATURES = [
     ("qie_debug_tr16_probe", C.c_int, [_P]),
     ("qie_silu_mul", C.c_int, [_P, _P, _P, _I64, _P]),
     ("qie_residual_add", C.c_int, [_P, _P, _I64, _P]),
+    ("qie_residual_add_f32", C.c_int, [_P, _P, _I64, _P]),
     ("qie_sample_workspace_bytes", C.c_int64, [_I64, _I64]),
     ("qie_sample", C.c_int, [_P, _I64, _I64, _I64, C.POINTER(SamplingC), _P, _P, _P, _P]),
     ("qie_keys_to_ids", C.c_int, [_P, _I64, _P, _P]),
     ("qie_tensor_id", C.c_uint32, [C.c_char_p]),
     ("qie_synthetic_fill", C.c_int, [_P, _I64, _U32, _U64, _F, _F, _P]),
     ("qie_synthetic_fill_host", C.c_int, [_P, _I64, _U32, _U64, _F, _F]),
+    ("qie_synthetic_fill_slice", C.c_int, [_P, _I64, _I64, _I64, _I64, _I64, _U32, _U64, _F, _F, _P]),
     # qie_engine.h
+    ("qie_comm_unique_id", C.c_int, [_P]),
+    ("qie_comm_create_rccl", C.c_int, [_P, _I32, _I32, _I32, C.POINTER(_P)]),
+    ("qie_comm_create_local", C.c_int, [_I32, C.POINTER(_P)]),
+    ("qie_comm_rank", C.c_int, [_P, _PI32, _PI32]),
+    ("qie_comm_allreduce_sum_f32", C.c_int, [_P, _P, _I64, _P]),
+    ("qie_comm_destroy", None, [_P]),
     ("qie_index_load_meta", C.c_int, [C.c_char_p, C.POINTER(_P)]),
     ("qie_index_synthetic", C.c_int, [C.POINTER(ModelSpecC), C.POINTER(_P)]),
     ("qie_index_count", C.c_int, [_P]),

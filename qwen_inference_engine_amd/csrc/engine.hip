@@ -17,6 +17,7 @@
 #include "qie_common.hpp"
 #include "../../include/qie/qie_engine.h"
 #include "qie_index.hpp"
+#include "qie_comm.hpp"
 
 #include <chrono>
 #include <cstring>
@@ -30,8 +31,19 @@ int gemm(const qie_linear_args* a, hipStream_t st);
 
 using namespace qie;
 
+// Tensor-parallel shard of one rank (tp = 1: the whole model).  Column-parallel
+// QKV (by heads) and gate/up (by I), row-parallel O and down, vocab-parallel lm_head;
+// embedding, norms and the residual stream are replicated.
+struct TpShard {
+    int tp = 1, rank = 0;
+    int nq = 0, nkv = 0, ffn = 0, vocab = 0;   // local counts
+    int64_t vocab0 = 0;                         // first global vocab row of this rank
+};
+
 struct qie_engine {
-    qie_model_spec spec{};
+    qie_model_spec spec{};   // the full model
+    TpShard sh;              // this rank's shard
+    qie_comm* comm = nullptr;
     qie_engine_opts opts{};
     hipStream_t stream = nullptr;
     void* arena = nullptr;
@@ -65,6 +77,11 @@ struct qie_batch {
     void* attn_ws = nullptr;
     void* dec_ws = nullptr;     // fused decode attention: split partials + zeroed counters
     void* samp_ws = nullptr;
+    // tensor parallel: fp32 partials of the row-parallel projections, gathered logits
+    float* part = nullptr;            // [B][H]
+    uint16_t* logits_full = nullptr;  // [B][V]
+    uint16_t* gather_tmp = nullptr;   // [tp][B][V/tp]
+    float* pf_part = nullptr;         // [pf_rows][H]
     std::vector<int32_t> h_pos;
     // prefill scratch
     int64_t pf_rows = 0;
@@ -191,7 +208,7 @@ static int bind_from_index(qie_engine* e) {
     }
     QIE_TRY(get("embed_tokens.weight", -1, &e->w.embed, true));
     QIE_TRY(get("norm.weight", -1, &e->w.final_norm, true));
-    if (s.tie_embeddings) e->w.lm_head = e->w.embed;
+    if (s.tie_embeddings && e->sh.tp == 1) e->w.lm_head = e->w.embed;
     else QIE_TRY(get("logits", -1, &e->w.lm_head, true));
     e->w.n_layers = s.n_layers;
     e->w.layers = e->layers.data();
@@ -206,14 +223,31 @@ static qie_linear_args lin_base() {
     return a;
 }
 
+// Row-parallel projection epilogue under tensor parallelism: fp32 partials -> all-reduce
+// -> x = bf16(x + bf16(sum)); the single-GPU path fuses the residual into the GEMV/GEMM.
+static int row_parallel(qie_batch* b, qie_linear_args& a, uint16_t* x, float* part, int64_t rows) {
+    qie_engine* e = b->e;
+    if (e->sh.tp == 1) {
+        a.y = x;
+        a.epilogue = QIE_EPI_RESIDUAL;
+        return qie_linear(&a, e->stream);
+    }
+    a.y = part;
+    a.epilogue = QIE_EPI_F32;
+    QIE_TRY(qie_linear(&a, e->stream));
+    const int64_t n = rows * e->spec.hidden;
+    QIE_TRY(e->comm->allreduce_sum_f32(part, n, e->stream));
+    return qie_residual_add_f32(x, part, n, e->stream);
+}
+
 static int enqueue_layer_decode(qie_batch* b, int l) {
     qie_engine* e = b->e;
     const qie_model_spec& s = e->spec;
     const qie_layer_weights& L = e->layers[l];
     hipStream_t st = e->stream;
-    const int64_t H = s.hidden, hd = s.head_dim, QD = (int64_t)s.n_heads * hd, KD = (int64_t)s.n_kv_heads * hd;
-    const int64_t QKVD = QD + 2 * KD, I = s.ffn, B = b->B;
-    qie_kv_cache cache{b->kc, b->vc, b->seq_stride, s.n_layers, s.n_kv_heads, s.head_dim, b->max_ctx};
+    const int64_t H = s.hidden, hd = s.head_dim, QD = (int64_t)e->sh.nq * hd, KD = (int64_t)e->sh.nkv * hd;
+    const int64_t QKVD = QD + 2 * KD, I = e->sh.ffn, B = b->B;
+    qie_kv_cache cache{b->kc, b->vc, b->seq_stride, s.n_layers, e->sh.nkv, s.head_dim, b->max_ctx};
 
     qie_linear_args a = lin_base();
     a.x = b->x_res; a.ldx = H;
@@ -226,16 +260,15 @@ static int enqueue_layer_decode(qie_batch* b, int l) {
     a.norm_w = L.attn_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
     QIE_TRY(gemv(&a, st));
 
-    QIE_TRY(qie_attention_decode(b->qkv, B, b->d_pos, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, s.n_heads,
+    QIE_TRY(qie_attention_decode(b->qkv, B, b->d_pos, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, e->sh.nq,
                                  &cache, l, s.rms_eps, s.numerics, b->att, b->dec_ws, st));
 
     a = lin_base();
     a.x = b->att; a.ldx = QD;
     a.w[0] = L.wo; a.seg_rows[0] = H;
     a.M = B; a.K = QD; a.N = H;
-    a.y = b->x_res; a.ldy = H;
-    a.epilogue = QIE_EPI_RESIDUAL;
-    QIE_TRY(gemv(&a, st));
+    a.ldy = H;
+    QIE_TRY(row_parallel(b, a, b->x_res, b->part, B));
 
     a = lin_base();
     a.x = b->x_res; a.ldx = H;
@@ -250,13 +283,33 @@ static int enqueue_layer_decode(qie_batch* b, int l) {
     a.x = b->h; a.ldx = I;
     a.w[0] = L.w_down; a.seg_rows[0] = H;
     a.M = B; a.K = I; a.N = H;
-    a.y = b->x_res; a.ldy = H;
-    a.epilogue = QIE_EPI_RESIDUAL;
-    QIE_TRY(gemv(&a, st));
-    return 0;
+    a.ldy = H;
+    return row_parallel(b, a, b->x_res, b->part, B);
 }
 
 static bool is_greedy(const qie_sampling* s) { return !s || s->top_k <= 1 || !(s->temperature > 0.f); }
+
+// tmp[r][i][j] (rank r's logit shard of row i) -> full[m0 + i][r * Vl + j]
+__global__ void unshard_rows_kernel(const uint16_t* __restrict__ tmp, uint16_t* __restrict__ full, int tp, int M,
+                                    int64_t Vl, int64_t V, int m0) {
+    const int64_t n = (int64_t)tp * M * Vl;
+    for (int64_t k = blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256) {
+        const int64_t j = k % Vl, i = (k / Vl) % M, r = k / (Vl * M);
+        full[(m0 + i) * V + r * Vl + j] = tmp[k];
+    }
+}
+
+// all-gather of the vocab-parallel logits of rows [m0, m0 + M) into logits_full
+static int gather_logits(qie_batch* b, int m0, int M) {
+    qie_engine* e = b->e;
+    const int64_t Vl = e->sh.vocab;
+    QIE_TRY(e->comm->allgather(b->logits + (int64_t)m0 * Vl, b->gather_tmp, (int64_t)M * Vl * 2, e->stream));
+    const int64_t n = (int64_t)e->sh.tp * M * Vl;
+    hipLaunchKernelGGL(unshard_rows_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)), dim3(256), 0,
+                       e->stream, b->gather_tmp, b->logits_full, e->sh.tp, M, Vl, (int64_t)e->spec.vocab, m0);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
 
 // lm_head over rows [m0, m0+M) of x (already the residual stream), then the
 // sampler; leaves ids in d_keys (greedy) or d_ids.
@@ -264,19 +317,29 @@ static int enqueue_head(qie_batch* b, const uint16_t* x, int64_t ldx, int m0, in
     qie_engine* e = b->e;
     const qie_model_spec& s = e->spec;
     hipStream_t st = e->stream;
+    const int64_t Vl = e->sh.vocab;
     qie_linear_args a = lin_base();
     a.x = x; a.ldx = ldx;
-    a.w[0] = e->w.lm_head; a.seg_rows[0] = s.vocab;
-    a.M = M; a.K = s.hidden; a.N = s.vocab;
-    a.y = b->logits + (int64_t)m0 * s.vocab; a.ldy = s.vocab;
+    a.w[0] = e->w.lm_head; a.seg_rows[0] = Vl;
+    a.M = M; a.K = s.hidden; a.N = Vl;
+    a.y = b->logits + (int64_t)m0 * Vl; a.ldy = Vl;
     a.epilogue = QIE_EPI_STORE;
     a.norm_w = e->w.final_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
     const bool greedy = is_greedy(smp);
-    if (greedy) a.argmax_keys = (uint64_t*)(b->d_keys + m0);
+    if (greedy) {
+        a.argmax_keys = (uint64_t*)(b->d_keys + m0);
+        a.key_col0 = e->sh.vocab0;   // keys carry global vocab ids
+    }
     QIE_TRY(gemv(&a, st));
-    if (!greedy)
-        QIE_TRY(qie_sample(b->logits + (int64_t)m0 * s.vocab, M, s.vocab, s.vocab, smp, b->d_step + m0,
-                           b->d_ids + m0, b->samp_ws, st));
+    if (greedy && e->sh.tp > 1) QIE_TRY(e->comm->allreduce_max_u64((uint64_t*)(b->d_keys + m0), M, st));
+    if (!greedy) {
+        const uint16_t* lg = b->logits + (int64_t)m0 * Vl;
+        if (e->sh.tp > 1) {   // every rank samples the same draw from the gathered row
+            QIE_TRY(gather_logits(b, m0, M));
+            lg = b->logits_full + (int64_t)m0 * s.vocab;
+        }
+        QIE_TRY(qie_sample(lg, M, s.vocab, s.vocab, smp, b->d_step + m0, b->d_ids + m0, b->samp_ws, st));
+    }
     hipLaunchKernelGGL(finalize_kernel, dim3(M), dim3(256), 0, st, m0, greedy ? b->d_keys : nullptr,
                        b->d_ids, b->d_ids, b->d_pos, b->d_step, b->d_hist, b->max_ctx,
                        (const uint4*)e->w.embed, (uint4*)b->x_res, (int64_t)s.hidden / 8, s.vocab);
@@ -292,19 +355,22 @@ static int enqueue_decode(qie_batch* b, const qie_sampling* smp) {
 static int ensure_prefill_scratch(qie_batch* b, int64_t n) {
     if (n <= b->pf_rows) return 0;
     const qie_model_spec& s = b->e->spec;
-    const int64_t H = s.hidden, QD = (int64_t)s.n_heads * s.head_dim, KD = (int64_t)s.n_kv_heads * s.head_dim;
+    const TpShard& sh = b->e->sh;
+    const int64_t H = s.hidden, QD = (int64_t)sh.nq * s.head_dim, KD = (int64_t)sh.nkv * s.head_dim;
     hipFree(b->pf_x); hipFree(b->pf_hn); hipFree(b->pf_qkv); hipFree(b->pf_q); hipFree(b->pf_att);
-    hipFree(b->pf_h); hipFree(b->pf_pos); hipFree(b->pf_ids); hipFree(b->pf_attn_ws);
+    hipFree(b->pf_h); hipFree(b->pf_pos); hipFree(b->pf_ids); hipFree(b->pf_attn_ws); hipFree(b->pf_part);
+    b->pf_part = nullptr;
     b->pf_rows = 0;
+    if (sh.tp > 1) QIE_TRY(dmalloc((void**)&b->pf_part, n * H * 4));
     QIE_TRY(dmalloc((void**)&b->pf_x, n * H * 2));
     QIE_TRY(dmalloc((void**)&b->pf_hn, n * H * 2));
     QIE_TRY(dmalloc((void**)&b->pf_qkv, n * (QD + 2 * KD) * 2));
     QIE_TRY(dmalloc((void**)&b->pf_q, n * QD * 2));
     QIE_TRY(dmalloc((void**)&b->pf_att, n * QD * 2));
-    QIE_TRY(dmalloc((void**)&b->pf_h, n * (int64_t)s.ffn * 2));
+    QIE_TRY(dmalloc((void**)&b->pf_h, n * (int64_t)sh.ffn * 2));
     QIE_TRY(dmalloc((void**)&b->pf_pos, n * 4));
     QIE_TRY(dmalloc((void**)&b->pf_ids, n * 4));
-    int64_t ws = qie_attention_workspace_bytes(n, s.n_heads, s.head_dim, b->max_ctx);
+    int64_t ws = qie_attention_workspace_bytes(n, sh.nq, s.head_dim, b->max_ctx);
     QIE_TRY(dmalloc(&b->pf_attn_ws, (size_t)ws));
     b->pf_rows = n;
     return 0;
@@ -329,11 +395,27 @@ int qie_engine_create(const qie_model_spec* spec, const qie_engine_opts* opts, q
                 "qie_engine_create: invalid model spec");
     QIE_REQUIRE(s.hidden % 8 == 0 && s.ffn % 8 == 0 && (s.head_dim == 64 || s.head_dim == 128),
                 "qie_engine_create: hidden/ffn must be multiples of 8 and head_dim 64 or 128");
+    qie_comm* comm = opts ? (qie_comm*)opts->tp_comm : nullptr;
+    const int tp = comm ? comm->world : 1;
+    QIE_REQUIRE(s.n_heads % tp == 0 && s.n_kv_heads % tp == 0 && s.ffn % tp == 0 && (s.ffn / tp) % 8 == 0 &&
+                    s.vocab % tp == 0,
+                "qie_engine_create: tensor parallel %d needs n_heads, n_kv_heads, vocab divisible by it and "
+                "ffn / tp a multiple of 8 (use replicas for this model at this size)", tp);
     qie_engine* e = new qie_engine();
     e->spec = s;
     if (opts) e->opts = *opts;
     if (e->opts.max_ctx <= 0) e->opts.max_ctx = 32786;   // reference CONTEXT_SIZE (iengine.cuh:19)
-    if (e->opts.tp_size <= 0) e->opts.tp_size = 1;
+    e->comm = comm;
+    e->sh.tp = tp;
+    e->sh.rank = comm ? comm->rank : 0;
+    e->sh.nq = s.n_heads / tp;
+    e->sh.nkv = s.n_kv_heads / tp;
+    e->sh.ffn = s.ffn / tp;
+    e->sh.vocab = s.vocab / tp;
+    e->sh.vocab0 = (int64_t)e->sh.rank * e->sh.vocab;
+    e->opts.tp_size = tp;
+    e->opts.tp_rank = e->sh.rank;
+    if (comm && !comm->graph_capturable()) e->opts.use_graph = 0;
     hipError_t he = hipSetDevice(e->opts.device);
     if (he != hipSuccess) {
         delete e;
@@ -364,8 +446,107 @@ static int alloc_arena_synthetic(qie_engine* e) {
     return 0;
 }
 
+// This rank's part of one full tensor: rows [row0, row0 + rows) x cols [col0, col0 + cols)
+// of the row-major [full_rows, full_cols] tensor `src` (1-D tensors are one row).
+struct ShardSlice {
+    const qie_index_entry* src = nullptr;
+    int64_t rows = 0, cols = 0, full_cols = 0, row0 = 0, col0 = 0;
+};
+
+static ShardSlice plan_slice(const qie_index_entry& t, const qie_model_spec& s, const TpShard& sh) {
+    ShardSlice x;
+    x.src = &t;
+    const int64_t d0 = t.shape.empty() ? 1 : t.shape[0];
+    const int64_t d1 = t.shape.size() >= 2 ? t.shape[1] : 1;
+    const bool two_d = t.shape.size() >= 2;
+    x.rows = two_d ? d0 : 1;
+    x.cols = two_d ? d1 : d0;
+    x.full_cols = x.cols;
+    const int64_t hd = s.head_dim;
+    const std::string& n = t.short_name;
+    auto rows_part = [&](int64_t local) { x.rows = local; x.row0 = (int64_t)sh.rank * local; };
+    auto cols_part = [&](int64_t local) { x.cols = local; x.col0 = (int64_t)sh.rank * local; };
+    if (sh.tp == 1) return x;
+    if (n == "self_attn.q_proj.weight") rows_part(sh.nq * hd);                        // column-parallel
+    else if (n == "self_attn.k_proj.weight" || n == "self_attn.v_proj.weight") rows_part(sh.nkv * hd);
+    else if (n == "self_attn.q_proj.bias") cols_part(sh.nq * hd);
+    else if (n == "self_attn.k_proj.bias" || n == "self_attn.v_proj.bias") cols_part(sh.nkv * hd);
+    else if (n == "self_attn.o_proj.weight") cols_part(sh.nq * hd);                   // row-parallel
+    else if (n == "mlp.gate_proj.weight" || n == "mlp.up_proj.weight") rows_part(sh.ffn);
+    else if (n == "mlp.down_proj.weight") cols_part(sh.ffn);
+    else if (n == "logits") rows_part(sh.vocab);                                      // vocab-parallel
+    return x;
+}
+
+// Shard index: same names / roles as the full index, local shapes and arena offsets
+// (256-B aligned).  A tied lm_head becomes a vocab slice of the embedding under tp > 1.
+static int build_shard_index(qie_engine* e, const qie_index* full, qie_index** out, std::vector<ShardSlice>& sl) {
+    qie_index* idx = new qie_index();
+    sl.clear();
+    int64_t off = 0;
+    auto add = [&](const qie_index_entry& src, const ShardSlice& x, const char* short_name) {
+        qie_index_entry le;
+        le.name = src.name;
+        le.short_name = short_name ? short_name : src.short_name;
+        le.layer = src.layer;
+        le.shape = src.shape.size() >= 2 ? std::vector<int64_t>{x.rows, x.cols} : std::vector<int64_t>{x.cols};
+        le.off0 = off;
+        le.off1 = off + x.rows * x.cols * 2;
+        off = (le.off1 + 255) / 256 * 256;
+        idx->t.push_back(le);
+        sl.push_back(x);
+    };
+    for (const auto& t : full->t) add(t, plan_slice(t, e->spec, e->sh), nullptr);
+    if (e->spec.tie_embeddings && e->sh.tp > 1) {
+        const qie_index_entry* emb = index_find(full, "embed_tokens.weight", -1);
+        if (!emb) {
+            delete idx;
+            return fail(-22, "tied lm_head: embed_tokens.weight missing from index");
+        }
+        qie_index_entry as_logits = *emb;
+        as_logits.short_name = "logits";
+        ShardSlice x = plan_slice(as_logits, e->spec, e->sh);
+        x.src = emb;
+        add(*emb, x, "logits");
+    }
+    *out = idx;
+    return 0;
+}
+
+static int init_synthetic_sharded(qie_engine* e, uint64_t seed, float w_scale, float norm_scale, float bias_scale) {
+    qie_index* full = nullptr;
+    QIE_TRY(qie_index_synthetic(&e->spec, &full));
+    std::vector<ShardSlice> sl;
+    qie_index* local = nullptr;
+    int rc = build_shard_index(e, full, &local, sl);
+    if (!rc) {
+        if (e->index) qie_index_destroy(e->index);
+        e->index = local;
+        e->arena_bytes = (size_t)(local->t.empty() ? 16 : local->t.back().off1);
+        if (e->arena) hipFree(e->arena);
+        e->arena = nullptr;
+        hipError_t he = hipMalloc(&e->arena, e->arena_bytes);
+        if (he != hipSuccess) rc = fail((int)he, "weight arena (%zu bytes): %s", e->arena_bytes, hipGetErrorString(he));
+    }
+    for (size_t i = 0; !rc && i < sl.size(); i++) {
+        const qie_index_entry& le = local->t[i];
+        const ShardSlice& x = sl[i];
+        const std::string& sn = x.src->short_name;
+        float scale = w_scale, offset = 0.f;
+        if (sn.find("norm") != std::string::npos) { scale = norm_scale; offset = 1.0f; }
+        else if (sn.find("bias") != std::string::npos) { scale = bias_scale; }
+        rc = qie_synthetic_fill_slice((char*)e->arena + le.off0, x.rows, x.cols, x.full_cols, x.row0, x.col0,
+                                      qie_tensor_id(x.src->name.c_str()), seed, scale, offset, e->stream);
+    }
+    qie_index_destroy(full);   // slices point into it only during the fill
+    if (rc) return rc;
+    QIE_HIP(hipStreamSynchronize(e->stream));
+    return bind_from_index(e);
+}
+
 int qie_engine_init_synthetic(qie_engine* e, uint64_t seed, float w_scale, float norm_scale, float bias_scale) {
     QIE_REQUIRE(e, "qie_engine_init_synthetic: null engine");
+    if (e->sh.tp > 1) return init_synthetic_sharded(e, seed, w_scale, norm_scale, bias_scale);
     QIE_TRY(alloc_arena_synthetic(e));
     const int n = qie_index_count(e->index);
     for (int i = 0; i < n; i++) {
@@ -384,8 +565,58 @@ int qie_engine_init_synthetic(qie_engine* e, uint64_t seed, float w_scale, float
     return bind_from_index(e);
 }
 
+// Tensor-parallel load: each rank reads only its slices of weights.bin (row slices in
+// one read, column slices row by row) — 1/tp of the bytes per rank for the big tensors.
+static int load_weights_sharded(qie_engine* e, const char* weights_bin, const char* meta) {
+    qie_index* full = nullptr;
+    QIE_TRY(qie_index_load_meta(meta, &full));
+    std::vector<ShardSlice> sl;
+    qie_index* local = nullptr;
+    int rc = build_shard_index(e, full, &local, sl);
+    if (rc) {
+        qie_index_destroy(full);
+        return rc;
+    }
+    if (e->index) qie_index_destroy(e->index);
+    e->index = local;
+    e->arena_bytes = (size_t)(local->t.empty() ? 16 : local->t.back().off1);
+    if (e->arena) hipFree(e->arena);
+    e->arena = nullptr;
+    std::ifstream f(weights_bin, std::ios::binary);
+    if (!f.good()) rc = fail(-2, "cannot open %s", weights_bin);
+    if (!rc) {
+        hipError_t he = hipMalloc(&e->arena, e->arena_bytes);
+        if (he != hipSuccess) rc = fail((int)he, "weight arena: %s", hipGetErrorString(he));
+    }
+    std::vector<uint16_t> host;
+    for (size_t i = 0; !rc && i < sl.size(); i++) {
+        const ShardSlice& x = sl[i];
+        host.resize((size_t)(x.rows * x.cols));
+        if (x.cols == x.full_cols) {
+            f.seekg(x.src->off0 + x.row0 * x.full_cols * 2);
+            f.read((char*)host.data(), x.rows * x.cols * 2);
+            if (!f) rc = fail(-5, "short read of %s (%s)", weights_bin, x.src->name.c_str());
+        } else {
+            for (int64_t r = 0; r < x.rows && !rc; r++) {
+                f.seekg(x.src->off0 + ((x.row0 + r) * x.full_cols + x.col0) * 2);
+                f.read((char*)(host.data() + r * x.cols), x.cols * 2);
+                if (!f) rc = fail(-5, "short read of %s (%s)", weights_bin, x.src->name.c_str());
+            }
+        }
+        if (!rc) {
+            hipError_t he = hipMemcpy((char*)e->arena + local->t[i].off0, host.data(), (size_t)(x.rows * x.cols * 2),
+                                      hipMemcpyHostToDevice);
+            if (he != hipSuccess) rc = fail((int)he, "H2D: %s", hipGetErrorString(he));
+        }
+    }
+    qie_index_destroy(full);
+    if (rc) return rc;
+    return bind_from_index(e);
+}
+
 int qie_engine_load_weights_bin(qie_engine* e, const char* weights_bin, const char* meta, int64_t chunk_bytes) {
     QIE_REQUIRE(e && weights_bin && meta, "qie_engine_load_weights_bin: bad arguments");
+    if (e->sh.tp > 1) return load_weights_sharded(e, weights_bin, meta);
     if (e->index) qie_index_destroy(e->index);
     e->index = nullptr;
     QIE_TRY(qie_index_load_meta(meta, &e->index));
@@ -496,8 +727,9 @@ int qie_batch_create(qie_engine* e, int32_t batch, int32_t max_ctx, qie_batch** 
     b->e = e;
     b->B = batch;
     b->max_ctx = max_ctx;
-    const int64_t H = s.hidden, hd = s.head_dim, QD = (int64_t)s.n_heads * hd, KD = (int64_t)s.n_kv_heads * hd;
-    b->seq_stride = (int64_t)s.n_layers * s.n_kv_heads * max_ctx * hd;
+    const TpShard& sh = e->sh;
+    const int64_t H = s.hidden, hd = s.head_dim, QD = (int64_t)sh.nq * hd, KD = (int64_t)sh.nkv * hd;
+    b->seq_stride = (int64_t)s.n_layers * sh.nkv * max_ctx * hd;   // this rank's kv heads only
     int rc = 0;
     auto A = [&](void** p, size_t bytes) {
         if (!rc) rc = dmalloc(p, bytes);
@@ -513,12 +745,17 @@ int qie_batch_create(qie_engine* e, int32_t batch, int32_t max_ctx, qie_batch** 
     A((void**)&b->qkv, batch * (QD + 2 * KD) * 2);
     A((void**)&b->q, batch * QD * 2);
     A((void**)&b->att, batch * QD * 2);
-    A((void**)&b->h, batch * (int64_t)s.ffn * 2);
-    A((void**)&b->logits, batch * (int64_t)s.vocab * 2);
-    A(&b->attn_ws, (size_t)qie_attention_workspace_bytes(batch, s.n_heads, s.head_dim, max_ctx));
+    A((void**)&b->h, batch * (int64_t)sh.ffn * 2);
+    A((void**)&b->logits, batch * (int64_t)sh.vocab * 2);
+    A(&b->attn_ws, (size_t)qie_attention_workspace_bytes(batch, sh.nq, s.head_dim, max_ctx));
     A(&b->samp_ws, (size_t)qie_sample_workspace_bytes(batch, s.vocab));
-    const int64_t dec_ws = qie_attention_decode_workspace_bytes(batch, s.n_heads, s.n_kv_heads, s.head_dim, max_ctx);
+    const int64_t dec_ws = qie_attention_decode_workspace_bytes(batch, sh.nq, sh.nkv, s.head_dim, max_ctx);
     A(&b->dec_ws, (size_t)dec_ws);
+    if (sh.tp > 1) {
+        A((void**)&b->part, batch * H * 4);
+        A((void**)&b->logits_full, batch * (int64_t)s.vocab * 2);
+        A((void**)&b->gather_tmp, batch * (int64_t)s.vocab * 2);
+    }
     if (!rc) {
         hipMemsetAsync(b->dec_ws, 0, (size_t)dec_ws, e->stream);
         hipMemsetAsync(b->kc, 0, (size_t)batch * b->seq_stride * 2, e->stream);
@@ -547,7 +784,8 @@ void qie_batch_destroy(qie_batch* b) {
     if (b->gexec) hipGraphExecDestroy(b->gexec);
     void* ps[] = {b->kc, b->vc, b->d_pos, b->d_step, b->d_hist, b->d_ids, b->d_keys, b->x_res, b->qkv, b->q,
                   b->att, b->h, b->logits, b->attn_ws, b->dec_ws, b->samp_ws, b->pf_x, b->pf_hn, b->pf_qkv, b->pf_q,
-                  b->pf_att, b->pf_h, b->pf_pos, b->pf_ids, b->pf_attn_ws};
+                  b->pf_att, b->pf_h, b->pf_pos, b->pf_ids, b->pf_attn_ws, b->part, b->logits_full,
+                  b->gather_tmp, b->pf_part};
     for (void* p : ps)
         if (p) hipFree(p);
     delete b;
@@ -562,15 +800,16 @@ int qie_prefill(qie_batch* b, int32_t seq, const int32_t* ids, int32_t n, const 
         QIE_REQUIRE(ids[i] >= 0 && ids[i] < s.vocab, "qie_prefill: token id %d out of range", ids[i]);
     hipStream_t st = e->stream;
     QIE_TRY(ensure_prefill_scratch(b, n));
-    const int64_t H = s.hidden, hd = s.head_dim, QD = (int64_t)s.n_heads * hd, KD = (int64_t)s.n_kv_heads * hd;
-    const int64_t QKVD = QD + 2 * KD, I = s.ffn;
+    const TpShard& sh = e->sh;
+    const int64_t H = s.hidden, hd = s.head_dim, QD = (int64_t)sh.nq * hd, KD = (int64_t)sh.nkv * hd;
+    const int64_t QKVD = QD + 2 * KD, I = sh.ffn;
     QIE_HIP(hipMemcpyAsync(b->pf_ids, ids, (size_t)n * 4, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(iota_kernel, dim3((n + 255) / 256), dim3(256), 0, st, b->pf_pos, n, 0);
     hipLaunchKernelGGL(copy_ids_kernel, dim3((n + 255) / 256), dim3(256), 0, st, b->pf_ids,
                        b->d_hist + (int64_t)seq * b->max_ctx, n);
     QIE_TRY(qie_embedding(e->w.embed, b->pf_ids, b->pf_x, n, H, st));
     qie_kv_cache cache{b->kc + (int64_t)seq * b->seq_stride, b->vc + (int64_t)seq * b->seq_stride, b->seq_stride,
-                       s.n_layers, s.n_kv_heads, s.head_dim, b->max_ctx};
+                       s.n_layers, sh.nkv, s.head_dim, b->max_ctx};
     for (int l = 0; l < s.n_layers; l++) {
         const qie_layer_weights& L = e->layers[l];
         QIE_TRY(qie_rmsnorm(b->pf_x, L.attn_norm, b->pf_hn, n, H, s.rms_eps, s.numerics, st));
@@ -581,13 +820,13 @@ int qie_prefill(qie_batch* b, int32_t seq, const int32_t* ids, int32_t n, const 
         a.seg_rows[0] = QD; a.seg_rows[1] = KD; a.seg_rows[2] = KD;
         a.M = n; a.K = H; a.N = QKVD; a.y = b->pf_qkv; a.ldy = QKVD; a.epilogue = QIE_EPI_STORE;
         QIE_TRY(qie_linear(&a, st));
-        QIE_TRY(qie_qkv_post(b->pf_qkv, n, b->pf_pos, n, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, s.n_heads,
+        QIE_TRY(qie_qkv_post(b->pf_qkv, n, b->pf_pos, n, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, sh.nq,
                              &cache, l, s.rms_eps, s.numerics, b->pf_q, st));
-        QIE_TRY(qie_attention(b->pf_q, n, b->pf_pos, n, &cache, l, s.n_heads, b->pf_att, b->pf_attn_ws, st));
+        QIE_TRY(qie_attention(b->pf_q, n, b->pf_pos, n, &cache, l, sh.nq, b->pf_att, b->pf_attn_ws, st));
         a = lin_base();
         a.x = b->pf_att; a.ldx = QD; a.w[0] = L.wo; a.seg_rows[0] = H;
-        a.M = n; a.K = QD; a.N = H; a.y = b->pf_x; a.ldy = H; a.epilogue = QIE_EPI_RESIDUAL;
-        QIE_TRY(qie_linear(&a, st));
+        a.M = n; a.K = QD; a.N = H; a.ldy = H;
+        QIE_TRY(row_parallel(b, a, b->pf_x, b->pf_part, n));
         QIE_TRY(qie_rmsnorm(b->pf_x, L.ffn_norm, b->pf_hn, n, H, s.rms_eps, s.numerics, st));
         a = lin_base();
         a.x = b->pf_hn; a.ldx = H; a.w[0] = L.w_gate; a.w[1] = L.w_up; a.seg_rows[0] = I; a.seg_rows[1] = I;
@@ -595,8 +834,8 @@ int qie_prefill(qie_batch* b, int32_t seq, const int32_t* ids, int32_t n, const 
         QIE_TRY(qie_linear(&a, st));
         a = lin_base();
         a.x = b->pf_h; a.ldx = I; a.w[0] = L.w_down; a.seg_rows[0] = H;
-        a.M = n; a.K = I; a.N = H; a.y = b->pf_x; a.ldy = H; a.epilogue = QIE_EPI_RESIDUAL;
-        QIE_TRY(qie_linear(&a, st));
+        a.M = n; a.K = I; a.N = H; a.ldy = H;
+        QIE_TRY(row_parallel(b, a, b->pf_x, b->pf_part, n));
     }
     // position of the last prompt token; finalize advances it to n (the new token).
     hipLaunchKernelGGL(set_state_kernel, dim3(1), dim3(64), 0, st, seq, n - 1, 0, ids[n - 1], b->d_pos, b->d_step,
@@ -674,8 +913,13 @@ int qie_decode(qie_batch* b, int32_t n_steps, const qie_sampling* smp, int32_t* 
 
 int qie_batch_logits(qie_batch* b, void* host_out) {
     QIE_REQUIRE(b && host_out, "qie_batch_logits: bad arguments");
+    const uint16_t* src = b->logits;
+    if (b->e->sh.tp > 1) {   // collective: every rank calls this at the same point
+        QIE_TRY(gather_logits(b, 0, b->B));
+        src = b->logits_full;
+    }
     QIE_HIP(hipStreamSynchronize(b->e->stream));
-    QIE_HIP(hipMemcpy(host_out, b->logits, (size_t)b->B * b->e->spec.vocab * 2, hipMemcpyDeviceToHost));
+    QIE_HIP(hipMemcpy(host_out, src, (size_t)b->B * b->e->spec.vocab * 2, hipMemcpyDeviceToHost));
     return 0;
 }
 
@@ -713,12 +957,13 @@ int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* av
     qie_engine* e = b->e;
     const qie_model_spec& s = e->spec;
     const qie_layer_weights& L = e->layers[0];
-    const int64_t H = s.hidden, hd = s.head_dim, QD = (int64_t)s.n_heads * hd, KD = (int64_t)s.n_kv_heads * hd;
-    const int64_t I = s.ffn, B = b->B;
+    const TpShard& sh = e->sh;   // this rank's shard sizes
+    const int64_t H = s.hidden, hd = s.head_dim, QD = (int64_t)sh.nq * hd, KD = (int64_t)sh.nkv * hd;
+    const int64_t I = sh.ffn, B = b->B, V = sh.vocab;
     // scratch output so timing never disturbs the sequence state
     uint16_t* scratch = nullptr;
     QIE_TRY(dmalloc((void**)&scratch,
-                    (size_t)B * std::max<int64_t>(std::max(I, (int64_t)s.vocab), QD + 2 * KD) * 2 + B * 8 + 64));
+                    (size_t)B * std::max<int64_t>(std::max(I, V), QD + 2 * KD) * 2 + B * 8 + 64));
     qie_linear_args a = lin_base();
     double by = 0;
     if (which == 0) {
@@ -742,16 +987,16 @@ int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* av
         a.M = B; a.K = QD; a.N = H; a.y = scratch; a.ldy = H; a.epilogue = QIE_EPI_STORE;
         by = (double)H * QD * 2 + B * QD * 2 + B * H * 2;
     } else if (which == 4) {
-        a.x = b->x_res; a.ldx = H; a.w[0] = e->w.lm_head; a.seg_rows[0] = s.vocab;
-        a.M = B; a.K = H; a.N = s.vocab; a.y = scratch; a.ldy = s.vocab; a.epilogue = QIE_EPI_STORE;
+        a.x = b->x_res; a.ldx = H; a.w[0] = e->w.lm_head; a.seg_rows[0] = V;
+        a.M = B; a.K = H; a.N = V; a.y = scratch; a.ldy = V; a.epilogue = QIE_EPI_STORE;
         a.norm_w = e->w.final_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
-        a.argmax_keys = (uint64_t*)(((uintptr_t)(scratch + B * (int64_t)s.vocab) + 7) & ~(uintptr_t)7);   // as the greedy step runs it
-        by = (double)s.vocab * H * 2 + B * H * 2 + B * (double)s.vocab * 2;
+        a.argmax_keys = (uint64_t*)(((uintptr_t)(scratch + B * V) + 7) & ~(uintptr_t)7);   // as the greedy step runs it
+        by = (double)V * H * 2 + B * H * 2 + B * (double)V * 2;
     } else if (which != 5) {
         hipFree(scratch);
         return fail(-22, "qie_batch_time_kernel: unknown kernel %d", which);
     }
-    qie_kv_cache cache{b->kc, b->vc, b->seq_stride, s.n_layers, s.n_kv_heads, s.head_dim, b->max_ctx};
+    qie_kv_cache cache{b->kc, b->vc, b->seq_stride, s.n_layers, sh.nkv, s.head_dim, b->max_ctx};
     if (which == 5) {
         std::vector<int32_t> pos(B);
         hipMemcpy(pos.data(), b->d_pos, B * 4, hipMemcpyDeviceToHost);
@@ -764,7 +1009,7 @@ int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* av
     QIE_HIP(hipEventCreate(&t1));
     auto run = [&]() -> int {
         if (which == 5)
-            return qie_attention_decode(b->qkv, B, b->d_pos, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, s.n_heads,
+            return qie_attention_decode(b->qkv, B, b->d_pos, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, sh.nq,
                                         &cache, 0, s.rms_eps, s.numerics, scratch, b->dec_ws, e->stream);
         return qie_linear(&a, e->stream);
     };
@@ -798,7 +1043,9 @@ int qie_linear(const qie_linear_args* a, void* stream) {
         QIE_REQUIRE(a->seg_rows[1] == 0 || a->w[1], "qie_linear: missing weight segment 1");
         QIE_REQUIRE(a->seg_rows[2] == 0 || a->w[2], "qie_linear: missing weight segment 2");
     }
-    QIE_REQUIRE(a->epilogue >= 0 && a->epilogue <= 2, "qie_linear: bad epilogue");
+    QIE_REQUIRE(a->epilogue >= 0 && a->epilogue <= 3, "qie_linear: bad epilogue");
+    QIE_REQUIRE(a->epilogue != QIE_EPI_F32 || (a->bias[0] == nullptr && a->bias[1] == nullptr && a->bias[2] == nullptr),
+                "qie_linear: F32 (partial-sum) epilogue takes no bias");
     QIE_REQUIRE(a->argmax_keys == nullptr || a->epilogue == QIE_EPI_STORE, "qie_linear: arg-max needs STORE");
     hipStream_t st = (hipStream_t)stream;
     if (a->M <= 8) return gemv(a, st);

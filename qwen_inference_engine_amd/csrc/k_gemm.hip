@@ -186,6 +186,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
                 for (int r = 0; r < 4; r++) {
                     const int64_t row = m0 + wr * 64 + i * 16 + fq * 4 + r;
                     if (row >= p.M) continue;
+                    if constexpr (EPI == QIE_EPI_F32) {
+                        reinterpret_cast<float*>(p.C)[row * p.ldc + col] = acc[i][j][r];
+                        continue;
+                    }
                     uint16_t* dst = p.C + row * p.ldc + col;
                     if constexpr (EPI == QIE_EPI_RESIDUAL)
                         *dst = f2bf(bf2f(*dst) + rbf(acc[i][j][r]));
@@ -224,6 +228,9 @@ int gemm(const qie_linear_args* a, hipStream_t st) {
                            shm, st, p);
     } else if (a->epilogue == QIE_EPI_RESIDUAL) {
         hipLaunchKernelGGL(gemm_kernel<QIE_EPI_RESIDUAL>, dim3(gm, (unsigned)cdiv(a->N, BN)), dim3(256),
+                           shm, st, p);
+    } else if (a->epilogue == QIE_EPI_F32) {
+        hipLaunchKernelGGL(gemm_kernel<QIE_EPI_F32>, dim3(gm, (unsigned)cdiv(a->N, BN)), dim3(256),
                            shm, st, p);
     } else {
         hipLaunchKernelGGL(gemm_kernel<QIE_EPI_STORE>, dim3(gm, (unsigned)cdiv(a->N, BN)), dim3(256),

@@ -42,6 +42,7 @@ struct GemvParams {
     int M;             // runtime rows (<= MT)
     int xlds;          // 1: x staged in LDS
     unsigned long long* keys;
+    int64_t key_col0;
     int64_t n_tasks;
 };
 
@@ -254,6 +255,11 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
                         float a = rbf(g * (1.0f / (1.0f + expf(-g))));
                         yr[col[i]] = f2bf(u * a);
                     }
+                } else if constexpr (EPI == QIE_EPI_F32) {
+                    float* yf = reinterpret_cast<float*>(p.y) + (int64_t)m * p.ldy;
+#pragma unroll
+                    for (int i = 0; i < RPW; i++)
+                        if (col[i] < p.N) yf[col[i]] = acc[m][i];
                 } else if constexpr (EPI == QIE_EPI_RESIDUAL) {
 #pragma unroll
                     for (int i = 0; i < RPW; i++) {
@@ -275,7 +281,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
                         uint16_t o = f2bf(v);
                         yr[c] = o;
                         if (p.keys) {
-                            unsigned long long kk = sel_key(bf2f(o), (uint32_t)c);
+                            unsigned long long kk = sel_key(bf2f(o), (uint32_t)(c + p.key_col0));
                             best = kk > best ? kk : best;
                         }
                     }
@@ -330,6 +336,9 @@ static int launch_gemv_m(const GemvParams& p, int rpw, int epi, hipStream_t st, 
     } else if (epi == QIE_EPI_RESIDUAL) {
         return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_RESIDUAL, PF>(p, st, bpc)
                         : launch_gemv_t<MT, 2, QIE_EPI_RESIDUAL, PF>(p, st, bpc);
+    } else if (epi == QIE_EPI_F32) {
+        return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_F32, PF>(p, st, bpc)
+                        : launch_gemv_t<MT, 2, QIE_EPI_F32, PF>(p, st, bpc);
     }
     return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_STORE, PF>(p, st, bpc)
                     : launch_gemv_t<MT, 2, QIE_EPI_STORE, PF>(p, st, bpc);
@@ -367,6 +376,7 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
     p.numerics = a->numerics;
     p.M = (int)a->M;
     p.keys = (unsigned long long*)a->argmax_keys;
+    p.key_col0 = a->key_col0;
     const int MT = a->M <= 1 ? 1 : a->M <= 2 ? 2 : a->M <= 4 ? 4 : 8;
     p.xlds = ((size_t)MT * a->K * 2 <= kGemvLdsCap) ? 1 : 0;
     QIE_REQUIRE(p.xlds || !p.norm_w,

@@ -251,6 +251,22 @@ __global__ __launch_bounds__(256) void resadd_kernel(uint4* __restrict__ x, cons
     }
 }
 
+// x = bf16(x + bf16(sum)): tensor-parallel residual after the fp32 all-reduce
+__global__ __launch_bounds__(256) void resadd_f32_kernel(uint4* __restrict__ x, const float4* __restrict__ s,
+                                                         int64_t n8) {
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+        const uint4 a = x[i];
+        const float4 s0 = s[2 * i], s1 = s[2 * i + 1];
+        const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        const uint32_t aa[4] = {a.x, a.y, a.z, a.w};
+        uint32_t o[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            o[j] = pack2(bf_lo(aa[j]) + rbf(sv[2 * j]), bf_hi(aa[j]) + rbf(sv[2 * j + 1]));
+        x[i] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+}
+
 // ------------------------------------------------------ synthetic weights
 __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
     z += 0x9E3779B97F4A7C15ull;
@@ -278,6 +294,17 @@ __global__ __launch_bounds__(256) void synth_kernel(uint32_t* __restrict__ out, 
         float a = synth_value(base, 2 * i, scale, offset);
         float b = (2 * i + 1 < n) ? synth_value(base, 2 * i + 1, scale, offset) : 0.f;
         out[i] = pack2(a, b);
+    }
+}
+
+__global__ __launch_bounds__(256) void synth_slice_kernel(uint16_t* __restrict__ out, int64_t rows, int64_t cols,
+                                                          int64_t full_cols, int64_t row0, int64_t col0,
+                                                          uint64_t base, float scale, float offset) {
+#pragma clang fp contract(off)
+    const int64_t n = rows * cols;
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const int64_t r = i / cols, c = i % cols;
+        out[i] = f2bf(synth_value(base, (row0 + r) * full_cols + col0 + c, scale, offset));
     }
 }
 
@@ -443,6 +470,32 @@ int qie_residual_add(void* x, const void* y, int64_t n, void* stream) {
     unsigned grid = (unsigned)std::min<int64_t>((n8 + 255) / 256, 8192);
     hipLaunchKernelGGL(resadd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (uint4*)x,
                        (const uint4*)y, n8);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+
+int qie_residual_add_f32(void* x, const float* sum, int64_t n, void* stream) {
+    QIE_REQUIRE(x && sum && n >= 0 && n % 8 == 0 && ((uintptr_t)sum % 16) == 0,
+                "qie_residual_add_f32: bad arguments");
+    if (n == 0) return 0;
+    const int64_t n8 = n / 8;
+    const unsigned grid = (unsigned)std::min<int64_t>((n8 + 255) / 256, 8192);
+    hipLaunchKernelGGL(resadd_f32_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (uint4*)x,
+                       (const float4*)sum, n8);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+
+int qie_synthetic_fill_slice(void* dev, int64_t rows, int64_t cols, int64_t full_cols, int64_t row0,
+                             int64_t col0, uint32_t tensor_id, uint64_t seed, float scale, float offset,
+                             void* stream) {
+    QIE_REQUIRE(dev && rows >= 0 && cols >= 0 && row0 >= 0 && col0 >= 0 && col0 + cols <= full_cols,
+                "qie_synthetic_fill_slice: bad arguments");
+    const int64_t n = rows * cols;
+    if (n == 0) return 0;
+    const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 16384);
+    hipLaunchKernelGGL(synth_slice_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (uint16_t*)dev, rows,
+                       cols, full_cols, row0, col0, synth_base(tensor_id, seed), scale, offset);
     QIE_LAUNCH_CHECK();
     return 0;
 }

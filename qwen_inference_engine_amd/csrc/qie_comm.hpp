@@ -1,0 +1,26 @@
+// qie_comm.hpp — internal definition of the tensor-parallel communicator behind the
+// opaque qie_comm handle of qie_engine.h.
+//
+// Two backends:
+//   * RCCL (one process per GPU, xGMI): ncclAllReduce / ncclAllGather enqueued on the
+//     engine stream, so they are captured into the decode hipGraph;
+//   * local (test backend): `world` ranks driven by host threads of ONE process, all
+//     on one device; collectives are event waits + a host barrier + a reduction kernel.
+//     Not graph-capturable (host barriers) — engines on it run eagerly.  It exists so
+//     the sharded forward can be checked against the oracle on a one-GPU box, where
+//     RCCL refuses two ranks on one device.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+struct qie_comm {
+    int world = 1, rank = 0;
+    virtual ~qie_comm() = default;
+    // in place; every rank ends with the identical sum (ranks summed in order 0..world-1
+    // by the local backend; RCCL's ring gives one reduced value per element to all)
+    virtual int allreduce_sum_f32(float* buf, int64_t n, hipStream_t st) = 0;
+    virtual int allreduce_max_u64(uint64_t* buf, int64_t n, hipStream_t st) = 0;
+    // recv = [world][bytes], rank r's send at offset r * bytes
+    virtual int allgather(const void* send, void* recv, int64_t bytes, hipStream_t st) = 0;
+    virtual bool graph_capturable() const = 0;
+};

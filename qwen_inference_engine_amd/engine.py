@@ -64,14 +64,57 @@ def weights_struct(spec: ModelSpec, ptr: Dict[str, int]):
     return w, layers
 
 
+class Comm:
+    """Tensor-parallel communicator (qie_comm).  ``Comm.rccl(uid, world, rank, device)`` for
+    one process per GPU (rank 0 makes ``Comm.unique_id()`` and ships the bytes to the others);
+    ``Comm.local(world)`` for `world` in-process ranks on one device, one host thread each
+    (the test backend; engines on it run without hipGraphs)."""
+
+    def __init__(self, handle: int, lib, owner=None):
+        self.h, self.lib, self._owner = handle, lib, owner
+        w, r = C.c_int32(), C.c_int32()
+        _lib.check(lib.qie_comm_rank(handle, C.byref(w), C.byref(r)), "qie_comm_rank")
+        self.world, self.rank = w.value, r.value
+
+    @staticmethod
+    def unique_id() -> bytes:
+        lib = _lib.load()
+        buf = C.create_string_buffer(_lib.QIE_COMM_ID_BYTES)
+        _lib.check(lib.qie_comm_unique_id(buf), "qie_comm_unique_id")
+        return buf.raw
+
+    @staticmethod
+    def rccl(uid: bytes, world: int, rank: int, device: int) -> "Comm":
+        lib = _lib.load()
+        buf = C.create_string_buffer(uid, _lib.QIE_COMM_ID_BYTES)
+        h = C.c_void_p()
+        _lib.check(lib.qie_comm_create_rccl(buf, world, rank, device, C.byref(h)), "qie_comm_create_rccl")
+        return Comm(h.value, lib)
+
+    @staticmethod
+    def local(world: int) -> List["Comm"]:
+        lib = _lib.load()
+        hs = (C.c_void_p * world)()
+        _lib.check(lib.qie_comm_create_local(world, hs), "qie_comm_create_local")
+        return [Comm(hs[r], lib) for r in range(world)]
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            self.lib.qie_comm_destroy(self.h)
+            self.h = None
+
+
 class Engine:
-    def __init__(self, spec: ModelSpec, device: int = 0, max_ctx: int = 4096, use_graph: bool = True):
+    def __init__(self, spec: ModelSpec, device: int = 0, max_ctx: int = 4096, use_graph: bool = True,
+                 comm: Optional[Comm] = None):
         self.lib = _lib.load()
         self.spec = spec
         self._spec_c = spec.to_c()
         opts = _lib.EngineOptsC()
         opts.device, opts.max_ctx, opts.use_graph = device, max_ctx, int(use_graph)
-        opts.tp_rank, opts.tp_size = 0, 1
+        opts.tp_rank, opts.tp_size = (comm.rank, comm.world) if comm else (0, 1)
+        opts.tp_comm = comm.h if comm else None
+        self.comm = comm
         h = C.c_void_p()
         _lib.check(self.lib.qie_engine_create(C.byref(self._spec_c), C.byref(opts), C.byref(h)),
                    "qie_engine_create")

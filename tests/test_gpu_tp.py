@@ -1,0 +1,161 @@
+"""Tensor-parallel engine on ONE GPU: `world` ranks as host threads of this process on the
+local communicator backend (qie_comm_create_local), each holding only its shard —
+column-parallel QKV / gate-up, row-parallel O / down with fp32 all-reduce, vocab-parallel
+lm_head with a max-all-reduce of the arg-max keys.  RCCL itself needs one GPU per rank, so
+the RCCL backend is exercised only through its one-rank communicator here.
+
+Bar: ranks agree bit-exactly (ids, gathered logits); against the unsharded engine the
+logits are within 4 bf16 ulps of max |logit| (the split changes only the fp32 summation
+order of the row-parallel sums) and greedy ids match step by step, teacher-forced past
+near-ties exactly as tests/test_gpu_engine.py; the sharded weights.bin loader equals the
+sharded synthetic init bit-exactly.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+import gpu_util as G
+from conftest import rng
+
+import qwen_inference_engine_amd as Q
+from qwen_inference_engine_amd import spec as S, weights as W
+
+pytestmark = pytest.mark.gpu
+
+SYN = W.SynthParams(seed=11, w_scale=0.08, norm_scale=0.25, bias_scale=0.05)
+LOGIT_ULPS = 4
+CONFIGS = {
+    "qwen2-bias-hd64": (S.tiny("t-q2", n_layers=3, hidden=256, n_heads=4, n_kv_heads=2, head_dim=64, ffn=512,
+                               vocab=1000, bias=True), 2),
+    "qwen3-qknorm-hd128": (S.tiny("t-q3", n_layers=2, hidden=512, n_heads=8, n_kv_heads=2, head_dim=128, ffn=768,
+                                  vocab=1536, bias=False, qk_norm=True), 2),
+    "tied-tp4": (S.tiny("t-tied4", n_layers=2, hidden=256, n_heads=8, n_kv_heads=4, head_dim=64, ffn=512,
+                        vocab=1024, tie=True, bias=True), 4),
+}
+
+
+def logit_tol(want):
+    return LOGIT_ULPS * 2.0 ** -7 * max(1.0, float(np.abs(G.bf(want)).max()))
+
+
+def run_ranks(world, fn, timeout=300):
+    """fn(rank, comm) on `world` threads; returns the per-rank results, re-raises failures."""
+    comms = Q.Comm.local(world)
+    out, err = [None] * world, [None] * world
+
+    def body(r):
+        try:
+            out[r] = fn(r, comms[r])
+        except BaseException as ex:  # noqa: BLE001 - reported below
+            err[r] = ex
+
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout)
+        assert not t.is_alive(), "tensor-parallel rank hung"
+    for e in err:
+        if e is not None:
+            raise e
+    for c in comms:
+        c.close()
+    return out
+
+
+def greedy_trace(spec, world, prompt, n_new, forced=None):
+    """Per-rank (ids, per-step logits); `forced` = ids to teacher-force after each step."""
+    def fn(rank, comm):
+        eng = Q.Engine(spec, max_ctx=128, comm=comm).init_synthetic(SYN)
+        b = eng.batch(1, 128)
+        raw, lgs = [b.prefill(0, prompt)], []   # the engine's own choices, before forcing
+        for i in range(n_new):
+            lgs.append(b.logits()[0])
+            if forced is not None and raw[-1] != forced[i]:
+                b.set_position(0, len(prompt) + i, forced[i])
+            if i + 1 < n_new:
+                raw.append(b.decode_step()[0])
+        return raw, np.stack(lgs)
+    return run_ranks(world, fn)
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_tp_matches_single_gpu(name):
+    spec, world = CONFIGS[name]
+    prompt = list(rng(3).integers(0, spec.vocab, 13))
+    n_new = 12
+    # reference: the unsharded engine's greedy run
+    eng = Q.Engine(spec, max_ctx=128).init_synthetic(SYN)
+    b = eng.batch(1, 128)
+    ref_ids, ref_lgs = [b.prefill(0, prompt)], []
+    for i in range(n_new):
+        ref_lgs.append(b.logits()[0])
+        if i + 1 < n_new:
+            ref_ids.append(b.decode_step()[0])
+    res = greedy_trace(spec, world, prompt, n_new, forced=ref_ids)
+    ids0, lgs0 = res[0]
+    for r in range(1, world):   # ranks agree bit-exactly
+        assert res[r][0] == ids0
+        assert np.array_equal(res[r][1], lgs0)
+    flips = 0
+    for i in range(n_new):
+        d = np.abs(G.bf(lgs0[i]).astype(np.float64) - G.bf(ref_lgs[i]).astype(np.float64)).max()
+        assert d <= logit_tol(ref_lgs[i]), f"step {i}: max |dlogit| {d}"
+        t_tp = ids0[i]   # a different choice must be a near-tie of the unsharded logits
+        if t_tp != ref_ids[i]:
+            gap = abs(float(G.bf(ref_lgs[i][ref_ids[i]])) - float(G.bf(ref_lgs[i][t_tp])))
+            assert gap <= logit_tol(ref_lgs[i]), f"step {i}: tp {t_tp} vs {ref_ids[i]} gap {gap}"
+            flips += 1
+    assert flips <= 2
+
+
+def test_tp_sampling_ranks_agree():
+    spec, world = CONFIGS["qwen2-bias-hd64"]
+    prompt = list(rng(5).integers(0, spec.vocab, 9))
+    smp = Q.Sampling(top_k=50, temperature=0.7, seed=1234)
+
+    def fn(rank, comm):
+        eng = Q.Engine(spec, max_ctx=96, comm=comm).init_synthetic(SYN)
+        b = eng.batch(2, 96)
+        first = [b.prefill(s, prompt, sampling=smp) for s in range(2)]
+        return first, b.decode(10, sampling=smp).tolist()
+    res = run_ranks(world, fn)
+    assert res[0] == res[1]
+
+
+def test_tp_weights_bin_equals_synthetic(tmp_path):
+    spec, world = CONFIGS["qwen3-qknorm-hd128"]
+    hw = W.HostWeights.synthetic(spec, SYN)
+    binp, meta = str(tmp_path / "weights.bin"), str(tmp_path / "meta_data.txt")
+    hw.write_weights_bin(binp, meta)
+    prompt = [5, 9, 2, 7, 1, 3]
+
+    def fn(rank, comm):
+        out = []
+        for src in ("syn", "bin"):
+            e = Q.Engine(spec, max_ctx=64, comm=comm)
+            e = e.init_synthetic(SYN) if src == "syn" else e.load_weights_bin(binp, meta)
+            b = e.batch(1, 64)
+            ids = [b.prefill(0, prompt)] + list(b.decode(6)[:, 0])
+            out.append((ids, b.logits()))
+        return out
+    res = run_ranks(world, fn)
+    for r in range(world):
+        (i1, l1), (i2, l2) = res[r]
+        assert i1 == i2
+        assert np.array_equal(l1, l2)
+
+
+def test_rccl_single_rank_communicator():
+    """The RCCL backend end to end with world = 1 (one GPU box): unique id, init, and an
+    all-reduce on the device (identity)."""
+    lib = Q._lib.load()
+    uid = Q.Comm.unique_id()
+    c = Q.Comm.rccl(uid, 1, 0, 0)
+    x = np.arange(1024, dtype=np.float32)
+    d = G.dev(x)
+    G.check(lib.qie_comm_allreduce_sum_f32(c.h, G.p(d), 1024, None))
+    G.check(lib.qie_synchronize())
+    assert np.array_equal(G.host(d), x)
+    c.close()

@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-prompt", type=int, default=16)
     ap.add_argument("--cpu-decode", type=int, default=8)
+    ap.add_argument("--tp", action="store_true",
+                    help="tensor-parallel over all ranks (RCCL) instead of independent replicas")
     return ap.parse_args()
 
 
@@ -61,7 +63,12 @@ def main():
     spec = S.PRESETS[a.model]
     B, P = a.batch, a.prompt
     max_ctx = P + max(a.gen, a.steps, a.warmup) + 16
-    eng = Q.Engine(spec, device=local, max_ctx=max_ctx, use_graph=not a.no_graph)
+    comm = None
+    if a.tp and world > 1:   # one RCCL communicator over all ranks; the id travels by file
+        uid = Q.Comm.unique_id().hex() if rank == 0 else None
+        uid = group.allgather(uid)[0]
+        comm = Q.Comm.rccl(bytes.fromhex(uid), world, rank, local)
+    eng = Q.Engine(spec, device=local, max_ctx=max_ctx, use_graph=not a.no_graph, comm=comm)
     eng.init_synthetic(W.SynthParams(seed=0))
     batch = eng.batch(B, max_ctx)
     prompts = np.random.default_rng(1 + rank).integers(0, spec.vocab, size=(B, P), dtype=np.int32)
@@ -95,8 +102,9 @@ def main():
         t_prefill = group.max(t_prefill)
 
     ms_step = dt * 1e3 / max(a.steps, 1)
-    value = world * B * a.steps / dt
-    prefill_tok_s = world * B * P / t_prefill
+    groups = 1 if comm else world          # TP: all ranks produce ONE batch's tokens together
+    value = groups * B * a.steps / dt
+    prefill_tok_s = groups * B * P / t_prefill
 
     # ---------------- dominant kernel, timed live with hipEvents on the engine stream
     kern = {}
@@ -108,7 +116,7 @@ def main():
     traffic, traffic_src = pmc_traffic("gate_up") if spec.name == "Qwen2-7B" and B == 1 else (None, None)
     avg_ctx = P + (a.steps + 1) / 2.0
     step_bytes = spec.decode_weight_bytes() + B * spec.kv_bytes_per_position() * avg_ctx
-    step_gbs = step_bytes / (ms_step * 1e-3) / 1e9
+    step_gbs = step_bytes / (ms_step * 1e-3) / 1e9 / (world if comm else 1)   # per GPU
 
     out = {
         "metric": "decode tokens/s + prefill tok/s, Qwen2-7B bf16 batch=1, 1/2/4/8 MI355X",
@@ -119,20 +127,21 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(ms_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if comm else "weak",
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic: random-init weights at real shapes, random prompt ids",
         "config": {"workload": f"{spec.name} bf16 decode, batch={B}, prompt={P}, gen={a.gen}",
                    "batch_per_gpu": B, "prompt": P, "gen": a.gen,
-                   "parallelism": "replicas" if world > 1 else "single", "graph": not a.no_graph},
+                   "parallelism": (f"tp{world}" if comm else f"replicas{world}") if world > 1 else "single",
+                   "graph": not a.no_graph},
         "prefill_tok_s": round(prefill_tok_s, 1),
         "prefill_ms": round(t_prefill * 1e3, 3),
         "roofline": {"bound": "hbm", "kernel": "gate_up_gemv (rms + gate/up GEMV + SwiGLU, layer 0)",
                      "achieved": dom["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(dom["GBps"] / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "algorithmic_bytes": dom["bytes"], "traffic_source": traffic_src},
-        "step_roofline": {"bytes_per_step": step_bytes, "achieved_GBps": round(step_gbs, 1),
+        "step_roofline": {"bytes_per_step": step_bytes, "achieved_GBps_per_gpu": round(step_gbs, 1),
                           "frac": round(step_gbs / HBM_PEAK_GBS, 4),
                           "roofline_tok_s": round(HBM_PEAK_GBS * 1e9 / step_bytes * B * world, 1)},
         "kernels": kern,

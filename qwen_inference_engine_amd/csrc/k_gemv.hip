@@ -64,7 +64,7 @@ __device__ __forceinline__ void unpack8(u32x4 v, float* f) {
     f[6] = bf_lo(v.w); f[7] = bf_hi(v.w);
 }
 
-template <int MT, int RPW, int EPI, int U, bool PF>
+template <int MT, int RPW, int EPI, int U, int XCH>
 __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint16_t* xs = reinterpret_cast<uint16_t*>(smem);
@@ -106,13 +106,16 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
             for (int i = 0; i < RPW; i++) col[i] = task * RPW + i;
         }
     };
+    // Chunk slots past K re-read the row's last 16 B and are skipped by compute_chunk.  A
+    // load under a condition (even a per-lane one) is branched around, and at the join
+    // the waitcnt pass can no longer count it, so every later wait degrades to vmcnt(0).
     auto load_chunk = [&](const u32x4* const (&wr)[RPW], int64_t k0, u32x4 (&wv)[U][RPW]) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int64_t k = k0 + u * 512;
 #pragma unroll
-            for (int i = 0; i < RPW; i++)
-                wv[u][i] = (k < K) ? __builtin_nontemporal_load(wr[i] + (k >> 3)) : u32x4{0u, 0u, 0u, 0u};
+            for (int i = 0; i < RPW; i++)   // unconditional (clamped) loads: see below
+                wv[u][i] = __builtin_nontemporal_load(wr[i] + ((k < K ? k : K - 8) >> 3));
         }
     };
     auto compute_chunk = [&](int64_t k0, const u32x4 (&wv)[U][RPW], float (&acc)[MT][RPW]) {
@@ -138,14 +141,88 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
     const int64_t task0 = (int64_t)blockIdx.x * 4 + wave;
     const u32x4* wr[RPW];
     u32x4 wv[U][RPW];
-    if (PF && task0 < p.n_tasks) {
-        task_ptrs(task0, wr);
-        load_chunk(wr, (int64_t)lane * 8, wv);
-    }
-    __builtin_amdgcn_sched_barrier(0);
+    constexpr bool PF = XCH > 0;
 
-    // ---------------- prologue: activation rows -> LDS (optionally RMS-normed)
-    if (p.xlds) {
+    if constexpr (XCH > 0) {
+        // ---------------- x-first prologue (MT = 1, x staged in LDS, K <= 2048 * XCH; the
+        // host guarantees it).  Order of issue: this thread's x chunks (+ norm weights),
+        // then the first weight chunk of the wave's first task, THEN the x arithmetic — so
+        // the weight stream's first HBM round trip overlaps the x round trip instead of
+        // following it (vmcnt retires in order: x must be issued first).
+        constexpr int NV = XCH <= 2 ? XCH : 1;   // norm weights: fused-norm variants only (XCH <= 2)
+        const bool nrm = NV == XCH && p.norm_w != nullptr;
+        uint4 xv[XCH], nv[NV];
+#pragma unroll
+        for (int c = 0; c < XCH; c++) {
+            const int64_t k = (int64_t)tid * 8 + c * 2048;
+            const int64_t kc = k < K ? k : K - 8;   // clamped: loads stay unconditional
+            xv[c] = *reinterpret_cast<const uint4*>(p.x + kc);
+            if (c < NV) nv[c] = *reinterpret_cast<const uint4*>((nrm ? p.norm_w : p.x) + kc);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // unconditional (a wave without a task re-reads the last row): a load under a
+        // branch makes the vmcnt bookkeeping at the join wait for everything
+        task_ptrs(task0 < p.n_tasks ? task0 : p.n_tasks - 1, wr);
+        load_chunk(wr, (int64_t)lane * 8, wv);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int c = 0; c < XCH; c++) {   // opaque: x math cannot be hoisted above the weight issue
+            asm volatile("" : "+v"(xv[c].x), "+v"(xv[c].y), "+v"(xv[c].z), "+v"(xv[c].w));
+            if (c < NV) asm volatile("" : "+v"(nv[c].x), "+v"(nv[c].y), "+v"(nv[c].z), "+v"(nv[c].w));
+        }
+        bool staged = false;
+        if constexpr (NV == XCH) if (nrm) {
+            staged = true;
+            float ss = 0.f;
+#pragma unroll
+            for (int c = 0; c < XCH; c++) {
+                if ((int64_t)tid * 8 + c * 2048 >= K) continue;
+                float f[8];
+                unpack8(u32x4{xv[c].x, xv[c].y, xv[c].z, xv[c].w}, f);
+#pragma unroll
+                for (int j = 0; j < 8; j++) ss += f[j] * f[j];
+            }
+            ss = wave_sum(ss);
+            if (lane == 0) red[wave] = ss;
+            __syncthreads();
+            ss = red[0] + red[1] + red[2] + red[3];
+            const float rms = sqrtf((ss / (float)K) + p.eps);
+            const float inv = 1.0f / rms;
+            const bool hf = p.numerics == QIE_NUMERICS_HF;
+#pragma unroll
+            for (int c = 0; c < XCH; c++) {
+#pragma clang fp contract(off)
+                const int64_t k = (int64_t)tid * 8 + c * 2048;
+                if (k >= K) continue;
+                float f[8], wf[8];
+                unpack8(u32x4{xv[c].x, xv[c].y, xv[c].z, xv[c].w}, f);
+                unpack8(u32x4{nv[c].x, nv[c].y, nv[c].z, nv[c].w}, wf);
+                uint32_t o[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    float y0, y1;
+                    if (hf) {
+                        y0 = wf[2 * j] * rbf(f[2 * j] * inv);
+                        y1 = wf[2 * j + 1] * rbf(f[2 * j + 1] * inv);
+                    } else {
+                        y0 = (f[2 * j] / rms) * wf[2 * j];
+                        y1 = (f[2 * j + 1] / rms) * wf[2 * j + 1];
+                    }
+                    o[j] = pack2(y0, y1);
+                }
+                *reinterpret_cast<uint4*>(xs + k) = make_uint4(o[0], o[1], o[2], o[3]);
+            }
+        }
+        if (!staged) {
+#pragma unroll
+            for (int c = 0; c < XCH; c++) {
+                const int64_t k = (int64_t)tid * 8 + c * 2048;
+                if (k < K) *reinterpret_cast<uint4*>(xs + k) = xv[c];
+            }
+        }
+        __syncthreads();
+    } else if (p.xlds) {
+        // ---------------- prologue: activation rows -> LDS (optionally RMS-normed)
         for (int m = 0; m < MT; m++) {
             const uint16_t* xr = p.x + (int64_t)m * p.ldx;
             uint16_t* xo = xs + (int64_t)m * K;
@@ -174,10 +251,10 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
                 for (int64_t k = tid * 8; k < K; k += 2048) {
 #pragma clang fp contract(off)
                     uint4 v = *reinterpret_cast<const uint4*>(xr + k);
-                    uint4 wv = *reinterpret_cast<const uint4*>(p.norm_w + k);
+                    uint4 nw = *reinterpret_cast<const uint4*>(p.norm_w + k);
                     float f[8], wf[8];
                     unpack8(u32x4{v.x, v.y, v.z, v.w}, f);
-                    unpack8(u32x4{wv.x, wv.y, wv.z, wv.w}, wf);
+                    unpack8(u32x4{nw.x, nw.y, nw.z, nw.w}, wf);
                     uint32_t o[4];
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
@@ -308,7 +385,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
     }
 }
 
-template <int MT, int RPW, int EPI, bool PF>
+template <int MT, int RPW, int EPI, int XCH>
 static int launch_gemv_t(const GemvParams& p, hipStream_t st, int blocks_per_cu) {
     constexpr int U = (RPW >= 4) ? 4 : 8;
     const int64_t n_blocks_needed = (p.n_tasks + 3) / 4;
@@ -318,34 +395,36 @@ static int launch_gemv_t(const GemvParams& p, hipStream_t st, int blocks_per_cu)
     if (shm > 65536) {
         static bool raised = false;   // per instantiation
         if (!raised) {
-            QIE_HIP(hipFuncSetAttribute((const void*)gemv_kernel<MT, RPW, EPI, U, PF>,
+            QIE_HIP(hipFuncSetAttribute((const void*)gemv_kernel<MT, RPW, EPI, U, XCH>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
             raised = true;
         }
     }
-    hipLaunchKernelGGL((gemv_kernel<MT, RPW, EPI, U, PF>), dim3(grid), dim3(256), shm, st, p);
+    hipLaunchKernelGGL((gemv_kernel<MT, RPW, EPI, U, XCH>), dim3(grid), dim3(256), shm, st, p);
     QIE_LAUNCH_CHECK();
     return 0;
 }
 
-template <int MT, bool PF>
+template <int MT, int XCH>
 static int launch_gemv_m(const GemvParams& p, int rpw, int epi, hipStream_t st, int bpc) {
     if (epi == QIE_EPI_SWIGLU) {
-        return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_SWIGLU, PF>(p, st, bpc)
-                        : launch_gemv_t<MT, 2, QIE_EPI_SWIGLU, PF>(p, st, bpc);
+        return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_SWIGLU, XCH>(p, st, bpc)
+                        : launch_gemv_t<MT, 2, QIE_EPI_SWIGLU, XCH>(p, st, bpc);
     } else if (epi == QIE_EPI_RESIDUAL) {
-        return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_RESIDUAL, PF>(p, st, bpc)
-                        : launch_gemv_t<MT, 2, QIE_EPI_RESIDUAL, PF>(p, st, bpc);
+        return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_RESIDUAL, XCH>(p, st, bpc)
+                        : launch_gemv_t<MT, 2, QIE_EPI_RESIDUAL, XCH>(p, st, bpc);
     } else if (epi == QIE_EPI_F32) {
-        return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_F32, PF>(p, st, bpc)
-                        : launch_gemv_t<MT, 2, QIE_EPI_F32, PF>(p, st, bpc);
+        return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_F32, XCH>(p, st, bpc)
+                        : launch_gemv_t<MT, 2, QIE_EPI_F32, XCH>(p, st, bpc);
     }
-    return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_STORE, PF>(p, st, bpc)
-                    : launch_gemv_t<MT, 2, QIE_EPI_STORE, PF>(p, st, bpc);
+    return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_STORE, XCH>(p, st, bpc)
+                    : launch_gemv_t<MT, 2, QIE_EPI_STORE, XCH>(p, st, bpc);
 }
-template <int MT>
-static int launch_gemv_pf(const GemvParams& p, int rpw, int epi, hipStream_t st, int bpc, bool pf) {
-    return pf ? launch_gemv_m<MT, true>(p, rpw, epi, st, bpc) : launch_gemv_m<MT, false>(p, rpw, epi, st, bpc);
+// x-first prologue variants (MT = 1 only): XCH 2048-element x chunks per thread
+static int launch_gemv_1(const GemvParams& p, int rpw, int epi, hipStream_t st, int bpc, int xch) {
+    if (xch == 2) return launch_gemv_m<1, 2>(p, rpw, epi, st, bpc);
+    if (xch == 10) return launch_gemv_m<1, 10>(p, rpw, epi, st, bpc);
+    return launch_gemv_m<1, 0>(p, rpw, epi, st, bpc);
 }
 
 static int env_int(const char* name, int dflt) {
@@ -354,6 +433,7 @@ static int env_int(const char* name, int dflt) {
 }
 
 constexpr size_t kGemvLdsCap = 96 * 1024;
+static bool K_fits(int64_t K, int xch) { return K <= 2048 * (int64_t)xch && K % 8 == 0; }
 
 int gemv(const qie_linear_args* a, hipStream_t st) {
     GemvParams p;
@@ -392,15 +472,17 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
     (void)cus;
     p.n_tasks = (rows + rpw - 1) / rpw;
     const int bpc = std::max(1, env_int("QIE_GEMV_BLOCKS_PER_CU", 8));
-    // Cross-task weight prefetch (QIE_GEMV_PREFETCH=1) measured slower on every Qwen2-7B
-    // decode GEMV (qkv 11.4 vs 9.4 us): the prologue's x loads queue behind the prefetched
-    // weights (vmcnt retires in order) and occupancy drops 4 -> 3 waves/SIMD.
-    const bool pf = env_int("QIE_GEMV_PREFETCH", 0) != 0;
+    // x-first prologue + cross-task weight prefetch (QIE_GEMV_XFIRST, MT = 1).  A first
+    // attempt that issued the weights BEFORE x was slower everywhere (qkv 11.4 vs 9.4 us):
+    // x then queued behind the weights in the in-order vmcnt.
+    int xch = 0;
+    if (MT == 1 && p.xlds && p.M == 1 && env_int("QIE_GEMV_XFIRST", 1) != 0)
+        xch = K_fits(a->K, 2) ? 2 : (K_fits(a->K, 10) ? 10 : 0);
     switch (MT) {
-        case 1: return launch_gemv_pf<1>(p, rpw, a->epilogue, st, bpc, pf);
-        case 2: return launch_gemv_pf<2>(p, rpw, a->epilogue, st, bpc, pf);
-        case 4: return launch_gemv_pf<4>(p, rpw, a->epilogue, st, bpc, pf);
-        default: return launch_gemv_pf<8>(p, rpw, a->epilogue, st, bpc, pf);
+        case 1: return launch_gemv_1(p, rpw, a->epilogue, st, bpc, xch);
+        case 2: return launch_gemv_m<2, 0>(p, rpw, a->epilogue, st, bpc);
+        case 4: return launch_gemv_m<4, 0>(p, rpw, a->epilogue, st, bpc);
+        default: return launch_gemv_m<8, 0>(p, rpw, a->epilogue, st, bpc);
     }
 }
 

@@ -29,7 +29,7 @@ def main():
     variants += [("attn", 5, {"QIE_DEC_DBG": d}) for d in ("1", "6", "8", "16", "64")]
     for which in (0, 1, 2, 3, 4):
         variants.append((NAMES[which], which, {}))
-        variants.append((NAMES[which], which, {"QIE_GEMV_PREFETCH": "0"}))
+        variants.append((NAMES[which], which, {"QIE_GEMV_XFIRST": "0"}))
         variants.append((NAMES[which], which, {"QIE_GEMV_BLOCKS_PER_CU": "4"}))
     res = {}
     for rnd in range(3):

@@ -1079,15 +1079,412 @@ __global__ __launch_bounds__(256) void attn_decode_mfma_kernel(DecodeAttnParams 
     for (int gh = wave; gh < G; gh += 4) {   // cw[h][j] = exp(m_j - M) / sum_j l_j exp(m_j - M)
         const int64_t base = (m * nq + g * G + gh) * (int64_t)a.nsplit_max;
         float mm = -INFINITY;
-        for (int j = lane; j < nsplit; j += 64) {
-            const float mj = a.part_ml[(base + j) * 2];
-            cw[gh][j] = mj;
-            mm = fmaxf(mm, mj);
+        float ml[2][2];   // (m, l) of splits lane and lane + 64: one 8-B load each, no 2nd round trip
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const int j = lane + 64 * q;
+            const float2 v2 = j < nsplit ? *reinterpret_cast<const float2*>(&a.part_ml[(base + j) * 2])
+                                         : make_float2(-INFINITY, 0.f);
+            ml[q][0] = v2.x;
+            ml[q][1] = v2.y;
+            mm = fmaxf(mm, v2.x);
         }
+        for (int j = lane + 128; j < nsplit; j += 64) mm = fmaxf(mm, a.part_ml[(base + j) * 2]);
         mm = wave_max(mm);
         float lv = 0.f;
-        for (int j = lane; j < nsplit; j += 64) {
-            const float c = expf(cw[gh][j] - mm);
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const int j = lane + 64 * q;
+            if (j >= nsplit) continue;
+            const float c = __expf(ml[q][0] - mm);
+            cw[gh][j] = c;
+            lv += ml[q][1] * c;
+        }
+        for (int j = lane + 128; j < nsplit; j += 64) {
+            const float c = __expf(a.part_ml[(base + j) * 2] - mm);
+            cw[gh][j] = c;
+            lv += a.part_ml[(base + j) * 2 + 1] * c;
+        }
+        lv = wave_sum(lv);
+        const float inv = 1.0f / lv;
+        for (int j = lane; j < nsplit; j += 64) cw[gh][j] *= inv;
+    }
+    __syncthreads();
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int j0 = 0; j0 < nsplit; j0 += 16) {
+        if (j0 > 0) {
+#pragma unroll
+            for (int jj = 0; jj < 16; jj++) v[jj] = src4[(int64_t)min(j0 + jj, nsplit - 1) * (HD / 4)];
+        }
+#pragma unroll
+        for (int jj = 0; jj < 16; jj++) {
+            const float c = j0 + jj < nsplit ? cw[gi][j0 + jj] : 0.f;
+            acc.x = fmaf(c, v[jj].x, acc.x);
+            acc.y = fmaf(c, v[jj].y, acc.y);
+            acc.z = fmaf(c, v[jj].z, acc.z);
+            acc.w = fmaf(c, v[jj].w, acc.w);
+        }
+    }
+    if (has_item) {
+        uint16_t* dst = a.out + m * (int64_t)nq * HD + (int64_t)(g * G + gi) * HD + d4 * 4;
+        *reinterpret_cast<uint2*>(dst) = make_uint2(pack2(acc.x, acc.y), pack2(acc.z, acc.w));
+    }
+    if (tid == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---------------------------------------------------------------------------
+// Decode attention, MFMA v2 (default): as attn_decode_mfma_kernel, but the 4 waves of
+// a block split the head dimension for P.V instead of the keys, so no cross-wave
+// softmax merge is needed:
+//   * S^T for the step's 128 keys: wave w computes keys 32w..32w+31 (2 MFMA tiles),
+//     writes the raw dots to LDS, one barrier, then EVERY wave holds all 128 scores;
+//   * each wave runs the (identical) online softmax over the 128 keys itself and
+//     accumulates O for ITS d-slice (HD/4 dims: 2 tiles at hd 128) over the 4 key
+//     blocks of 32 (P in natural key order, V slice via ds_read_b64_tr_b16);
+//   * the split's partial O leaves straight from the accumulators (the v1 kernel's
+//     LDS merge of 4 waves cost ~2.7 us of a 13.5 us launch).
+struct DecPro {
+    uint4 raw, nraw;
+    float4 c0, s0, c1, s1;
+    bool is_q, is_k, is_v, pro, nrm, hf;
+};
+
+template <int HD>
+__device__ __forceinline__ DecPro dec_pro_issue(const DecodeAttnParams& a, const uint16_t* row, int g, int G, int grp,
+                                                int dl, int p, bool has_new) {
+    DecPro d;
+    d.is_q = grp < G;
+    d.is_k = grp == G;
+    d.is_v = grp == G + 1;
+    d.pro = d.is_q || ((d.is_k || d.is_v) && has_new);
+    d.hf = a.numerics == QIE_NUMERICS_HF;
+    const uint16_t* src = d.is_q ? row + (g * G + grp) * HD
+                                 : (d.is_k ? row + a.nq * HD + g * HD : row + (a.nq + a.nkv) * HD + g * HD);
+    if (!(d.is_q || d.is_k || d.is_v)) src = row;
+    d.raw = *reinterpret_cast<const uint4*>(src + dl * 8);
+    const uint16_t* nwp = d.is_q ? a.q_norm : a.k_norm;
+    d.nrm = nwp != nullptr && !d.is_v;
+    d.nraw = *reinterpret_cast<const uint4*>((nwp ? nwp : row) + dl * 8);
+    const float* cp = a.cs + (int64_t)p * (HD / 2);
+    const float* sp = a.sn + (int64_t)p * (HD / 2);
+    const int rb = d.hf ? (dl * 8) % (HD / 2) : dl * 4;
+    const int rb2 = d.hf ? rb + 4 : rb;
+    d.c0 = *reinterpret_cast<const float4*>(cp + rb);
+    d.s0 = *reinterpret_cast<const float4*>(sp + rb);
+    d.c1 = *reinterpret_cast<const float4*>(cp + rb2);
+    d.s1 = *reinterpret_cast<const float4*>(sp + rb2);
+    return d;
+}
+
+// qk-norm + RoPE of the q heads and the new k, then q -> LDS (bf16), new k/v -> cache
+// and LDS.  Branch-free (only the stores are predicated), see attn_decode_kernel.
+template <int HD>
+__device__ __forceinline__ void dec_pro_finish(const DecodeAttnParams& a, DecPro& d, int dl, int grp, int p,
+                                               uint16_t* kb, uint16_t* vb, uint16_t (*q_s)[HD],
+                                               uint16_t (*kv_new)[HD]) {
+#pragma clang fp contract(off)
+    constexpr int LPT = HD / 8;
+    pin4(d.raw); pin4(d.nraw); pin4(d.c0); pin4(d.s0); pin4(d.c1); pin4(d.s1);
+    float x[8], wv[8];
+    unpack_bf8(d.raw, x);
+    unpack_bf8(d.nraw, wv);
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; j++) ss += x[j] * x[j];
+    ss = group_sum<LPT>(ss);
+    const float rms = sqrtf((ss / (float)HD) + a.eps);
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const float xn = d.hf ? rbf(wv[j] * rbf(x[j] * (1.0f / rms))) : rbf((x[j] / rms) * wv[j]);
+        x[j] = d.nrm ? xn : x[j];
+    }
+    const float cv[8] = {d.c0.x, d.c0.y, d.c0.z, d.c0.w, d.c1.x, d.c1.y, d.c1.z, d.c1.w};
+    const float sv[8] = {d.s0.x, d.s0.y, d.s0.z, d.s0.w, d.s1.x, d.s1.y, d.s1.z, d.s1.w};
+    float o[8], y[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) o[j] = __shfl_xor(x[j], LPT / 2, 64);
+    const bool first = dl < LPT / 2;
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+        const float ya = rbf(x[j] * cv[j / 2] - x[j + 1] * sv[j / 2]);
+        const float yb = rbf(x[j + 1] * cv[j / 2] + x[j] * sv[j / 2]);
+        const float ha = first ? rbf(rbf(x[j] * cv[j]) + rbf(-o[j] * sv[j])) : rbf(rbf(x[j] * cv[j]) + rbf(o[j] * sv[j]));
+        const float hb = first ? rbf(rbf(x[j + 1] * cv[j + 1]) + rbf(-o[j + 1] * sv[j + 1]))
+                               : rbf(rbf(x[j + 1] * cv[j + 1]) + rbf(o[j + 1] * sv[j + 1]));
+        y[j] = d.hf ? ha : ya;
+        y[j + 1] = d.hf ? hb : yb;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) x[j] = d.is_v ? x[j] : y[j];
+    const uint4 packed = make_uint4(pack2(x[0], x[1]), pack2(x[2], x[3]), pack2(x[4], x[5]), pack2(x[6], x[7]));
+    if (d.is_q) {
+        *reinterpret_cast<uint4*>(&q_s[grp][dl * 8]) = packed;
+    } else if (d.pro) {
+        uint16_t* dst = (d.is_k ? kb : vb) + (int64_t)p * HD + dl * 8;
+        *reinterpret_cast<uint4*>(dst) = packed;
+        *reinterpret_cast<uint4*>(&kv_new[d.is_k ? 0 : 1][dl * 8]) = packed;
+    }
+}
+
+template <int HD>
+__global__ __launch_bounds__(256) void attn_decode_mfma2_kernel(DecodeAttnParams a) {
+#pragma clang fp contract(off)
+    constexpr int LPT = HD / 8;          // prologue: lanes per head row
+    constexpr int KSTEPS = HD / 32;      // MFMA k-steps over d for S
+    constexpr int CPR = HD / 8;          // 16-byte chunks per K row
+    constexpr int DW = HD / 4;           // output dims per wave
+    constexpr int DTW = DW / 16;         // output d tiles per wave (2 at hd 128, 1 at 64)
+    constexpr int CPW = DW / 8;          // 16-byte chunks of a V row per wave
+    constexpr int VCH = kDecMStep * CPW / 64;   // V chunks per lane per step
+    __shared__ __attribute__((aligned(16))) uint16_t q_s[16][HD];
+    __shared__ __attribute__((aligned(16))) uint16_t kv_new[2][HD];
+    __shared__ __attribute__((aligned(16))) uint16_t v_s[4][kDecMStep * DW];
+    __shared__ __attribute__((aligned(16))) float s_s[16][kDecMStep + 4];
+    __shared__ float cw[kMaxGroup][kDecMaxSplits];
+    __shared__ int last_flag;
+
+    const int64_t m = blockIdx.y;
+    const int g = blockIdx.x / a.nsplit_max, s = blockIdx.x % a.nsplit_max;
+    const int G = a.nq / a.nkv;
+    const int p = a.pos[m], ctx = p + 1;
+    const int chunk = decm_chunk(ctx, a.splits_target);
+    const int nsplit = (ctx + chunk - 1) / chunk;
+    if (s >= nsplit || (a.dbg & 64)) return;
+    const int t0 = s * chunk, t1 = min(ctx, t0 + chunk);
+    const int nstep = (t1 - t0 + kDecMStep - 1) / kDecMStep;
+    const bool has_new = (t1 == ctx);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int fr = lane & 15, gq = lane >> 4;
+    const int grp = tid / LPT, dl = tid % LPT;
+    const int QKVD = (a.nq + 2 * a.nkv) * HD;
+    const uint16_t* row = a.qkv + m * (int64_t)QKVD;
+    const int64_t head_off = (((int64_t)a.layer * a.nkv + g) * a.max_ctx) * HD;
+    uint16_t* kb = a.kc + m * a.seq_stride + head_off;
+    uint16_t* vb = a.vc + m * a.seq_stride + head_off;
+
+    // ---------------- loads: prologue operands, then step 0's K tiles and V slice
+    DecPro pr = dec_pro_issue<HD>(a, row, g, G, grp, dl, p, has_new);
+    __builtin_amdgcn_sched_barrier(0);
+    uint4 kf[2][KSTEPS], vr[VCH];
+    auto load_step = [&](int st) {
+        const int kb0 = t0 + st * kDecMStep;
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+            const int key = min(kb0 + 32 * wave + 16 * t + fr, t1 - 1);
+#pragma unroll
+            for (int ks = 0; ks < KSTEPS; ks++)
+                kf[t][ks] = *reinterpret_cast<const uint4*>(kb + (int64_t)key * HD + 32 * ks + 8 * gq);
+        }
+#pragma unroll
+        for (int i = 0; i < VCH; i++) {
+            const int c = lane + 64 * i;
+            const int key = min(kb0 + c / CPW, t1 - 1);
+            vr[i] = *reinterpret_cast<const uint4*>(vb + (int64_t)key * HD + wave * DW + (c % CPW) * 8);
+        }
+    };
+    load_step(0);
+    dec_pro_finish<HD>(a, pr, dl, grp, p, kb, vb, q_s, kv_new);
+    for (int idx = tid; idx < (16 - G) * CPR; idx += 256)   // padded q rows
+        *reinterpret_cast<uint4*>(&q_s[G + idx / CPR][(idx % CPR) * 8]) = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    if (a.dbg & 8) {
+        if (tid == 0) a.out[m] = (uint16_t)(kf[0][0].x + vr[VCH - 1].y + kf[1][KSTEPS - 1].z);
+        return;
+    }
+
+    bf16x8_t qb[KSTEPS];
+    uint4 knew[KSTEPS];
+#pragma unroll
+    for (int ks = 0; ks < KSTEPS; ks++) {
+        qb[ks] = *reinterpret_cast<const bf16x8_t*>(&q_s[fr][32 * ks + 8 * gq]);
+        knew[ks] = *reinterpret_cast<const uint4*>(&kv_new[0][32 * ks + 8 * gq]);
+    }
+    const float scale = sqrtf((float)HD);
+    float m_run = -INFINITY, l_run = 0.f;
+    f32x4_t oacc[DTW];
+#pragma unroll
+    for (int d = 0; d < DTW; d++) oacc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    uint16_t* vw = &v_s[wave][0];
+    const int q4 = fr >> 2, p4 = fr & 3;
+
+    for (int st = 0; st < nstep; st++) {
+        const int kb0 = t0 + st * kDecMStep;
+        // ---- S^T for this wave's 32 keys -> LDS (raw dots)
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+            f32x4_t sacc = f32x4_t{0.f, 0.f, 0.f, 0.f};
+            const bool nw = kb0 + 32 * wave + 16 * t + fr == p;
+#pragma unroll
+            for (int ks = 0; ks < KSTEPS; ks++)
+                sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                    __builtin_bit_cast(bf16x8_t, sel4(nw, knew[ks], kf[t][ks])), qb[ks], sacc, 0, 0, 0);
+            // C map: col = head fr, rows = keys 4 gq + r of the tile; scores s = dot / sqrt(hd)
+            // (self_attension.cu) divided once here, not by every wave that reads them
+            *reinterpret_cast<float4*>(&s_s[fr][32 * wave + 16 * t + 4 * gq]) =
+                make_float4(sacc[0] / scale, sacc[1] / scale, sacc[2] / scale, sacc[3] / scale);
+        }
+        // ---- this wave's V slice -> LDS (the new token's row from kv_new)
+#pragma unroll
+        for (int i = 0; i < VCH; i++) {
+            const int c = lane + 64 * i;
+            const int r = c / CPW, ch = c % CPW;
+            const uint4 vn = *reinterpret_cast<const uint4*>(&kv_new[1][wave * DW + ch * 8]);
+            *reinterpret_cast<uint4*>(vw + r * DW + ch * 8) = sel4(kb0 + r == p, vn, vr[i]);
+        }
+        if (st + 1 < nstep) load_step(st + 1);
+        __syncthreads();   // scores and V slices visible
+        // ---- online softmax over the step's 128 keys (every wave, identical); lane:
+        // head fr, keys 32 c + 8 gq + j (natural order, the P.V k slots)
+        float e[4][8];
+        float mt = -INFINITY;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const float4 lo = *reinterpret_cast<const float4*>(&s_s[fr][32 * c + 8 * gq]);
+            const float4 hi = *reinterpret_cast<const float4*>(&s_s[fr][32 * c + 8 * gq + 4]);
+            const float v8[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const float sc = kb0 + 32 * c + 8 * gq + j < t1 ? v8[j] : -INFINITY;
+                e[c][j] = sc;
+                mt = fmaxf(mt, sc);
+            }
+        }
+        mt = xor32_max(xor16_max(mt));
+        const float m_new = fmaxf(m_run, mt);
+        const float m_use = m_new == -INFINITY ? 0.f : m_new;
+        // __expf (v_exp_f32 on x * log2 e, ~2 ulp): every wave exponentiates all 128 scores,
+        // and the libm expf sequence was ~0.8 us of the step; the reference build itself
+        // compiles with -use_fast_math, i.e. the same approximation.
+        const float alpha = __expf(m_run - m_use);
+        float ls = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                e[c][j] = __expf(e[c][j] - m_use);
+                ls += e[c][j];
+            }
+        ls = xor32_sum(xor16_sum(ls));
+        l_run = l_run * alpha + ls;
+        m_run = m_new;
+        float ar[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) ar[r] = __shfl(alpha, gq * 4 + r, 64);
+#pragma unroll
+        for (int d = 0; d < DTW; d++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) oacc[d][r] *= ar[r];
+        // ---- O[:, slice] += P . V[:, slice], P = hi + lo
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            bf16x8_t ph, pl;
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                ph[j] = (__bf16)e[c][j];
+                pl[j] = (__bf16)(e[c][j] - (float)ph[j]);
+            }
+#pragma unroll
+            for (int d = 0; d < DTW; d++) {
+                const uint16_t* a0 = vw + (32 * c + 8 * gq + q4) * DW + 16 * d + 4 * p4;
+                const i16x4_t v0 =
+                    __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4_t*)(a0));
+                const i16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (__attribute__((address_space(3))) i16x4_t*)(a0 + 4 * DW));
+                const bf16x8_t vb8 = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+                oacc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph, vb8, oacc[d], 0, 0, 0);
+                oacc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pl, vb8, oacc[d], 0, 0, 0);
+            }
+        }
+        __syncthreads();   // scores / V slots free for the next step
+    }
+    if (a.dbg & 16) {
+        if (tid == 0) a.out[m] = (uint16_t)(oacc[0][0] + m_run);
+        return;
+    }
+
+    // ---------------- this wave's d-slice of the split result (rows = heads 4 gq + r)
+    const int nq = a.nq;
+    float lr[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) lr[r] = __shfl(l_run, gq * 4 + r, 64);
+    if (nsplit == 1) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int h = 4 * gq + r;
+            if (h >= G) continue;
+#pragma unroll
+            for (int d = 0; d < DTW; d++)
+                a.out[m * (int64_t)nq * HD + (int64_t)(g * G + h) * HD + wave * DW + 16 * d + fr] =
+                    f2bf(oacc[d][r] / lr[r]);
+        }
+        return;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int h = 4 * gq + r;
+        if (h >= G) continue;
+        const int64_t pi = (m * nq + g * G + h) * (int64_t)a.nsplit_max + s;
+        // write-through (sc1) stores: published by the drain + ticket below, no release
+        // fence (cdna_hip_programming.md, in-launch split-K reduction)
+#pragma unroll
+        for (int d = 0; d < DTW; d++)
+            __hip_atomic_store(&a.part_o[pi * HD + wave * DW + 16 * d + fr], oacc[d][r], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (wave == 0 && gq == 0 && fr < G) {
+        const int64_t pi = (m * nq + g * G + fr) * (int64_t)a.nsplit_max + s;
+        __hip_atomic_store(&a.part_ml[pi * 2], m_run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&a.part_ml[pi * 2 + 1], l_run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // ---------------- publish this split; the last arriver combines (acquire)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
+    __syncthreads();
+    if (a.dbg & 1) return;
+    unsigned* cnt = a.counters + m * a.nkv + g;
+    if (tid == 0) {
+        const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_flag = (old == (unsigned)nsplit - 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (!last_flag) return;
+    if (tid == 0 && !(a.dbg & 4)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // each (head, d4) item issues its first 16 partial loads together with the m / l loads
+    const bool has_item = tid < G * (HD / 4);
+    const int gi = has_item ? tid / (HD / 4) : 0, d4 = tid % (HD / 4);
+    const float4* src4 =
+        reinterpret_cast<const float4*>(a.part_o) + ((m * nq + g * G + gi) * (int64_t)a.nsplit_max) * (HD / 4) + d4;
+    float4 v[16];
+#pragma unroll
+    for (int jj = 0; jj < 16; jj++) v[jj] = src4[(int64_t)min(jj, nsplit - 1) * (HD / 4)];
+    __builtin_amdgcn_sched_barrier(0);
+    for (int gh = wave; gh < G; gh += 4) {   // cw[h][j] = exp(m_j - M) / sum_j l_j exp(m_j - M)
+        const int64_t base = (m * nq + g * G + gh) * (int64_t)a.nsplit_max;
+        float mm = -INFINITY;
+        float ml[2][2];   // (m, l) of splits lane and lane + 64: one 8-B load each, no 2nd round trip
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const int j = lane + 64 * q;
+            const float2 v2 = j < nsplit ? *reinterpret_cast<const float2*>(&a.part_ml[(base + j) * 2])
+                                         : make_float2(-INFINITY, 0.f);
+            ml[q][0] = v2.x;
+            ml[q][1] = v2.y;
+            mm = fmaxf(mm, v2.x);
+        }
+        for (int j = lane + 128; j < nsplit; j += 64) mm = fmaxf(mm, a.part_ml[(base + j) * 2]);
+        mm = wave_max(mm);
+        float lv = 0.f;
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const int j = lane + 64 * q;
+            if (j >= nsplit) continue;
+            const float c = __expf(ml[q][0] - mm);
+            cw[gh][j] = c;
+            lv += ml[q][1] * c;
+        }
+        for (int j = lane + 128; j < nsplit; j += 64) {
+            const float c = __expf(a.part_ml[(base + j) * 2] - mm);
             cw[gh][j] = c;
             lv += a.part_ml[(base + j) * 2 + 1] * c;
         }
@@ -1283,7 +1680,13 @@ int qie_attention_decode(const void* qkv, int64_t B, const int32_t* pos, const v
                                      attn_decode_kernel<64, 3>, attn_decode_kernel<64, 4>,
                                      attn_decode_kernel<64, 5>, attn_decode_kernel<64, 6>,
                                      attn_decode_kernel<64, 7>, attn_decode_kernel<64, 8>};
-    if (!valu) {
+    const bool v1 = getenv("QIE_DEC_MFMA1") && atoi(getenv("QIE_DEC_MFMA1")) != 0;   // A/B timing only
+    if (!valu && !v1) {
+        if (cache->head_dim == 128)
+            hipLaunchKernelGGL(attn_decode_mfma2_kernel<128>, grid, dim3(256), 0, (hipStream_t)stream, a);
+        else
+            hipLaunchKernelGGL(attn_decode_mfma2_kernel<64>, grid, dim3(256), 0, (hipStream_t)stream, a);
+    } else if (!valu) {
         if (cache->head_dim == 128)
             hipLaunchKernelGGL(attn_decode_mfma_kernel<128>, grid, dim3(256), 0, (hipStream_t)stream, a);
         else

@@ -388,18 +388,36 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
 template <int MT, int RPW, int EPI, int XCH>
 static int launch_gemv_t(const GemvParams& p, hipStream_t st, int blocks_per_cu) {
     constexpr int U = (RPW >= 4) ? 4 : 8;
-    const int64_t n_blocks_needed = (p.n_tasks + 3) / 4;
-    const int64_t cap = (int64_t)device_cu_count() * blocks_per_cu;
-    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min(n_blocks_needed, cap));
+    const void* fn = (const void*)gemv_kernel<MT, RPW, EPI, U, XCH>;
     const size_t shm = (p.xlds ? (size_t)MT * p.K * 2 : 0) + 64;
     if (shm > 65536) {
         static bool raised = false;   // per instantiation
         if (!raised) {
-            QIE_HIP(hipFuncSetAttribute((const void*)gemv_kernel<MT, RPW, EPI, U, XCH>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+            QIE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
             raised = true;
         }
     }
+    const int64_t n_blocks_needed = (p.n_tasks + 3) / 4;
+    int64_t cap = (int64_t)device_cu_count() * blocks_per_cu;
+    int64_t grid64 = std::max<int64_t>(1, std::min(n_blocks_needed, cap));
+    if (blocks_per_cu <= 0) {
+        // Balanced persistent grid (default): the grid is what fits on the chip at once, and
+        // the task count per wave is made (nearly) equal — e.g. gate/up (18,944 tasks) on
+        // 768 resident blocks: 7 rounds over 677 blocks instead of 4.6 rounds over 1024
+        // blocks, whose last 0.6 round ran the chip at 60 % of its waves.
+        static size_t cached_shm = 0;   // per instantiation: occupancy depends on LDS bytes
+        static int cached_nb = 0;
+        int nb = cached_shm == shm ? cached_nb : 0;
+        if (nb == 0) {
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 256, shm) != hipSuccess || nb < 1) nb = 2;
+            cached_shm = shm;
+            cached_nb = nb;
+        }
+        cap = (int64_t)device_cu_count() * nb;
+        const int64_t rounds = (p.n_tasks + 4 * cap - 1) / (4 * cap);
+        grid64 = std::max<int64_t>(1, (p.n_tasks + 4 * rounds - 1) / (4 * rounds));
+    }
+    const unsigned grid = (unsigned)grid64;
     hipLaunchKernelGGL((gemv_kernel<MT, RPW, EPI, U, XCH>), dim3(grid), dim3(256), shm, st, p);
     QIE_LAUNCH_CHECK();
     return 0;
@@ -471,7 +489,9 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
     if (rpw != 2 && rpw != 4) rpw = 2;
     (void)cus;
     p.n_tasks = (rows + rpw - 1) / rpw;
-    const int bpc = std::max(1, env_int("QIE_GEMV_BLOCKS_PER_CU", 8));
+    // blocks per CU cap of the grid (8: measured best for every Qwen2-7B decode GEMV but lm_head);
+    // 0 = the occupancy-balanced persistent grid (QIE_GEMV_BLOCKS_PER_CU=0)
+    const int bpc = std::max(0, env_int("QIE_GEMV_BLOCKS_PER_CU", 8));
     // x-first prologue + cross-task weight prefetch (QIE_GEMV_XFIRST, MT = 1).  A first
     // attempt that issued the weights BEFORE x was slower everywhere (qkv 11.4 vs 9.4 us):
     // x then queued behind the weights in the in-order vmcnt.

@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-prompt", type=int, default=16)
     ap.add_argument("--cpu-decode", type=int, default=8)
+    ap.add_argument("--fp8", action="store_true",
+                    help="linear weights + lm_head as OCP e4m3 with power-of-two row scales")
     ap.add_argument("--tp", action="store_true",
                     help="tensor-parallel over all ranks (RCCL) instead of independent replicas")
     return ap.parse_args()
@@ -68,7 +70,7 @@ def main():
         uid = Q.Comm.unique_id().hex() if rank == 0 else None
         uid = group.allgather(uid)[0]
         comm = Q.Comm.rccl(bytes.fromhex(uid), world, rank, local)
-    eng = Q.Engine(spec, device=local, max_ctx=max_ctx, use_graph=not a.no_graph, comm=comm)
+    eng = Q.Engine(spec, device=local, max_ctx=max_ctx, use_graph=not a.no_graph, comm=comm, weight_fp8=a.fp8)
     eng.init_synthetic(W.SynthParams(seed=0))
     batch = eng.batch(B, max_ctx)
     prompts = np.random.default_rng(1 + rank).integers(0, spec.vocab, size=(B, P), dtype=np.int32)
@@ -113,9 +115,9 @@ def main():
         us, by = batch.time_kernel(which, 50)
         kern[name] = {"avg_us": round(us, 3), "bytes": by, "GBps": round(by / us / 1e3, 1)}
     dom = kern["gate_up_gemv"]
-    traffic, traffic_src = pmc_traffic("gate_up") if spec.name == "Qwen2-7B" and B == 1 else (None, None)
+    traffic, traffic_src = pmc_traffic("gate_up") if spec.name == "Qwen2-7B" and B == 1 and not a.fp8 else (None, None)
     avg_ctx = P + (a.steps + 1) / 2.0
-    step_bytes = spec.decode_weight_bytes() + B * spec.kv_bytes_per_position() * avg_ctx
+    step_bytes = spec.decode_weight_bytes(fp8=a.fp8) + B * spec.kv_bytes_per_position() * avg_ctx
     step_gbs = step_bytes / (ms_step * 1e-3) / 1e9 / (world if comm else 1)   # per GPU
 
     out = {
@@ -129,9 +131,9 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if comm else "weak",
         "vs_baseline": None,
-        "dtype": "bf16",
+        "dtype": "fp8-e4m3 weights, bf16 activations / fp32 accumulate" if a.fp8 else "bf16",
         "data": "synthetic: random-init weights at real shapes, random prompt ids",
-        "config": {"workload": f"{spec.name} bf16 decode, batch={B}, prompt={P}, gen={a.gen}",
+        "config": {"workload": f"{spec.name} {'fp8' if a.fp8 else 'bf16'} decode, batch={B}, prompt={P}, gen={a.gen}",
                    "batch_per_gpu": B, "prompt": P, "gen": a.gen,
                    "parallelism": (f"tp{world}" if comm else f"replicas{world}") if world > 1 else "single",
                    "graph": not a.no_graph},
@@ -147,7 +149,7 @@ def main():
         "kernels": kern,
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.fp8 and B == 1:
         out["cpu_baseline"] = cpu_baseline(spec, a, batch, eng)
     if rank == 0:
         print(json.dumps(out), flush=True)

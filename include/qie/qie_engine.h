@@ -72,7 +72,9 @@ typedef struct qie_engine_opts {
     int32_t use_graph;       /* 1: decode steps replay a captured hipGraph           */
     int32_t tp_rank, tp_size;/* informational; taken from tp_comm when it is set     */
     void* tp_comm;           /* qie_comm* (tensor parallel over its ranks) or NULL   */
-    int32_t reserved[8];
+    int32_t weight_fp8;      /* 1: linear weights + lm_head quantised to OCP e4m3 with
+                                power-of-two row scales after loading (qie_ops.h)     */
+    int32_t reserved[7];
 } qie_engine_opts;
 
 int qie_engine_create(const qie_model_spec* spec, const qie_engine_opts* opts, qie_engine** out);

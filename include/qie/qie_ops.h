@@ -91,7 +91,7 @@ typedef struct qie_linear_args {
     int32_t numerics;       /* for the fused norm                                       */
     const void* norm_w;     /* optional fused RMSNorm of x (weight [K]); GEMV path only */
     float norm_eps;
-    int32_t flags;          /* reserved, 0                                              */
+    int32_t flags;          /* QIE_LINEAR_FP8: w[i] are fp8 weights (see below); else 0  */
     uint64_t* argmax_keys;  /* optional [M] selection keys, atomically max-merged
                                (fused greedy arg-max, logit_decode.cu:15-33); caller
                                zeroes them before the launch                            */
@@ -190,6 +190,17 @@ int qie_synthetic_fill(void* dev, int64_t n, uint32_t tensor_id, uint64_t seed, 
                        float offset, void* stream);
 int qie_synthetic_fill_host(void* host, int64_t n, uint32_t tensor_id, uint64_t seed,
                             float scale, float offset);
+/* ------------------------------------------------------------ fp8 weights
+ * A linear weight [rows, cols] in fp8 is rows*cols OCP e4m3 codes followed by rows fp32
+ * power-of-two row scales (qie_fp8_weight_bytes); every dequantised value is exactly a
+ * bf16.  qie_linear reads such weights when args.flags has QIE_LINEAR_FP8. */
+#define QIE_LINEAR_FP8 1
+int64_t qie_fp8_weight_bytes(int64_t rows, int64_t cols);
+int qie_quantize_fp8(const void* w_bf16, int64_t rows, int64_t cols, void* out, void* stream);
+int qie_quantize_fp8_host(const void* w_bf16, int64_t rows, int64_t cols, void* out);
+/* Test probe: out_dev[i] = the device decode of e4m3 code i (i < 256). */
+int qie_debug_fp8_decode(float* out_dev);
+
 /* Tensor-parallel shard of the same synthetic tensor: dev[i][j] = element
  * (row0 + i) * full_cols + col0 + j of the full tensor, rows x cols, row-major. */
 int qie_synthetic_fill_slice(void* dev, int64_t rows, int64_t cols, int64_t full_cols, int64_t row0,

@@ -20,6 +20,7 @@ QIE_EPI_STORE = 0
 QIE_EPI_RESIDUAL = 1
 QIE_EPI_SWIGLU = 2
 QIE_EPI_F32 = 3
+QIE_LINEAR_FP8 = 1
 QIE_COMM_ID_BYTES = 128
 
 
@@ -68,7 +69,7 @@ class KvCacheC(C.Structure):
 class EngineOptsC(C.Structure):
     _fields_ = [("device", C.c_int32), ("max_ctx", C.c_int32), ("use_graph", C.c_int32),
                 ("tp_rank", C.c_int32), ("tp_size", C.c_int32), ("tp_comm", C.c_void_p),
-                ("reserved", C.c_int32 * 8)]
+                ("weight_fp8", C.c_int32), ("reserved", C.c_int32 * 7)]
 
 
 # (name, restype, argtypes) — every symbol the public headers declare.
@@ -113,6 +114,10 @@ SIGNATURES = [
     ("qie_synthetic_fill", C.c_int, [_P, _I64, _U32, _U64, _F, _F, _P]),
     ("qie_synthetic_fill_host", C.c_int, [_P, _I64, _U32, _U64, _F, _F]),
     ("qie_synthetic_fill_slice", C.c_int, [_P, _I64, _I64, _I64, _I64, _I64, _U32, _U64, _F, _F, _P]),
+    ("qie_fp8_weight_bytes", C.c_int64, [_I64, _I64]),
+    ("qie_quantize_fp8", C.c_int, [_P, _I64, _I64, _P, _P]),
+    ("qie_quantize_fp8_host", C.c_int, [_P, _I64, _I64, _P]),
+    ("qie_debug_fp8_decode", C.c_int, [_P]),
     # qie_engine.h
     ("qie_comm_unique_id", C.c_int, [_P]),
     ("qie_comm_create_rccl", C.c_int, [_P, _I32, _I32, _I32, C.POINTER(_P)]),

@@ -52,6 +52,8 @@ struct qie_engine {
     std::vector<qie_layer_weights> layers;
     qie_model_weights w{};
     bool have_weights = false;
+    bool fp8 = false;            // linear weights are e4m3 + row scales (fp8_arena)
+    void* fp8_arena = nullptr;
     float* rope_cos = nullptr;
     float* rope_sin = nullptr;
     int rope_rows = 0;
@@ -173,6 +175,45 @@ static int check_align(const void* p, const char* what, int layer) {
     return 0;
 }
 
+// fp8 weights (opts.weight_fp8): every linear weight and the lm_head are quantised on
+// device into a second arena (OCP e4m3 codes + power-of-two row scales, qie_ops.h) and
+// the layer pointers switched to it; embeddings, norms and biases stay bf16 in the
+// first arena (a tied embedding keeps its bf16 copy for the token gather).
+static int quantize_weights_fp8(qie_engine* e) {
+    QIE_REQUIRE(e->sh.tp == 1, "fp8 weights with tensor parallelism are not supported yet");
+    const qie_model_spec& s = e->spec;
+    const int64_t H = s.hidden, QD = (int64_t)s.n_heads * s.head_dim, KD = (int64_t)s.n_kv_heads * s.head_dim;
+    const int64_t I = s.ffn, V = s.vocab;
+    QIE_REQUIRE(H % 16 == 0 && QD % 16 == 0 && I % 16 == 0, "fp8 weights need hidden, q dim and ffn % 16 == 0");
+    struct Slot { const void** p; int64_t rows, cols; };
+    std::vector<Slot> ts;
+    for (auto& L : e->layers) {
+        ts.push_back({&L.wq, QD, H});
+        ts.push_back({&L.wk, KD, H});
+        ts.push_back({&L.wv, KD, H});
+        ts.push_back({&L.wo, H, QD});
+        ts.push_back({&L.w_gate, I, H});
+        ts.push_back({&L.w_up, I, H});
+        ts.push_back({&L.w_down, H, I});
+    }
+    ts.push_back({&e->w.lm_head, V, H});
+    size_t total = 0;
+    for (auto& t : ts) total += (size_t)((qie_fp8_weight_bytes(t.rows, t.cols) + 255) / 256 * 256);
+    if (e->fp8_arena) hipFree(e->fp8_arena);
+    e->fp8_arena = nullptr;
+    QIE_HIP(hipMalloc(&e->fp8_arena, total));
+    char* dst = (char*)e->fp8_arena;
+    for (auto& t : ts) {
+        QIE_TRY(qie_quantize_fp8(*t.p, t.rows, t.cols, dst, e->stream));
+        *t.p = dst;
+        dst += (qie_fp8_weight_bytes(t.rows, t.cols) + 255) / 256 * 256;
+    }
+    QIE_HIP(hipStreamSynchronize(e->stream));
+    e->w.layers = e->layers.data();
+    e->fp8 = true;
+    return 0;
+}
+
 // Resolve role pointers from the reference index (short_name, layer) ->
 // arena + data_offsets[0]  (assign_weight_pointer, helpers.cuh:19-30).
 static int bind_from_index(qie_engine* e) {
@@ -213,13 +254,15 @@ static int bind_from_index(qie_engine* e) {
     e->w.n_layers = s.n_layers;
     e->w.layers = e->layers.data();
     e->have_weights = true;
-    return 0;
+    return e->opts.weight_fp8 ? quantize_weights_fp8(e) : 0;
 }
 
 // ------------------------------------------------------------- enqueue helpers
-static qie_linear_args lin_base() {
+// every weight linear of the engine: fp8 weights when the engine quantised them
+static qie_linear_args lin_base(const qie_engine* e) {
     qie_linear_args a;
     std::memset(&a, 0, sizeof(a));
+    a.flags = e->fp8 ? QIE_LINEAR_FP8 : 0;
     return a;
 }
 
@@ -249,7 +292,7 @@ static int enqueue_layer_decode(qie_batch* b, int l) {
     const int64_t QKVD = QD + 2 * KD, I = e->sh.ffn, B = b->B;
     qie_kv_cache cache{b->kc, b->vc, b->seq_stride, s.n_layers, e->sh.nkv, s.head_dim, b->max_ctx};
 
-    qie_linear_args a = lin_base();
+    qie_linear_args a = lin_base(e);
     a.x = b->x_res; a.ldx = H;
     a.w[0] = L.wq; a.w[1] = L.wk; a.w[2] = L.wv;
     a.bias[0] = L.bq; a.bias[1] = L.bk; a.bias[2] = L.bv;
@@ -263,14 +306,14 @@ static int enqueue_layer_decode(qie_batch* b, int l) {
     QIE_TRY(qie_attention_decode(b->qkv, B, b->d_pos, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, e->sh.nq,
                                  &cache, l, s.rms_eps, s.numerics, b->att, b->dec_ws, st));
 
-    a = lin_base();
+    a = lin_base(e);
     a.x = b->att; a.ldx = QD;
     a.w[0] = L.wo; a.seg_rows[0] = H;
     a.M = B; a.K = QD; a.N = H;
     a.ldy = H;
     QIE_TRY(row_parallel(b, a, b->x_res, b->part, B));
 
-    a = lin_base();
+    a = lin_base(e);
     a.x = b->x_res; a.ldx = H;
     a.w[0] = L.w_gate; a.w[1] = L.w_up; a.seg_rows[0] = I; a.seg_rows[1] = I;
     a.M = B; a.K = H; a.N = I;
@@ -279,7 +322,7 @@ static int enqueue_layer_decode(qie_batch* b, int l) {
     a.norm_w = L.ffn_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
     QIE_TRY(gemv(&a, st));
 
-    a = lin_base();
+    a = lin_base(e);
     a.x = b->h; a.ldx = I;
     a.w[0] = L.w_down; a.seg_rows[0] = H;
     a.M = B; a.K = I; a.N = H;
@@ -318,7 +361,7 @@ static int enqueue_head(qie_batch* b, const uint16_t* x, int64_t ldx, int m0, in
     const qie_model_spec& s = e->spec;
     hipStream_t st = e->stream;
     const int64_t Vl = e->sh.vocab;
-    qie_linear_args a = lin_base();
+    qie_linear_args a = lin_base(e);
     a.x = x; a.ldx = ldx;
     a.w[0] = e->w.lm_head; a.seg_rows[0] = Vl;
     a.M = M; a.K = s.hidden; a.N = Vl;
@@ -683,7 +726,7 @@ int qie_engine_set_weights(qie_engine* e, const qie_model_weights* w) {
     e->w = *w;
     e->w.layers = e->layers.data();
     e->have_weights = true;
-    return 0;
+    return e->opts.weight_fp8 ? quantize_weights_fp8(e) : 0;
 }
 
 int qie_engine_weights(const qie_engine* e, qie_model_weights* out, const qie_layer_weights** layers) {
@@ -711,6 +754,7 @@ void qie_engine_destroy(qie_engine* e) {
     if (!e) return;
     if (e->stream) hipStreamSynchronize(e->stream);
     if (e->arena) hipFree(e->arena);
+    if (e->fp8_arena) hipFree(e->fp8_arena);
     if (e->rope_cos) hipFree(e->rope_cos);
     if (e->rope_sin) hipFree(e->rope_sin);
     if (e->index) qie_index_destroy(e->index);
@@ -813,7 +857,7 @@ int qie_prefill(qie_batch* b, int32_t seq, const int32_t* ids, int32_t n, const 
     for (int l = 0; l < s.n_layers; l++) {
         const qie_layer_weights& L = e->layers[l];
         QIE_TRY(qie_rmsnorm(b->pf_x, L.attn_norm, b->pf_hn, n, H, s.rms_eps, s.numerics, st));
-        qie_linear_args a = lin_base();
+        qie_linear_args a = lin_base(e);
         a.x = b->pf_hn; a.ldx = H;
         a.w[0] = L.wq; a.w[1] = L.wk; a.w[2] = L.wv;
         a.bias[0] = L.bq; a.bias[1] = L.bk; a.bias[2] = L.bv;
@@ -823,16 +867,16 @@ int qie_prefill(qie_batch* b, int32_t seq, const int32_t* ids, int32_t n, const 
         QIE_TRY(qie_qkv_post(b->pf_qkv, n, b->pf_pos, n, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, sh.nq,
                              &cache, l, s.rms_eps, s.numerics, b->pf_q, st));
         QIE_TRY(qie_attention(b->pf_q, n, b->pf_pos, n, &cache, l, sh.nq, b->pf_att, b->pf_attn_ws, st));
-        a = lin_base();
+        a = lin_base(e);
         a.x = b->pf_att; a.ldx = QD; a.w[0] = L.wo; a.seg_rows[0] = H;
         a.M = n; a.K = QD; a.N = H; a.ldy = H;
         QIE_TRY(row_parallel(b, a, b->pf_x, b->pf_part, n));
         QIE_TRY(qie_rmsnorm(b->pf_x, L.ffn_norm, b->pf_hn, n, H, s.rms_eps, s.numerics, st));
-        a = lin_base();
+        a = lin_base(e);
         a.x = b->pf_hn; a.ldx = H; a.w[0] = L.w_gate; a.w[1] = L.w_up; a.seg_rows[0] = I; a.seg_rows[1] = I;
         a.M = n; a.K = H; a.N = I; a.y = b->pf_h; a.ldy = I; a.epilogue = QIE_EPI_SWIGLU;
         QIE_TRY(qie_linear(&a, st));
-        a = lin_base();
+        a = lin_base(e);
         a.x = b->pf_h; a.ldx = I; a.w[0] = L.w_down; a.seg_rows[0] = H;
         a.M = n; a.K = I; a.N = H; a.ldy = H;
         QIE_TRY(row_parallel(b, a, b->pf_x, b->pf_part, n));
@@ -964,34 +1008,35 @@ int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* av
     uint16_t* scratch = nullptr;
     QIE_TRY(dmalloc((void**)&scratch,
                     (size_t)B * std::max<int64_t>(std::max(I, V), QD + 2 * KD) * 2 + B * 8 + 64));
-    qie_linear_args a = lin_base();
+    qie_linear_args a = lin_base(e);
     double by = 0;
+    const double wb = e->fp8 ? 1.0 : 2.0;   // weight bytes per element (fp8 row scales: negligible)
     if (which == 0) {
         a.x = b->x_res; a.ldx = H; a.w[0] = L.w_gate; a.w[1] = L.w_up; a.seg_rows[0] = I; a.seg_rows[1] = I;
         a.M = B; a.K = H; a.N = I; a.y = scratch; a.ldy = I; a.epilogue = QIE_EPI_SWIGLU;
         a.norm_w = L.ffn_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
-        by = 2.0 * I * H * 2 + B * H * 2 + H * 2 + B * I * 2;
+        by = 2.0 * I * H * wb + B * H * 2 + H * 2 + B * I * 2;
     } else if (which == 1) {
         a.x = b->h; a.ldx = I; a.w[0] = L.w_down; a.seg_rows[0] = H;
         a.M = B; a.K = I; a.N = H; a.y = scratch; a.ldy = H; a.epilogue = QIE_EPI_STORE;
-        by = (double)H * I * 2 + B * I * 2 + B * H * 2;
+        by = (double)H * I * wb + B * I * 2 + B * H * 2;
     } else if (which == 2) {
         a.x = b->x_res; a.ldx = H; a.w[0] = L.wq; a.w[1] = L.wk; a.w[2] = L.wv;
         a.bias[0] = L.bq; a.bias[1] = L.bk; a.bias[2] = L.bv;
         a.seg_rows[0] = QD; a.seg_rows[1] = KD; a.seg_rows[2] = KD;
         a.M = B; a.K = H; a.N = QD + 2 * KD; a.y = scratch; a.ldy = QD + 2 * KD; a.epilogue = QIE_EPI_STORE;
         a.norm_w = L.attn_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
-        by = (double)(QD + 2 * KD) * H * 2 + B * H * 2 + B * (QD + 2 * KD) * 2;
+        by = (double)(QD + 2 * KD) * H * wb + B * H * 2 + B * (QD + 2 * KD) * 2;
     } else if (which == 3) {
         a.x = b->att; a.ldx = QD; a.w[0] = L.wo; a.seg_rows[0] = H;
         a.M = B; a.K = QD; a.N = H; a.y = scratch; a.ldy = H; a.epilogue = QIE_EPI_STORE;
-        by = (double)H * QD * 2 + B * QD * 2 + B * H * 2;
+        by = (double)H * QD * wb + B * QD * 2 + B * H * 2;
     } else if (which == 4) {
         a.x = b->x_res; a.ldx = H; a.w[0] = e->w.lm_head; a.seg_rows[0] = V;
         a.M = B; a.K = H; a.N = V; a.y = scratch; a.ldy = V; a.epilogue = QIE_EPI_STORE;
         a.norm_w = e->w.final_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
         a.argmax_keys = (uint64_t*)(((uintptr_t)(scratch + B * V) + 7) & ~(uintptr_t)7);   // as the greedy step runs it
-        by = (double)V * H * 2 + B * H * 2 + B * (double)V * 2;
+        by = (double)V * H * wb + B * H * 2 + B * (double)V * 2;
     } else if (which != 5) {
         hipFree(scratch);
         return fail(-22, "qie_batch_time_kernel: unknown kernel %d", which);

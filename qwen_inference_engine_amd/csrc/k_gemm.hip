@@ -40,27 +40,46 @@ struct GemmParams {
 
 constexpr int BM = 128, BN = 128, BK = 64;
 
-// Weight row for tile column c of block tile starting at output column n0.
+// Weight row for tile column c of block tile starting at output column n0; eb = bytes
+// per weight; for fp8 (eb = 1) also the row's scale (stored after the segment's codes).
 template <int EPI>
-__device__ __forceinline__ const uint16_t* w_row(const GemmParams& p, int64_t nblk, int c,
-                                                 bool& valid) {
+__device__ __forceinline__ const uint16_t* w_row(const GemmParams& p, int64_t nblk, int c, bool& valid, int eb,
+                                                 int64_t& row, float& scale) {
+    auto at = [&](const uint16_t* w, int64_t rows, int64_t r) {
+        const uint8_t* b = reinterpret_cast<const uint8_t*>(w);
+        scale = eb == 1 ? reinterpret_cast<const float*>(b + rows * p.K)[r] : 1.f;
+        row = r;
+        return reinterpret_cast<const uint16_t*>(b + r * p.K * eb);
+    };
     if constexpr (EPI == QIE_EPI_SWIGLU) {
         // 64 output columns per tile: cols [64wc, 64wc+32) gate, [64wc+32, 64wc+64) up.
         const int64_t j = nblk * 64 + 32 * (c >> 6) + (c & 31);
         valid = j < p.N;
         const int64_t jj = valid ? j : p.N - 1;
-        return ((c >> 5) & 1) ? p.w1 + jj * p.K : p.w0 + jj * p.K;
+        return ((c >> 5) & 1) ? at(p.w1, p.N, jj) : at(p.w0, p.N, jj);
     } else {
         const int64_t r = nblk * BN + c;
         valid = r < p.N;
         const int64_t rr = valid ? r : p.N - 1;
-        if (rr < p.n0) return p.w0 + rr * p.K;
-        if (rr < p.n01) return p.w1 + (rr - p.n0) * p.K;
-        return p.w2 + (rr - p.n01) * p.K;
+        if (rr < p.n0) return at(p.w0, p.n0, rr);
+        if (rr < p.n01) return at(p.w1, p.n01 - p.n0, rr - p.n0);
+        return at(p.w2, p.N - p.n01, rr - p.n01);
     }
 }
 
-template <int EPI>
+// fp8 weights (WT = 1, QIE_LINEAR_FP8): e4m3 codes + power-of-two row scales after the
+// [rows, K] code block; a B chunk (8 weights) is one 8-byte load, decoded and scaled to
+// bf16 (exact: 3 mantissa bits x 2^k) before the LDS store, so the MFMA path is the
+// bf16 one at half the weight bytes.
+__device__ __forceinline__ uint4 fp8x8_to_bf16(uint2 q, float sc) {
+    float f[8];
+    fp8x4_to_f32(q.x, f);
+    fp8x4_to_f32(q.y, f + 4);
+    return make_uint4(pack2(f[0] * sc, f[1] * sc), pack2(f[2] * sc, f[3] * sc), pack2(f[4] * sc, f[5] * sc),
+                      pack2(f[6] * sc, f[7] * sc));
+}
+
+template <int EPI, int WT>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
 #pragma clang fp contract(off)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -74,8 +93,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
 
     // Per-thread staging coordinates: 4 chunks (16 B) of A and of B per K-tile.
     const uint16_t* a_src[4];
-    const uint16_t* b_src[4];
+    const uint8_t* b_src[4];   // byte address of the row's chunk (bf16: 2 B / weight, fp8: 1)
+    float b_sc[4];             // fp8 row scale
     int lds_off[4];
+    constexpr int EB = WT ? 1 : 2;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const int c = tid + 256 * i;       // chunk id 0..1023
@@ -84,20 +105,33 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
         if (ar >= p.M) ar = p.M - 1;
         a_src[i] = p.A + ar * p.lda + ch * 8;
         bool v;
-        b_src[i] = w_row<EPI>(p, nblk, row, v) + ch * 8;
+        int64_t wr_row;
+        const uint16_t* wbase = w_row<EPI>(p, nblk, row, v, EB, wr_row, b_sc[i]);
+        b_src[i] = reinterpret_cast<const uint8_t*>(wbase) + ch * 8 * EB;
         lds_off[i] = row * BK + ((ch ^ (row & 7)) * 8);
     }
 
     const int nk = (int)((p.K + BK - 1) / BK);
     uint4 ra[4], rb[4];
+    uint2 rq[4];
+    // Unconditional loads at clamped addresses (chunks past K are re-reads of the last
+    // chunk, zeroed by a select): a load under a condition is branched around and the
+    // waitcnt pass then waits for everything at the join.
     auto gload = [&](int kt) {
         const int64_t kbase = (int64_t)kt * BK;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const int ch = (tid + 256 * i) & 7;
             const bool ok = kbase + ch * 8 < p.K;
-            ra[i] = ok ? *reinterpret_cast<const uint4*>(a_src[i] + kbase) : make_uint4(0, 0, 0, 0);
-            rb[i] = ok ? *reinterpret_cast<const uint4*>(b_src[i] + kbase) : make_uint4(0, 0, 0, 0);
+            const int64_t kb = ok ? kbase : p.K - 8 - ch * 8;
+            ra[i] = *reinterpret_cast<const uint4*>(a_src[i] + kb);
+            if constexpr (WT == 0) rb[i] = *reinterpret_cast<const uint4*>(b_src[i] + kb * 2);
+            else rq[i] = *reinterpret_cast<const uint2*>(b_src[i] + kb);
+            if (!ok) {
+                ra[i] = make_uint4(0, 0, 0, 0);
+                if constexpr (WT == 0) rb[i] = make_uint4(0, 0, 0, 0);
+                else rq[i] = make_uint2(0, 0);
+            }
         }
     };
     auto lstore = [&](int buf) {
@@ -106,7 +140,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             *reinterpret_cast<uint4*>(a + lds_off[i]) = ra[i];
-            *reinterpret_cast<uint4*>(b + lds_off[i]) = rb[i];
+            if constexpr (WT == 0) *reinterpret_cast<uint4*>(b + lds_off[i]) = rb[i];
+            else *reinterpret_cast<uint4*>(b + lds_off[i]) = fp8x8_to_bf16(rq[i], b_sc[i]);
         }
     };
 
@@ -201,6 +236,22 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
     }
 }
 
+template <int WT>
+static int launch_gemm(int epi, unsigned gm, const GemmParams& p, size_t shm, hipStream_t st) {
+    if (epi == QIE_EPI_SWIGLU) {
+        hipLaunchKernelGGL((gemm_kernel<QIE_EPI_SWIGLU, WT>), dim3(gm, (unsigned)cdiv(p.N, 64)), dim3(256), shm, st, p);
+    } else if (epi == QIE_EPI_RESIDUAL) {
+        hipLaunchKernelGGL((gemm_kernel<QIE_EPI_RESIDUAL, WT>), dim3(gm, (unsigned)cdiv(p.N, BN)), dim3(256), shm, st,
+                           p);
+    } else if (epi == QIE_EPI_F32) {
+        hipLaunchKernelGGL((gemm_kernel<QIE_EPI_F32, WT>), dim3(gm, (unsigned)cdiv(p.N, BN)), dim3(256), shm, st, p);
+    } else {
+        hipLaunchKernelGGL((gemm_kernel<QIE_EPI_STORE, WT>), dim3(gm, (unsigned)cdiv(p.N, BN)), dim3(256), shm, st, p);
+    }
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+
 int gemm(const qie_linear_args* a, hipStream_t st) {
     QIE_REQUIRE(a->norm_w == nullptr, "qie_linear: fused RMSNorm is GEMV-only (M <= 8)");
     QIE_REQUIRE(a->argmax_keys == nullptr, "qie_linear: fused arg-max is GEMV-only (M <= 8)");
@@ -223,21 +274,9 @@ int gemm(const qie_linear_args* a, hipStream_t st) {
     p.ldc = a->ldy;
     const size_t shm = (size_t)2 * (BM + BN) * BK * 2;
     const unsigned gm = (unsigned)cdiv(a->M, BM);
-    if (a->epilogue == QIE_EPI_SWIGLU) {
-        hipLaunchKernelGGL(gemm_kernel<QIE_EPI_SWIGLU>, dim3(gm, (unsigned)cdiv(a->N, 64)), dim3(256),
-                           shm, st, p);
-    } else if (a->epilogue == QIE_EPI_RESIDUAL) {
-        hipLaunchKernelGGL(gemm_kernel<QIE_EPI_RESIDUAL>, dim3(gm, (unsigned)cdiv(a->N, BN)), dim3(256),
-                           shm, st, p);
-    } else if (a->epilogue == QIE_EPI_F32) {
-        hipLaunchKernelGGL(gemm_kernel<QIE_EPI_F32>, dim3(gm, (unsigned)cdiv(a->N, BN)), dim3(256),
-                           shm, st, p);
-    } else {
-        hipLaunchKernelGGL(gemm_kernel<QIE_EPI_STORE>, dim3(gm, (unsigned)cdiv(a->N, BN)), dim3(256),
-                           shm, st, p);
-    }
-    QIE_LAUNCH_CHECK();
-    return 0;
+    QIE_REQUIRE(a->K % 8 == 0, "qie_linear: GEMM needs K %% 8 == 0");
+    if (a->flags & QIE_LINEAR_FP8) return launch_gemm<1>(a->epilogue, gm, p, shm, st);
+    return launch_gemm<0>(a->epilogue, gm, p, shm, st);
 }
 
 }  // namespace qie

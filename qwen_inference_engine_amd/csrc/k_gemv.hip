@@ -64,36 +64,62 @@ __device__ __forceinline__ void unpack8(u32x4 v, float* f) {
     f[6] = bf_lo(v.w); f[7] = bf_hi(v.w);
 }
 
-template <int MT, int RPW, int EPI, int U, int XCH>
+// fp8 weights (WT = 1): 16 codes per 16-byte lane load (1024 weights per wave-load),
+// decoded with v_cvt_pk_f32_fp8; the power-of-two row scale multiplies the fp32 sum
+// once in the epilogue (exact: the same value as summing the dequantised products).
+__device__ __forceinline__ const float* fp8_scales(const uint16_t* w, int64_t rows, int64_t K) {
+    return reinterpret_cast<const float*>(reinterpret_cast<const uint8_t*>(w) + rows * K);
+}
+
+template <int MT, int RPW, int EPI, int U, int XCH, int WT>
 __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint16_t* xs = reinterpret_cast<uint16_t*>(smem);
     float* red = reinterpret_cast<float*>(smem + (p.xlds ? (size_t)MT * p.K * 2 : 0));
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t K = p.K;
+    constexpr int EB = WT ? 1 : 2;     // bytes per weight
+    constexpr int EL = 16 / EB;        // weights per 16-byte lane load
+    constexpr int WS = 64 * EL;        // weights per wave-load
 
     // ---------------- task -> weight rows / output columns
     auto task_ptrs = [&](int64_t task, const u32x4* (&wr)[RPW]) {
+        const uint8_t* w0 = reinterpret_cast<const uint8_t*>(p.w0);
+        const uint8_t* w1 = reinterpret_cast<const uint8_t*>(p.w1);
+        const uint8_t* w2 = reinterpret_cast<const uint8_t*>(p.w2);
         if constexpr (EPI == QIE_EPI_SWIGLU) {
             constexpr int P2 = RPW / 2;
 #pragma unroll
             for (int i = 0; i < P2; i++) {
                 int64_t j = task * P2 + i;
                 if (j >= p.N) j = p.N - 1;
-                wr[i] = reinterpret_cast<const u32x4*>(p.w0 + j * K);
-                wr[P2 + i] = reinterpret_cast<const u32x4*>(p.w1 + j * K);
+                wr[i] = reinterpret_cast<const u32x4*>(w0 + j * K * EB);
+                wr[P2 + i] = reinterpret_cast<const u32x4*>(w1 + j * K * EB);
             }
         } else {
 #pragma unroll
             for (int i = 0; i < RPW; i++) {
                 int64_t r = task * RPW + i;
                 if (r >= p.N) r = p.N - 1;
-                const uint16_t* base;
-                if (r < p.n0) base = p.w0 + r * K;
-                else if (r < p.n01) base = p.w1 + (r - p.n0) * K;
-                else base = p.w2 + (r - p.n01) * K;
+                const uint8_t* base;
+                if (r < p.n0) base = w0 + r * K * EB;
+                else if (r < p.n01) base = w1 + (r - p.n0) * K * EB;
+                else base = w2 + (r - p.n01) * K * EB;
                 wr[i] = reinterpret_cast<const u32x4*>(base);
             }
+        }
+    };
+    // fp8: the row scale of output column c (segment-resolved like task_ptrs)
+    auto row_scale = [&](int64_t c, int i) -> float {
+        if constexpr (WT == 0) {
+            return 1.f;
+        } else if constexpr (EPI == QIE_EPI_SWIGLU) {
+            constexpr int P2 = RPW / 2;
+            return i < P2 ? fp8_scales(p.w0, p.N, K)[c] : fp8_scales(p.w1, p.N, K)[c];
+        } else {
+            if (c < p.n0) return fp8_scales(p.w0, p.n0, K)[c];
+            if (c < p.n01) return fp8_scales(p.w1, p.n01 - p.n0, K)[c - p.n0];
+            return fp8_scales(p.w2, p.N - p.n01, K)[c - p.n01];
         }
     };
     auto task_cols = [&](int64_t task, int64_t (&col)[RPW]) {
@@ -112,26 +138,51 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
     auto load_chunk = [&](const u32x4* const (&wr)[RPW], int64_t k0, u32x4 (&wv)[U][RPW]) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const int64_t k = k0 + u * 512;
+            const int64_t k = k0 + u * WS;
 #pragma unroll
             for (int i = 0; i < RPW; i++)   // unconditional (clamped) loads: see below
-                wv[u][i] = __builtin_nontemporal_load(wr[i] + ((k < K ? k : K - 8) >> 3));
+                wv[u][i] = __builtin_nontemporal_load(wr[i] + ((k < K ? k : K - EL) / EL));
         }
+    };
+    auto x_at = [&](int m, int64_t k) -> uint4 {
+        return p.xlds ? *reinterpret_cast<const uint4*>(xs + (int64_t)m * K + k)
+                      : (m < p.M ? *reinterpret_cast<const uint4*>(p.x + (int64_t)m * p.ldx + k)
+                                 : make_uint4(0, 0, 0, 0));
     };
     auto compute_chunk = [&](int64_t k0, const u32x4 (&wv)[U][RPW], float (&acc)[MT][RPW]) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const int64_t k = k0 + u * 512;
+            const int64_t k = k0 + u * WS;
             if (k < K) {
+                if constexpr (WT == 0) {
 #pragma unroll
-                for (int m = 0; m < MT; m++) {
-                    uint4 xv = p.xlds ? *reinterpret_cast<const uint4*>(xs + (int64_t)m * K + k)
-                                      : (m < p.M ? *reinterpret_cast<const uint4*>(p.x + (int64_t)m * p.ldx + k)
-                                                 : make_uint4(0, 0, 0, 0));
-                    float xf[8];
-                    unpack8(u32x4{xv.x, xv.y, xv.z, xv.w}, xf);
+                    for (int m = 0; m < MT; m++) {
+                        const uint4 xv = x_at(m, k);
+                        float xf[8];
+                        unpack8(u32x4{xv.x, xv.y, xv.z, xv.w}, xf);
 #pragma unroll
-                    for (int i = 0; i < RPW; i++) fma8(acc[m][i], xf, wv[u][i]);
+                        for (int i = 0; i < RPW; i++) fma8(acc[m][i], xf, wv[u][i]);
+                    }
+                } else {
+                    float wf[RPW][16];
+#pragma unroll
+                    for (int i = 0; i < RPW; i++) {
+                        fp8x4_to_f32(wv[u][i].x, wf[i]);
+                        fp8x4_to_f32(wv[u][i].y, wf[i] + 4);
+                        fp8x4_to_f32(wv[u][i].z, wf[i] + 8);
+                        fp8x4_to_f32(wv[u][i].w, wf[i] + 12);
+                    }
+#pragma unroll
+                    for (int m = 0; m < MT; m++) {
+                        const uint4 x0 = x_at(m, k), x1 = x_at(m, k + 8);
+                        float xf[16];
+                        unpack8(u32x4{x0.x, x0.y, x0.z, x0.w}, xf);
+                        unpack8(u32x4{x1.x, x1.y, x1.z, x1.w}, xf + 8);
+#pragma unroll
+                        for (int i = 0; i < RPW; i++)
+#pragma unroll
+                            for (int j = 0; j < 16; j++) acc[m][i] = fmaf(xf[j], wf[i][j], acc[m][i]);
+                    }
                 }
             }
         }
@@ -163,7 +214,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
         // unconditional (a wave without a task re-reads the last row): a load under a
         // branch makes the vmcnt bookkeeping at the join wait for everything
         task_ptrs(task0 < p.n_tasks ? task0 : p.n_tasks - 1, wr);
-        load_chunk(wr, (int64_t)lane * 8, wv);
+        load_chunk(wr, (int64_t)lane * EL, wv);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int c = 0; c < XCH; c++) {   // opaque: x math cannot be hoisted above the weight issue
@@ -294,26 +345,36 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
         task_cols(task, col);
         if constexpr (!PF) {
             task_ptrs(task, wr);
-            load_chunk(wr, (int64_t)lane * 8, wv);
+            load_chunk(wr, (int64_t)lane * EL, wv);
         }
         float acc[MT][RPW];
 #pragma unroll
         for (int m = 0; m < MT; m++)
 #pragma unroll
             for (int i = 0; i < RPW; i++) acc[m][i] = 0.f;
-        compute_chunk((int64_t)lane * 8, wv, acc);
-        for (int64_t k0 = (int64_t)lane * 8 + 512 * U; k0 < K; k0 += 512 * U) {
+        compute_chunk((int64_t)lane * EL, wv, acc);
+        for (int64_t k0 = (int64_t)lane * EL + WS * U; k0 < K; k0 += WS * U) {
             load_chunk(wr, k0, wv);
             compute_chunk(k0, wv, acc);
         }
         if (PF && task + tstride < p.n_tasks) {
             task_ptrs(task + tstride, wr);
-            load_chunk(wr, (int64_t)lane * 8, wv);
+            load_chunk(wr, (int64_t)lane * EL, wv);
         }
 #pragma unroll
         for (int m = 0; m < MT; m++)
 #pragma unroll
             for (int i = 0; i < RPW; i++) acc[m][i] = wave_sum(acc[m][i]);
+        if constexpr (WT != 0) {   // fp8: the power-of-two row scale, once per output
+            if (lane == 0) {
+#pragma unroll
+                for (int i = 0; i < RPW; i++) {
+                    const float sc = row_scale(col[i] < p.N ? col[i] : p.N - 1, i);
+#pragma unroll
+                    for (int m = 0; m < MT; m++) acc[m][i] *= sc;
+                }
+            }
+        }
 
         // ---------------- epilogue (lane 0 writes; outputs are tiny)
         if (lane == 0) {
@@ -385,10 +446,10 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
     }
 }
 
-template <int MT, int RPW, int EPI, int XCH>
+template <int MT, int RPW, int EPI, int XCH, int WT>
 static int launch_gemv_t(const GemvParams& p, hipStream_t st, int blocks_per_cu) {
     constexpr int U = (RPW >= 4) ? 4 : 8;
-    const void* fn = (const void*)gemv_kernel<MT, RPW, EPI, U, XCH>;
+    const void* fn = (const void*)gemv_kernel<MT, RPW, EPI, U, XCH, WT>;
     const size_t shm = (p.xlds ? (size_t)MT * p.K * 2 : 0) + 64;
     if (shm > 65536) {
         static bool raised = false;   // per instantiation
@@ -418,25 +479,25 @@ static int launch_gemv_t(const GemvParams& p, hipStream_t st, int blocks_per_cu)
         grid64 = std::max<int64_t>(1, (p.n_tasks + 4 * rounds - 1) / (4 * rounds));
     }
     const unsigned grid = (unsigned)grid64;
-    hipLaunchKernelGGL((gemv_kernel<MT, RPW, EPI, U, XCH>), dim3(grid), dim3(256), shm, st, p);
+    hipLaunchKernelGGL((gemv_kernel<MT, RPW, EPI, U, XCH, WT>), dim3(grid), dim3(256), shm, st, p);
     QIE_LAUNCH_CHECK();
     return 0;
 }
 
-template <int MT, int XCH>
+template <int MT, int XCH, int WT = 0>
 static int launch_gemv_m(const GemvParams& p, int rpw, int epi, hipStream_t st, int bpc) {
     if (epi == QIE_EPI_SWIGLU) {
-        return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_SWIGLU, XCH>(p, st, bpc)
-                        : launch_gemv_t<MT, 2, QIE_EPI_SWIGLU, XCH>(p, st, bpc);
+        return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_SWIGLU, XCH, WT>(p, st, bpc)
+                        : launch_gemv_t<MT, 2, QIE_EPI_SWIGLU, XCH, WT>(p, st, bpc);
     } else if (epi == QIE_EPI_RESIDUAL) {
-        return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_RESIDUAL, XCH>(p, st, bpc)
-                        : launch_gemv_t<MT, 2, QIE_EPI_RESIDUAL, XCH>(p, st, bpc);
+        return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_RESIDUAL, XCH, WT>(p, st, bpc)
+                        : launch_gemv_t<MT, 2, QIE_EPI_RESIDUAL, XCH, WT>(p, st, bpc);
     } else if (epi == QIE_EPI_F32) {
-        return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_F32, XCH>(p, st, bpc)
-                        : launch_gemv_t<MT, 2, QIE_EPI_F32, XCH>(p, st, bpc);
+        return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_F32, XCH, WT>(p, st, bpc)
+                        : launch_gemv_t<MT, 2, QIE_EPI_F32, XCH, WT>(p, st, bpc);
     }
-    return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_STORE, XCH>(p, st, bpc)
-                    : launch_gemv_t<MT, 2, QIE_EPI_STORE, XCH>(p, st, bpc);
+    return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_STORE, XCH, WT>(p, st, bpc)
+                    : launch_gemv_t<MT, 2, QIE_EPI_STORE, XCH, WT>(p, st, bpc);
 }
 // x-first prologue variants (MT = 1 only): XCH 2048-element x chunks per thread
 static int launch_gemv_1(const GemvParams& p, int rpw, int epi, hipStream_t st, int bpc, int xch) {
@@ -495,6 +556,15 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
     // x-first prologue + cross-task weight prefetch (QIE_GEMV_XFIRST, MT = 1).  A first
     // attempt that issued the weights BEFORE x was slower everywhere (qkv 11.4 vs 9.4 us):
     // x then queued behind the weights in the in-order vmcnt.
+    if (a->flags & QIE_LINEAR_FP8) {
+        QIE_REQUIRE(a->K % 16 == 0, "qie_linear: fp8 weights need K %% 16 == 0 (K=%lld)", (long long)a->K);
+        switch (MT) {
+            case 1: return launch_gemv_m<1, 0, 1>(p, rpw, a->epilogue, st, bpc);
+            case 2: return launch_gemv_m<2, 0, 1>(p, rpw, a->epilogue, st, bpc);
+            case 4: return launch_gemv_m<4, 0, 1>(p, rpw, a->epilogue, st, bpc);
+            default: return launch_gemv_m<8, 0, 1>(p, rpw, a->epilogue, st, bpc);
+        }
+    }
     int xch = 0;
     if (MT == 1 && p.xlds && p.M == 1 && env_int("QIE_GEMV_XFIRST", 1) != 0)
         xch = K_fits(a->K, 2) ? 2 : (K_fits(a->K, 10) ? 10 : 0);

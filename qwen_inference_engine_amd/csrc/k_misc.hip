@@ -297,6 +297,31 @@ __global__ __launch_bounds__(256) void synth_kernel(uint32_t* __restrict__ out, 
     }
 }
 
+// ------------------------------------------------------ fp8 weight quantisation
+// One block per weight row: amax -> power-of-two scale -> e4m3 codes (qie_common.hpp).
+__global__ __launch_bounds__(256) void quantize_fp8_kernel(const uint16_t* __restrict__ w, int64_t cols,
+                                                           uint8_t* __restrict__ codes, float* __restrict__ scales) {
+    __shared__ float red[4];
+    const int64_t r = blockIdx.x;
+    const uint16_t* row = w + r * cols;
+    float amax = 0.f;
+    for (int64_t c = threadIdx.x; c < cols; c += 256) amax = fmaxf(amax, fabsf(bf2f(row[c])));
+    amax = wave_max(amax);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
+    __syncthreads();
+    amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    const float s = e4m3_row_scale(amax);
+    for (int64_t c = threadIdx.x; c < cols; c += 256) codes[r * cols + c] = e4m3_encode(bf2f(row[c]) / s);
+    if (threadIdx.x == 0) scales[r] = s;
+}
+
+__global__ void fp8_decode_probe_kernel(float* out) {
+    const uint32_t b = threadIdx.x;   // 64 threads x 4 codes
+    float f[4];
+    fp8x4_to_f32((4 * b) | ((4 * b + 1) << 8) | ((4 * b + 2) << 16) | ((4 * b + 3) << 24), f);
+    for (int j = 0; j < 4; j++) out[4 * b + j] = f[j];
+}
+
 __global__ __launch_bounds__(256) void synth_slice_kernel(uint16_t* __restrict__ out, int64_t rows, int64_t cols,
                                                           int64_t full_cols, int64_t row0, int64_t col0,
                                                           uint64_t base, float scale, float offset) {
@@ -483,6 +508,48 @@ int qie_residual_add_f32(void* x, const float* sum, int64_t n, void* stream) {
     hipLaunchKernelGGL(resadd_f32_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (uint4*)x,
                        (const float4*)sum, n8);
     QIE_LAUNCH_CHECK();
+    return 0;
+}
+
+int64_t qie_fp8_weight_bytes(int64_t rows, int64_t cols) { return rows * cols + rows * 4; }
+
+int qie_quantize_fp8(const void* w_bf16, int64_t rows, int64_t cols, void* out, void* stream) {
+    QIE_REQUIRE(w_bf16 && out && rows > 0 && cols > 0 && cols % 16 == 0 && ((uintptr_t)out % 16) == 0,
+                "qie_quantize_fp8: bad arguments (cols must be a multiple of 16, out 16-B aligned)");
+    uint8_t* codes = (uint8_t*)out;
+    hipLaunchKernelGGL(quantize_fp8_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream,
+                       (const uint16_t*)w_bf16, cols, codes, (float*)(codes + rows * cols));
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+
+int qie_quantize_fp8_host(const void* w_bf16, int64_t rows, int64_t cols, void* out) {
+    QIE_REQUIRE(w_bf16 && out && rows > 0 && cols > 0 && cols % 16 == 0, "qie_quantize_fp8_host: bad arguments");
+    const uint16_t* w = (const uint16_t*)w_bf16;
+    uint8_t* codes = (uint8_t*)out;
+    float* scales = (float*)(codes + rows * cols);
+    auto h2f = [](uint16_t h) {
+        uint32_t u = (uint32_t)h << 16;
+        float f;
+        std::memcpy(&f, &u, 4);
+        return f;
+    };
+#pragma omp parallel for schedule(static)
+    for (int64_t r = 0; r < rows; r++) {
+        float amax = 0.f;
+        for (int64_t c = 0; c < cols; c++) amax = std::max(amax, std::fabs(h2f(w[r * cols + c])));
+        const float s = e4m3_row_scale(amax);
+        for (int64_t c = 0; c < cols; c++) codes[r * cols + c] = e4m3_encode(h2f(w[r * cols + c]) / s);
+        scales[r] = s;
+    }
+    return 0;
+}
+
+int qie_debug_fp8_decode(float* out_dev) {
+    QIE_REQUIRE(out_dev, "qie_debug_fp8_decode: null output");
+    hipLaunchKernelGGL(fp8_decode_probe_kernel, dim3(1), dim3(64), 0, (hipStream_t)0, out_dev);
+    QIE_LAUNCH_CHECK();
+    QIE_HIP(hipDeviceSynchronize());
     return 0;
 }
 

@@ -53,6 +53,55 @@ __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
     return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
 }
 
+// ------------------------------------------------------ fp8 (OCP e4m3fn) weights
+// A quantised weight row = e4m3 codes times a power-of-two row scale, so every
+// dequantised value (3 mantissa bits x 2^k) is exactly a bf16: the fp8 engine computes
+// the same products as a bf16 model whose weights are those dequantised values
+// (tests/oracle run exactly that).  Encode: round to nearest even, saturate at 448.
+__host__ __device__ inline uint8_t e4m3_encode(float v) {
+    const uint32_t sign = v < 0.f ? 0x80u : 0u;
+    float a = fabsf(v);
+    if (!(a > 0.f)) return (uint8_t)sign;                 // +-0 (NaN never produced upstream)
+    if (a >= 448.f) return (uint8_t)(sign | 0x7Eu);       // saturate (max finite 1.75 * 2^8)
+    if (a < 0.015625f) {                                  // subnormal range: step 2^-9
+        const uint32_t m = (uint32_t)rintf(a * 512.f);    // 0..8; 8 == 2^-6, code 0x08 (normal)
+        return (uint8_t)(sign | m);
+    }
+    int e;
+    const float f = frexpf(a, &e);                        // a = f * 2^e, f in [0.5, 1)
+    int E = e - 1;                                        // a = (2 f) * 2^E, 2f in [1, 2)
+    uint32_t m3 = (uint32_t)rintf((2.f * f - 1.f) * 8.f); // 0..8
+    if (m3 == 8) { m3 = 0; E += 1; }
+    uint32_t code = ((uint32_t)(E + 7) << 3) | m3;
+    if (code > 0x7Eu) code = 0x7Eu;
+    return (uint8_t)(sign | code);
+}
+__host__ __device__ inline float e4m3_decode(uint8_t b) {
+    const int ex = (b >> 3) & 0xF, man = b & 7;
+    const float v = ex == 0 ? (float)man * 0.001953125f : ldexpf(1.f + (float)man * 0.125f, ex - 7);
+    return (b & 0x80) ? -v : v;
+}
+// power-of-two row scale: the smallest 2^k with amax / 2^k <= 448
+__host__ __device__ inline float e4m3_row_scale(float amax) {
+    if (!(amax > 0.f)) return 1.f;
+    int e;
+    frexpf(amax / 448.f, &e);                             // amax / 448 = f * 2^e, f in [0.5, 1)
+    float s = ldexpf(1.f, e);                             // s >= amax / 448
+    if (ldexpf(1.f, e - 1) * 448.f >= amax) s = ldexpf(1.f, e - 1);
+    if (s * 448.f < amax) s *= 2.f;                       // exact checks: the division rounded
+    return s;
+}
+// 4 packed codes -> 4 floats (v_cvt_pk_f32_fp8; gfx950 "fp8" is OCP e4m3fn — checked
+// against e4m3_decode for all 256 codes by tests/test_gpu_fp8.py)
+__device__ __forceinline__ void fp8x4_to_f32(uint32_t w, float* f) {
+    const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8((int)w, false);
+    const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8((int)w, true);
+    f[0] = lo[0];
+    f[1] = lo[1];
+    f[2] = hi[0];
+    f[3] = hi[1];
+}
+
 // ------------------------------------------------------ cross-lane reductions
 // __shfl_xor lowers to ds_bpermute_b32 (an LDS round trip, ~100 cycles); chains of
 // them serialised the decode attention.  These use DPP row ops (folded into the

@@ -106,7 +106,7 @@ class Comm:
 
 class Engine:
     def __init__(self, spec: ModelSpec, device: int = 0, max_ctx: int = 4096, use_graph: bool = True,
-                 comm: Optional[Comm] = None):
+                 comm: Optional[Comm] = None, weight_fp8: bool = False):
         self.lib = _lib.load()
         self.spec = spec
         self._spec_c = spec.to_c()
@@ -114,6 +114,7 @@ class Engine:
         opts.device, opts.max_ctx, opts.use_graph = device, max_ctx, int(use_graph)
         opts.tp_rank, opts.tp_size = (comm.rank, comm.world) if comm else (0, 1)
         opts.tp_comm = comm.h if comm else None
+        opts.weight_fp8 = int(weight_fp8)
         self.comm = comm
         h = C.c_void_p()
         _lib.check(self.lib.qie_engine_create(C.byref(self._spec_c), C.byref(opts), C.byref(h)),

@@ -76,9 +76,16 @@ class ModelSpec:
             n += 2 * self.head_dim
         return 2 * n
 
-    def decode_weight_bytes(self) -> int:
-        """Weights streamed per decode step: every layer + final norm + lm_head once."""
-        return self.n_layers * self.layer_weight_bytes() + 2 * self.hidden + 2 * self.vocab * self.hidden
+    def decode_weight_bytes(self, fp8: bool = False) -> int:
+        """Weights streamed per decode step: every layer + final norm + lm_head once.
+        fp8: linear weights and lm_head at 1 byte per weight + one fp32 scale per row."""
+        if not fp8:
+            return self.n_layers * self.layer_weight_bytes() + 2 * self.hidden + 2 * self.vocab * self.hidden
+        lin = self.linear_params_per_layer()
+        rows = self.q_dim + 2 * self.kv_dim + self.hidden + 2 * self.ffn + self.hidden
+        other = self.layer_weight_bytes() - 2 * lin            # norms, biases (bf16)
+        per_layer = lin + 4 * rows + other
+        return self.n_layers * per_layer + 2 * self.hidden + (self.vocab * self.hidden + 4 * self.vocab)
 
     def kv_bytes_per_position(self) -> int:
         return self.n_layers * 2 * self.kv_dim * 2

@@ -162,6 +162,35 @@ def synthetic_index(spec: ModelSpec) -> List[Tensor]:
     return parsed_tensors([hdr])
 
 
+# ------------------------------------------------------------------ fp8 weights
+def e4m3_table() -> np.ndarray:
+    """float32 value of every OCP e4m3fn code (0x7F / 0xFF are NaN)."""
+    c = np.arange(256)
+    ex, man = (c >> 3) & 0xF, c & 7
+    v = np.where(ex == 0, man * 2.0 ** -9, (1 + man / 8.0) * 2.0 ** (ex - 7.0))
+    v = np.where((c & 0x7F) == 0x7F, np.nan, v)
+    return np.where(c & 0x80, -v, v).astype(np.float32)
+
+
+def quantize_fp8(w: np.ndarray):
+    """bf16 [rows, cols] -> (e4m3 codes uint8 [rows, cols], fp32 power-of-two row scales),
+    libqie's host quantiser (bit-identical to the device one, qie_quantize_fp8)."""
+    w = np.ascontiguousarray(w, np.uint16)
+    rows, cols = w.shape
+    lib = _lib.load()
+    out = np.empty(int(lib.qie_fp8_weight_bytes(rows, cols)), np.uint8)
+    _lib.check(lib.qie_quantize_fp8_host(w.ctypes.data, rows, cols, out.ctypes.data), "qie_quantize_fp8_host")
+    return out[:rows * cols].reshape(rows, cols), out[rows * cols:].view(np.float32).copy()
+
+
+def dequantize_fp8(codes: np.ndarray, scales: np.ndarray) -> np.ndarray:
+    """codes x row scale as bf16 bits (exact: 3 mantissa bits x 2^k)."""
+    v = e4m3_table()[codes] * scales[:, None].astype(np.float32)
+    b = v.view(np.uint32)
+    assert not (b & 0xFFFF).any(), "dequantised fp8 value not exactly representable in bf16"
+    return (b >> 16).astype(np.uint16)
+
+
 # ------------------------------------------------------------------ synthetic values
 @dataclasses.dataclass(frozen=True)
 class SynthParams:
@@ -233,6 +262,22 @@ class HostWeights:
         if self.spec.tie_embeddings:
             return self.tensors["model.embed_tokens.weight"]
         return self.tensors["lm_head.weight"]
+
+    def fp8_dequantized(self) -> "HostWeights":
+        """The model the fp8 engine computes (``qie_engine_opts.weight_fp8``): every linear
+        weight and the lm_head replaced by its e4m3 x power-of-two-scale dequantisation
+        (exactly representable in bf16).  A tied head gets its own (quantised) copy, so the
+        returned spec is untied; the token embedding stays bf16."""
+        t = dict(self.tensors)
+        spec = self.spec
+        for l in range(spec.n_layers):
+            for short in ("self_attn.q_proj.weight", "self_attn.k_proj.weight", "self_attn.v_proj.weight",
+                          "self_attn.o_proj.weight", "mlp.gate_proj.weight", "mlp.up_proj.weight",
+                          "mlp.down_proj.weight"):
+                name = f"model.layers.{l}.{short}"
+                t[name] = dequantize_fp8(*quantize_fp8(t[name]))
+        t["lm_head.weight"] = dequantize_fp8(*quantize_fp8(self.lm_head))
+        return HostWeights(spec.replace(tie_embeddings=False), t)
 
     def write_weights_bin(self, bin_path: str, meta_path: str) -> List[Tensor]:
         """Write the reference flat layout: tensors in parsed_tensors order, no gaps."""

@@ -1,0 +1,151 @@
+"""fp8 weights (BASELINE config "Qwen2-7B fp8 weights, batch 8"): OCP e4m3 codes with
+power-of-two row scales, so each dequantised weight is exactly a bf16 and the fp8 engine
+must compute what the oracle computes on the dequantised bf16 weights.
+
+Bar: the device decode of all 256 codes equals the e4m3fn table bit-exactly; device
+quantisation equals the host quantiser bit-exactly; fp8 GEMV / GEMM results meet the same
+tolerances as the bf16 linear tests against oracle.matmul on the dequantised weights;
+the fp8 engine's teacher-forced greedy run matches the oracle on the dequantised model
+under tests/test_gpu_engine.py's bar.
+"""
+import numpy as np
+import pytest
+
+import gpu_util as G
+from conftest import rng
+from test_gpu_ops import _linear, _abs_scale, rand_bf16
+from test_gpu_engine import forced_compare
+
+import qwen_inference_engine_amd as Q
+from qwen_inference_engine_amd import _lib, spec as S, weights as W
+
+pytestmark = pytest.mark.gpu
+
+SYN = W.SynthParams(seed=11, w_scale=0.08, norm_scale=0.25, bias_scale=0.05)
+
+
+def test_fp8_decode_all_codes(qlib):
+    out = G.zeros((256,), np.float32)
+    G.check(qlib.qie_debug_fp8_decode(G.p(out)))
+    got, want = G.host(out), W.e4m3_table()
+    ok = ~np.isnan(want)
+    assert np.array_equal(got[ok].view(np.uint32), want[ok].view(np.uint32))
+    assert np.isnan(got[~ok]).all()
+
+
+@pytest.mark.parametrize("rows,cols", [(7, 64), (33, 896), (5, 18944)])
+def test_quantize_device_equals_host(oracle, qlib, rows, cols):
+    w = rand_bf16(oracle, (rows, cols), 0.05, seed=rows)
+    w[0] = 0                                                 # all-zero row: scale 1
+    w[1 % rows, :3] = oracle.f32_to_bf16(np.array([1e4, -3e-3, 7.0], np.float32))
+    nbytes = int(qlib.qie_fp8_weight_bytes(rows, cols))
+    out = G.zeros((nbytes,), np.uint8)
+    G.check(qlib.qie_quantize_fp8(G.p(G.dev(w)), rows, cols, G.p(out), None))
+    G.check(qlib.qie_synchronize())
+    codes, scales = W.quantize_fp8(w)
+    got = G.host(out)
+    assert np.array_equal(got[:rows * cols].reshape(rows, cols), codes)
+    assert np.array_equal(got[rows * cols:].view(np.float32), scales)
+
+
+def _fp8_dev(qlib, w):
+    rows, cols = w.shape
+    out = G.zeros((int(qlib.qie_fp8_weight_bytes(rows, cols)),), np.uint8)
+    G.check(qlib.qie_quantize_fp8(G.p(G.dev(w)), rows, cols, G.p(out), None))
+    return out, W.dequantize_fp8(*W.quantize_fp8(w))
+
+
+def _linear_fp8(qlib, x, segs, biases, M, K, N, y, epi, **kw):
+    import ctypes as C
+    from qwen_inference_engine_amd._lib import LinearArgsC
+    a = LinearArgsC()
+    a.x, a.ldx = G.p(x), K
+    for i, s in enumerate(segs):
+        a.w[i] = G.p(s[0])
+        a.seg_rows[i] = s[1]
+    for i, b in enumerate(biases):
+        a.bias[i] = G.p(b) if b is not None else None
+    a.M, a.K, a.N = M, K, N
+    a.y, a.ldy = G.p(y), N
+    a.epilogue = epi
+    a.flags = _lib.QIE_LINEAR_FP8
+    if kw.get("keys") is not None:
+        a.argmax_keys = G.p(kw["keys"])
+    G.check(qlib.qie_linear(C.byref(a), None), "qie_linear fp8")
+
+
+@pytest.mark.parametrize("M", [1, 3, 8, 40, 300])
+@pytest.mark.parametrize("K,n", [(128, (64, 32, 32)), (3584, (512, 128, 128))])
+def test_fp8_linear_store_bias(oracle, qlib, M, K, n):
+    x = rand_bf16(oracle, (M, K), seed=M)
+    ws = [rand_bf16(oracle, (r, K), 0.05, seed=10 + i) for i, r in enumerate(n)]
+    bs = [rand_bf16(oracle, (r,), 0.1, seed=20 + i) for i, r in enumerate(n)]
+    q = [_fp8_dev(qlib, w) for w in ws]
+    N = sum(n)
+    want = np.concatenate([oracle.matmul(x, dq, b) for (_, dq), b in zip(q, bs)], axis=1)
+    y = G.zeros_bf16(M, N)
+    _linear_fp8(qlib, G.dev(x), [(d, r) for (d, _), r in zip(q, n)], [G.dev(b) for b in bs], M, K, N, y,
+                _lib.QIE_EPI_STORE)
+    scale = np.concatenate([_abs_scale(oracle, x, dq) for _, dq in q], axis=1)
+    G.assert_sum_close(G.host_bf16(y), want, scale, what=f"fp8 linear M={M} K={K}")
+
+
+@pytest.mark.parametrize("M", [1, 8, 64])
+def test_fp8_linear_swiglu_and_residual(oracle, qlib, M):
+    K, I = 896, 640
+    x = rand_bf16(oracle, (M, K), seed=6)
+    (dg, qg), (du, qu) = _fp8_dev(qlib, rand_bf16(oracle, (I, K), 0.08, seed=7)), \
+        _fp8_dev(qlib, rand_bf16(oracle, (I, K), 0.08, seed=8))
+    want = oracle.silu_mul(oracle.matmul(x, qg), oracle.matmul(x, qu))
+    y = G.zeros_bf16(M, I)
+    _linear_fp8(qlib, G.dev(x), [(dg, I), (du, I)], [], M, K, I, y, _lib.QIE_EPI_SWIGLU)
+    d = G.ulp_diff(G.host_bf16(y), want)
+    assert (d == 0).mean() > 0.97
+    gs = G.bf(oracle.matmul(x, qg)).astype(np.float64)
+    u = np.abs(G.bf(oracle.matmul(x, qu)).astype(np.float64))
+    ill = (np.abs(gs) < 1e-2 * _abs_scale(oracle, x, qg)) | (u < 1e-2 * _abs_scale(oracle, x, qu)) | (gs < -4)
+    assert not ((d > 2) & ~ill).any()
+    # residual: y = bf16(res + bf16(x W^T))
+    dw, qw = _fp8_dev(qlib, rand_bf16(oracle, (K, I), 0.02, seed=4))
+    h = rand_bf16(oracle, (M, I), seed=3)
+    res = rand_bf16(oracle, (M, K), seed=5)
+    want = oracle.resadd(res, oracle.matmul(h, qw))
+    yr = G.dev(res)
+    _linear_fp8(qlib, G.dev(h), [(dw, K)], [], M, I, K, yr, _lib.QIE_EPI_RESIDUAL)
+    acc = G.bf(oracle.matmul(h, qw)).astype(np.float64)
+    tol = 2.0 ** -7 * (np.abs(acc) + np.abs(G.bf(want))) + 1e-5 * _abs_scale(oracle, h, qw)
+    assert (np.abs(G.bf(G.host_bf16(yr)).astype(np.float64) - G.bf(want)) <= tol).all()
+
+
+CONFIGS = {
+    "qwen2-bias-hd64": S.tiny("t-q2", n_layers=3, hidden=256, n_heads=4, n_kv_heads=2, head_dim=64, ffn=512,
+                              vocab=1000, bias=True),
+    "tied-g7": S.tiny("t-tied", n_layers=2, hidden=448, n_heads=7, n_kv_heads=1, head_dim=64, ffn=640,
+                      vocab=777 * 2, tie=True, bias=True),
+}
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+@pytest.mark.parametrize("P", [5, 23])
+def test_fp8_engine_matches_oracle_on_dequantised_model(oracle, name, P):
+    spec = CONFIGS[name]
+    eng = Q.Engine(spec, max_ctx=128, weight_fp8=True).init_synthetic(SYN)
+    hw = W.HostWeights.synthetic(spec, SYN).fp8_dequantized()
+    om = oracle.Model(hw, 128)
+    prompt = list(rng(P).integers(0, spec.vocab, P))
+    ids, flips = forced_compare(oracle, eng.batch(1, 128), om, prompt, 12)
+    assert flips <= 2
+
+
+def test_fp8_batch8_equals_single(oracle):
+    spec = CONFIGS["qwen2-bias-hd64"]
+    eng = Q.Engine(spec, max_ctx=96, weight_fp8=True).init_synthetic(SYN)
+    prompts = [list(rng(40 + i).integers(0, spec.vocab, 4 + 3 * i)) for i in range(8)]
+    singles = []
+    for pr in prompts:
+        b = eng.batch(1, 96)
+        singles.append([b.prefill(0, pr)] + list(b.decode(6)[:, 0]))
+    b8 = eng.batch(8, 96)
+    firsts = [b8.prefill(i, pr) for i, pr in enumerate(prompts)]
+    rest = b8.decode(6)
+    assert [[firsts[i]] + list(rest[:, i]) for i in range(8)] == singles

@@ -1093,7 +1093,7 @@ int qie_linear(const qie_linear_args* a, void* stream) {
                 "qie_linear: F32 (partial-sum) epilogue takes no bias");
     QIE_REQUIRE(a->argmax_keys == nullptr || a->epilogue == QIE_EPI_STORE, "qie_linear: arg-max needs STORE");
     hipStream_t st = (hipStream_t)stream;
-    if (a->M <= 8) return gemv(a, st);
+    if (a->M <= 16) return gemv(a, st);   // GEMV (M = 1..8) or the skinny MFMA kernel (2..16)
     return gemm(a, st);
 }
 

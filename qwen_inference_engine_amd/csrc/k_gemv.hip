@@ -22,6 +22,8 @@
 namespace qie {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 struct GemvParams {
     const uint16_t* x;
@@ -446,6 +448,358 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Skinny MFMA GEMM for 2 <= M <= 16 (batched decode, short prefills): the M activation
+// rows are the 16 rows of v_mfma_f32_16x16x32_bf16's A operand (rows >= M compute
+// garbage that is never stored), a block owns 16 output columns (16 weight rows; 16
+// gate + 16 up for SwiGLU) and its 4 waves split K, so the weights stream exactly once
+// as B fragments (16 B per lane per MFMA step, one weight row per lane column) and the
+// per-element VALU work of the GEMV (M FMAs per weight) moves to the matrix cores.  fp8
+// weights: a 16-B load holds 16 codes = two k-steps; decoded to bf16 (exact) for the
+// bf16 MFMA, the row scale applied to the fp32 result.  Partial C tiles of the 4 waves
+// are summed in LDS, then the epilogue (bias / arg-max keys / residual / SwiGLU / f32).
+// Persistent over column tiles (grid <= 4 blocks per CU) so arg-max keys merge per block.
+template <int EPI, int WT, int XL>
+__global__ __launch_bounds__(256) void skinny_mfma_kernel(GemvParams p) {
+#pragma clang fp contract(off)
+    constexpr int NB = EPI == QIE_EPI_SWIGLU ? 2 : 1;   // B tiles per block (gate, up)
+    constexpr int KSTEP = WT ? 64 : 32;                   // k per 16-byte lane load
+    constexpr int U = (XL && NB == 1) ? 8 : 4;            // units per step (x2 buffers in flight)
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int64_t K = p.K;
+    const int M = p.M;
+    // [M][K + 8]: the 16-B row pad puts the 16 A rows of an MFMA fragment read on
+    // distinct LDS banks (an unpadded 7168-B row stride maps every row to one bank)
+    const int64_t KP = K + 8;
+    uint16_t* xs = reinterpret_cast<uint16_t*>(smem);
+    float* red = reinterpret_cast<float*>(smem + (XL ? (size_t)M * KP * 2 : 0));            // [4][NB][256]
+    __shared__ unsigned long long kb_s[16];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int fr = lane & 15, g = lane >> 4;
+    const int arow = fr < M ? fr : M - 1;   // A row of this lane (rows >= M: garbage, never stored)
+
+    // ---------------- prologue: the M activation rows -> LDS (optionally RMS-normed)
+    if (XL) {
+        if (p.norm_w) {
+            // pass 1: every row's sum of squares at once (loads of all rows in flight,
+            // clamped rows past M), ONE exchange — not a barrier pair per row
+            float ss[16];
+#pragma unroll
+            for (int m = 0; m < 16; m++) ss[m] = 0.f;
+            for (int64_t k = tid * 8; k < K; k += 2048) {
+                uint4 v[16];
+#pragma unroll
+                for (int m = 0; m < 16; m++)
+                    v[m] = *reinterpret_cast<const uint4*>(p.x + (int64_t)(m < M ? m : M - 1) * p.ldx + k);
+#pragma unroll
+                for (int m = 0; m < 16; m++) {
+                    if (m >= M) continue;   // uniform, ALU only (the loads are above)
+                    float f[8];
+                    unpack8(u32x4{v[m].x, v[m].y, v[m].z, v[m].w}, f);
+#pragma unroll
+                    for (int j = 0; j < 8; j++) ss[m] += f[j] * f[j];
+                }
+            }
+#pragma unroll
+            for (int m = 0; m < 16; m++) {
+                if (m >= M) continue;
+                const float t = wave_sum(ss[m]);
+                if (lane == 0) red[wave * 16 + m] = t;
+            }
+            __syncthreads();
+            const bool hf = p.numerics == QIE_NUMERICS_HF;
+            float rms[16], inv[16];
+#pragma unroll
+            for (int m = 0; m < 16; m++) {
+                const int mm = m < M ? m : 0;
+                const float sm = red[mm] + red[16 + mm] + red[32 + mm] + red[48 + mm];
+                rms[m] = sqrtf((sm / (float)K) + p.eps);
+                inv[m] = 1.0f / rms[m];
+            }
+            // pass 2: all rows of a chunk at once (loads unconditional and clamped; the
+            // per-row math under uniform branches).  REF's f / rms uses the FMA-corrected
+            // quotient (Markstein): correctly rounded, i.e. equal to the division, for
+            // normal operands — |f| outside [1e-30, 1e30] takes the real division.
+            for (int64_t k = tid * 8; k < K; k += 2048) {
+                const uint4 nw = *reinterpret_cast<const uint4*>(p.norm_w + k);
+                uint4 v[16];
+#pragma unroll
+                for (int m = 0; m < 16; m++)
+                    v[m] = *reinterpret_cast<const uint4*>(p.x + (int64_t)(m < M ? m : M - 1) * p.ldx + k);
+                float wf[8];
+                unpack8(u32x4{nw.x, nw.y, nw.z, nw.w}, wf);
+#pragma unroll
+                for (int m = 0; m < 16; m++) {
+                    if (m >= M) continue;
+                    float f[8];
+                    unpack8(u32x4{v[m].x, v[m].y, v[m].z, v[m].w}, f);
+                    uint32_t o[4];
+                    if (hf) {
+#pragma unroll
+                        for (int j = 0; j < 4; j++)
+                            o[j] = pack2(wf[2 * j] * rbf(f[2 * j] * inv[m]), wf[2 * j + 1] * rbf(f[2 * j + 1] * inv[m]));
+                    } else {
+                        float y[8];
+#pragma unroll
+                        for (int j = 0; j < 8; j++) {
+                            const float q = f[j] * inv[m];
+                            float d = fmaf(fmaf(-q, rms[m], f[j]), inv[m], q);
+                            const float af = fabsf(f[j]);
+                            if (af != 0.f && (af < 1e-30f || af > 1e30f)) d = f[j] / rms[m];
+                            y[j] = d * wf[j];
+                        }
+#pragma unroll
+                        for (int j = 0; j < 4; j++) o[j] = pack2(y[2 * j], y[2 * j + 1]);
+                    }
+                    *reinterpret_cast<uint4*>(xs + (int64_t)m * KP + k) = make_uint4(o[0], o[1], o[2], o[3]);
+                }
+            }
+        } else {
+            for (int m = 0; m < M; m++)
+                for (int64_t k = tid * 8; k < K; k += 2048)
+                    *reinterpret_cast<uint4*>(xs + (int64_t)m * KP + k) =
+                        *reinterpret_cast<const uint4*>(p.x + (int64_t)m * p.ldx + k);
+        }
+        __syncthreads();
+    }
+    auto xa = [&](int64_t k) -> uint4 {   // 8 activations of this lane's A row at k
+        return XL ? *reinterpret_cast<const uint4*>(xs + (int64_t)arow * KP + k)
+                  : *reinterpret_cast<const uint4*>(p.x + (int64_t)arow * p.ldx + k);
+    };
+
+    // segment pointers as laundered byte offsets from one base (see issue()): the
+    // result stays a global-address-space pointer derived from that base
+    const uint8_t* const wbase = reinterpret_cast<const uint8_t*>(p.w0);
+    const uint64_t dw1 = launder_u64((uint64_t)p.w1 - (uint64_t)p.w0);
+    const uint64_t dw2 = launder_u64((uint64_t)p.w2 - (uint64_t)p.w0);
+    const uint8_t* const bbase = reinterpret_cast<const uint8_t*>(p.x);
+    auto boff = [&](const uint16_t* b) { return launder_u64(b ? (uint64_t)b - (uint64_t)p.x : 0ull); };
+    const uint64_t db0 = boff(p.b0), db1 = boff(p.b1), db2 = boff(p.b2);
+    const uint64_t hb0 = launder_u64(p.b0 ? ~0ull : 0ull), hb1 = launder_u64(p.b1 ? ~0ull : 0ull),
+                   hb2 = launder_u64(p.b2 ? ~0ull : 0ull);   // segment has a bias (all-ones mask)
+    // this wave's K range, in 16-byte load units; a tile is NBAT steps of U units
+    const int64_t units = K / KSTEP;
+    const int64_t uw = (units + 3) / 4;
+    const int64_t ub = wave * uw, ue = ub + uw < units ? ub + uw : units;
+    const int64_t nbat = (uw + U - 1) / U;
+    const int64_t n_tiles = (p.N + 15) / 16;
+    if ((int64_t)blockIdx.x >= n_tiles) return;   // block-uniform, before any barrier
+    const int64_t my_tiles = (n_tiles - 1 - blockIdx.x) / gridDim.x + 1;
+    const int64_t S = my_tiles * nbat;            // steps of this block (same for every wave)
+    unsigned long long kbest[4] = {0ull, 0ull, 0ull, 0ull};   // rows 4 g + r
+
+    // One step = U units of every B tile of one column tile, plus that tile's epilogue
+    // operands (row scales, bias / residual values), all loaded unconditionally so no
+    // global load sits under a branch: the steps form one stream per wave, double-
+    // buffered in registers, so the next step's loads (next tile included) are in
+    // flight while this step's MFMAs, the cross-wave reduction and the epilogue run.
+    constexpr int AW = WT ? 2 : 1;   // 16-B A fragments per unit
+    constexpr int EB = WT ? 1 : 2;
+    struct Step {
+        u32x4 wv[U][NB];
+        uint4 av[XL ? 1 : U][AW];
+        float wsc[NB];
+        float ep[4];       // residual values (rows 4 g + r) or the bias (ep[0])
+        int64_t u0, tile;
+        bool last;         // last step of its tile
+    };
+    auto issue = [&](Step& st, int64_t s) {
+        s = s < S ? s : S - 1;
+        const int64_t tl = s / nbat, j = s - tl * nbat;
+        st.tile = blockIdx.x + tl * gridDim.x;
+        st.u0 = ub + j * U;
+        st.last = j == nbat - 1;
+        const int64_t n = st.tile * 16 + fr;
+        const int64_t nc = n < p.N ? n : p.N - 1;
+        const uint8_t* wrow[NB];
+        const float* scp[NB];
+        int64_t r = nc;    // row within the column's segment
+        if constexpr (NB == 2) {
+            wrow[0] = wbase + nc * K * EB;
+            wrow[1] = wbase + dw1 + nc * K * EB;
+            scp[0] = reinterpret_cast<const float*>(wbase + p.N * K) + nc;
+            scp[1] = reinterpret_cast<const float*>(wbase + dw1 + p.N * K) + nc;
+        } else {
+            // segment resolved by integer selects on laundered (register) pointers: a
+            // select between two kernel-argument loads would become a per-lane load
+            const bool s0 = nc < p.n0, s1 = !s0 && nc < p.n01;
+            r = s0 ? nc : (s1 ? nc - p.n0 : nc - p.n01);
+            const uint64_t m0 = 0ull - (uint64_t)s0, m1 = 0ull - (uint64_t)s1, m2 = ~(m0 | m1);
+            const uint8_t* wb = wbase + ((dw1 & m1) | (dw2 & m2));
+            (void)m0;
+            const int64_t rows = s0 ? p.n0 : (s1 ? p.n01 - p.n0 : p.N - p.n01);
+            wrow[0] = wb + r * K * EB;
+            scp[0] = reinterpret_cast<const float*>(wb + rows * K) + r;
+        }
+        if constexpr (WT != 0) {
+#pragma unroll
+            for (int b = 0; b < NB; b++) st.wsc[b] = *scp[b];
+        }
+        if constexpr (EPI == QIE_EPI_RESIDUAL) {
+#pragma unroll
+            for (int rr = 0; rr < 4; rr++) {
+                const int i = 4 * g + rr < M ? 4 * g + rr : M - 1;
+                st.ep[rr] = bf2f(p.y[(int64_t)i * p.ldy + nc]);
+            }
+        } else if constexpr (EPI == QIE_EPI_STORE) {
+            // bias: always loaded (a missing segment bias reads x[0] and is multiplied by 0)
+            const bool s0 = nc < p.n0, s1 = !s0 && nc < p.n01;
+            const uint64_t m0 = 0ull - (uint64_t)s0, m1 = 0ull - (uint64_t)s1, m2 = ~(m0 | m1);
+            const uint8_t* bb = bbase + ((db0 & m0) | (db1 & m1) | (db2 & m2));
+            const uint64_t hb = (hb0 & m0) | (hb1 & m1) | (hb2 & m2);
+            const uint16_t v = *(reinterpret_cast<const uint16_t*>(bb) + (r & (int64_t)hb));
+            st.ep[0] = __uint_as_float((uint32_t)hb & __float_as_uint(bf2f(v)));
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int64_t uu = st.u0 + u < ue ? st.u0 + u : ue - 1;
+#pragma unroll
+            for (int b = 0; b < NB; b++)   // bytes [uu * 64 + 16 g, +16) of the row, both formats
+                st.wv[u][b] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wrow[b]) + uu * 4 + g);
+            if constexpr (!XL) {
+                const int64_t kk = uu * KSTEP + (WT ? 16 : 8) * g;
+#pragma unroll
+                for (int h = 0; h < AW; h++) st.av[u][h] = xa(kk + 8 * h);
+            }
+        }
+    };
+    f32x4_t acc[NB];
+#pragma unroll
+    for (int b = 0; b < NB; b++) acc[b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    auto compute = [&](const Step& st) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const bool live = st.u0 + u < ue;   // dead steps multiply a zero A fragment
+            const int64_t uu = live ? st.u0 + u : ue - 1;
+            const int64_t kk = uu * KSTEP + (WT ? 16 : 8) * g;
+            uint4 ar[AW];
+#pragma unroll
+            for (int h = 0; h < AW; h++) {
+                const uint4 v = XL ? xa(kk + 8 * h) : st.av[XL ? 0 : u][h];
+                ar[h] = live ? v : make_uint4(0, 0, 0, 0);
+            }
+            if constexpr (WT == 0) {
+                const bf16x8_t a = __builtin_bit_cast(bf16x8_t, ar[0]);
+#pragma unroll
+                for (int b = 0; b < NB; b++)
+                    acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8_t, st.wv[u][b]),
+                                                                     acc[b], 0, 0, 0);
+            } else {
+                const bf16x8_t a0 = __builtin_bit_cast(bf16x8_t, ar[0]);
+                const bf16x8_t a1 = __builtin_bit_cast(bf16x8_t, ar[AW - 1]);
+#pragma unroll
+                for (int b = 0; b < NB; b++) {
+                    float f[16];
+                    fp8x4_to_f32(st.wv[u][b].x, f);
+                    fp8x4_to_f32(st.wv[u][b].y, f + 4);
+                    fp8x4_to_f32(st.wv[u][b].z, f + 8);
+                    fp8x4_to_f32(st.wv[u][b].w, f + 12);
+                    const uint4 lo = make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]),
+                                                pack2(f[6], f[7]));
+                    const uint4 hi = make_uint4(pack2(f[8], f[9]), pack2(f[10], f[11]), pack2(f[12], f[13]),
+                                                pack2(f[14], f[15]));
+                    acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, __builtin_bit_cast(bf16x8_t, lo), acc[b],
+                                                                     0, 0, 0);
+                    acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, __builtin_bit_cast(bf16x8_t, hi), acc[b],
+                                                                     0, 0, 0);
+                }
+            }
+        }
+    };
+    // ---- end of a tile: sum the 4 waves' partial tiles (C map: col = fr, rows 4 g + r),
+    // epilogue by wave 0.  The barriers wait on LDS only (no vmcnt), so the prefetched
+    // next step stays in flight.
+    auto tile_end = [&](const Step& st) {
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+            *reinterpret_cast<float4*>(&red[(wave * NB + b) * 256 + lane * 4]) =
+                make_float4(acc[b][0], acc[b][1], acc[b][2], acc[b][3]);
+            acc[b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        }
+        __syncthreads();
+        if (wave == 0) {
+            const int64_t n = st.tile * 16 + fr;
+            float c[NB][4];
+#pragma unroll
+            for (int b = 0; b < NB; b++)
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+                    c[b][r] = ((red[(0 * NB + b) * 256 + lane * 4 + r] + red[(1 * NB + b) * 256 + lane * 4 + r]) +
+                               red[(2 * NB + b) * 256 + lane * 4 + r]) + red[(3 * NB + b) * 256 + lane * 4 + r];
+            if constexpr (WT != 0) {
+#pragma unroll
+                for (int b = 0; b < NB; b++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) c[b][r] *= st.wsc[b];
+            }
+            if (n < p.N) {
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int i = 4 * g + r;
+                    if (i >= M) continue;
+                    uint16_t* yr = p.y + (int64_t)i * p.ldy;
+                    if constexpr (EPI == QIE_EPI_SWIGLU) {
+                        const float gg = rbf(c[0][r]);
+                        const float uu = rbf(c[1][r]);
+                        const float av = rbf(gg * (1.0f / (1.0f + expf(-gg))));
+                        yr[n] = f2bf(uu * av);
+                    } else if constexpr (EPI == QIE_EPI_RESIDUAL) {
+                        yr[n] = f2bf(st.ep[r] + rbf(c[0][r]));
+                    } else if constexpr (EPI == QIE_EPI_F32) {
+                        reinterpret_cast<float*>(p.y)[(int64_t)i * p.ldy + n] = c[0][r];
+                    } else {
+                        const uint16_t o = f2bf(c[0][r] + st.ep[0]);
+                        yr[n] = o;
+                        if (p.keys) {
+                            const unsigned long long kk = sel_key(bf2f(o), (uint32_t)(n + p.key_col0));
+                            kbest[r] = kk > kbest[r] ? kk : kbest[r];
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();   // red[] reused by the next tile
+    };
+
+    // steady state issues unconditionally (a load under a branch costs a vmcnt(0) at the
+    // join); the last one or two steps are peeled so nothing past step S - 1 is fetched
+    Step sa, sb;
+    issue(sa, 0);
+    int64_t s = 0;
+    for (; s + 2 < S; s += 2) {
+        issue(sb, s + 1);
+        compute(sa);
+        if (sa.last) tile_end(sa);
+        issue(sa, s + 2);
+        compute(sb);
+        if (sb.last) tile_end(sb);
+    }
+    if (S - s == 2) {
+        issue(sb, s + 1);
+        compute(sa);
+        if (sa.last) tile_end(sa);
+        compute(sb);
+        tile_end(sb);
+    } else {
+        compute(sa);
+        tile_end(sa);
+    }
+    if constexpr (EPI == QIE_EPI_STORE) {
+        if (p.keys && wave == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                unsigned long long v = kbest[r];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {   // max over the 16 columns of row 4 g + r
+                    const unsigned long long t = __shfl_xor(v, o, 64);
+                    v = t > v ? t : v;
+                }
+                if (fr == 0 && 4 * g + r < M && v) atomicMax(p.keys + 4 * g + r, v);
+            }
+        }
+    }
+}
+
 template <int MT, int RPW, int EPI, int XCH, int WT>
 static int launch_gemv_t(const GemvParams& p, hipStream_t st, int blocks_per_cu) {
     constexpr int U = (RPW >= 4) ? 4 : 8;
@@ -506,12 +860,61 @@ static int launch_gemv_1(const GemvParams& p, int rpw, int epi, hipStream_t st, 
     return launch_gemv_m<1, 0>(p, rpw, epi, st, bpc);
 }
 
+int gemm(const qie_linear_args* a, hipStream_t st);
+
 static int env_int(const char* name, int dflt) {
     const char* v = getenv(name);
     return v ? atoi(v) : dflt;
 }
 
 constexpr size_t kGemvLdsCap = 96 * 1024;
+constexpr size_t kSkinnyLdsCap = 120 * 1024;
+
+template <int EPI, int WT, int XL>
+static int launch_skinny_x(const GemvParams& p, hipStream_t st) {
+    constexpr int NB = EPI == QIE_EPI_SWIGLU ? 2 : 1;
+    const void* fn = (const void*)skinny_mfma_kernel<EPI, WT, XL>;
+    const size_t shm = (p.xlds ? (size_t)p.M * (p.K + 8) * 2 : 0) + (size_t)4 * NB * 256 * 4;
+    if (shm > 65536) {
+        static bool raised = false;
+        if (!raised) {
+            QIE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+            raised = true;
+        }
+    }
+    const int64_t n_tiles = (p.N + 15) / 16;
+    // as many blocks as are resident at once (LDS-limited when the M rows are staged)
+    static size_t cached_shm = 0;
+    static int cached_nb = 0;
+    if (cached_shm != shm || cached_nb == 0) {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 256, shm) != hipSuccess || nb < 1) nb = 1;
+        cached_shm = shm;
+        cached_nb = nb;
+    }
+    const unsigned grid =
+        (unsigned)std::max<int64_t>(1, std::min<int64_t>(n_tiles, (int64_t)device_cu_count() * cached_nb));
+    hipLaunchKernelGGL((skinny_mfma_kernel<EPI, WT, XL>), dim3(grid), dim3(256), shm, st, p);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+template <int EPI, int WT>
+static int launch_skinny_t(const GemvParams& p, hipStream_t st) {
+    return p.xlds ? launch_skinny_x<EPI, WT, 1>(p, st) : launch_skinny_x<EPI, WT, 0>(p, st);
+}
+
+static int launch_skinny(const GemvParams& p, int epi, bool fp8w, hipStream_t st) {
+    if (fp8w) {
+        if (epi == QIE_EPI_SWIGLU) return launch_skinny_t<QIE_EPI_SWIGLU, 1>(p, st);
+        if (epi == QIE_EPI_RESIDUAL) return launch_skinny_t<QIE_EPI_RESIDUAL, 1>(p, st);
+        if (epi == QIE_EPI_F32) return launch_skinny_t<QIE_EPI_F32, 1>(p, st);
+        return launch_skinny_t<QIE_EPI_STORE, 1>(p, st);
+    }
+    if (epi == QIE_EPI_SWIGLU) return launch_skinny_t<QIE_EPI_SWIGLU, 0>(p, st);
+    if (epi == QIE_EPI_RESIDUAL) return launch_skinny_t<QIE_EPI_RESIDUAL, 0>(p, st);
+    if (epi == QIE_EPI_F32) return launch_skinny_t<QIE_EPI_F32, 0>(p, st);
+    return launch_skinny_t<QIE_EPI_STORE, 0>(p, st);
+}
 static bool K_fits(int64_t K, int xch) { return K <= 2048 * (int64_t)xch && K % 8 == 0; }
 
 int gemv(const qie_linear_args* a, hipStream_t st) {
@@ -536,6 +939,17 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
     p.M = (int)a->M;
     p.keys = (unsigned long long*)a->argmax_keys;
     p.key_col0 = a->key_col0;
+    if (a->M >= 2 && a->M <= 16 && env_int("QIE_SKINNY_MFMA", 1) != 0) {
+        const bool fp8w = (a->flags & QIE_LINEAR_FP8) != 0;
+        const int kstep = fp8w ? 64 : 32;
+        const bool lds_ok = (size_t)a->M * (a->K + 8) * 2 <= kSkinnyLdsCap;
+        if (a->K % kstep == 0 && (lds_ok || !a->norm_w)) {
+            p.M = (int)a->M;
+            p.xlds = lds_ok ? 1 : 0;
+            return launch_skinny(p, a->epilogue, fp8w, st);
+        }
+    }
+    if (a->M > 8) return gemm(a, st);   // 9..16 rows the skinny kernel could not take
     const int MT = a->M <= 1 ? 1 : a->M <= 2 ? 2 : a->M <= 4 ? 4 : 8;
     p.xlds = ((size_t)MT * a->K * 2 <= kGemvLdsCap) ? 1 : 0;
     QIE_REQUIRE(p.xlds || !p.norm_w,

@@ -102,6 +102,20 @@ __device__ __forceinline__ void fp8x4_to_f32(uint32_t w, float* f) {
     f[3] = hi[1];
 }
 
+// A uniform pointer as an opaque register value: per-lane selects between
+// laundered pointers stay v_cndmask on values instead of being folded into a per-lane
+// load of the kernel-argument slot (which costs a vmcnt(0) round trip).
+template <class T>
+__device__ __forceinline__ const T* launder_ptr(const T* p) {
+    asm volatile("" : "+v"(p));
+    return p;
+}
+
+__device__ __forceinline__ uint64_t launder_u64(uint64_t v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
 // ------------------------------------------------------ cross-lane reductions
 // __shfl_xor lowers to ds_bpermute_b32 (an LDS round trip, ~100 cycles); chains of
 // them serialised the decode attention.  These use DPP row ops (folded into the

@@ -20,7 +20,7 @@ rc=$?; tail -3 gpurun_out/bench.log; echo "bench rc=$rc"
 if [ "${PROFILE:-0}" = "1" ]; then
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof" \
-      -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 64 --warmup 4 --prefill-iters 1 --no-cpu-baseline \
+      -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 64 --warmup 4 --prefill-iters 1 --no-cpu-baseline ${PROF_ARGS:-} \
       > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1
   rc=$?; echo "rocprof rc=$rc"; cd "$GRAFT_REPO_ROOT"
   [ $rc -eq 0 ] || exit $rc

@@ -768,6 +768,196 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(PrefillAttnParam
 }
 
 // ---------------------------------------------------------------------------
+// Prefill v2 (default): as attn_prefill_mfma_kernel, but each wave owns 32 query rows
+// (two 16-row groups), so every K fragment (S^T = K.Q^T) and every V fragment
+// (O += P.V) read from LDS feeds two MFMAs and one staged K/V tile serves 128 rows —
+// LDS reads and staging writes per MFMA halved.  Scores go to the log2 domain once
+// (dot * log2(e) / sqrt(hd)) and are exponentiated with v_exp_f32: the reference build
+// compiles with -use_fast_math, i.e. __expf / __fdividef, so the libm
+// expf and IEEE division of v1 (~25 VALU ops per score) bought nothing but VALU time.
+// A wave skips the MFMAs of a tile whose first key lies past its last row's position.
+template <int HD>
+__global__ __launch_bounds__(256) void attn_prefill_mfma2_kernel(PrefillAttnParams a) {
+    constexpr int KT = 64;
+    constexpr int CPR = HD / 8;
+    constexpr int KSTEPS = HD / 32;
+    constexpr int DT = HD / 16;
+    constexpr int CHUNKS = KT * CPR;
+    constexpr int LPT = CHUNKS / 256;
+    constexpr int QG = 2;                  // 16-row query groups per wave
+    constexpr int BQ = 4 * 16 * QG;        // query rows per block
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint16_t* Ks = reinterpret_cast<uint16_t*>(smem);
+    uint16_t* Vs = reinterpret_cast<uint16_t*>(smem + 2 * KT * HD * 2);
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int fr = lane & 15, g = lane >> 4;
+    const int h = blockIdx.y, seq = blockIdx.z;
+    const int ntiles_q = (a.rows_per_seq + BQ - 1) / BQ;
+    const int qt = ntiles_q - 1 - (int)blockIdx.x;
+    const int64_t row0 = (int64_t)seq * a.rows_per_seq;
+    const int rlo = qt * BQ, rhi = min(a.rows_per_seq, rlo + BQ);
+    const int G = a.nq / a.nkv, kvh = h / G;
+    const int64_t head_off = (((int64_t)a.layer * a.nkv + kvh) * a.max_ctx) * HD;
+    const uint16_t* kb = a.kc + seq * a.seq_stride + head_off;
+    const uint16_t* vb = a.vc + seq * a.seq_stride + head_off;
+    const int kmax = a.pos[row0 + rhi - 1];
+    const int nkt = kmax / KT + 1;
+    // positions are non-decreasing within a sequence: the wave's last row bounds its keys
+    const int wpos = a.pos[row0 + min(rlo + wave * 16 * QG + 16 * QG - 1, rhi - 1)];
+
+    int qpos[QG];
+    bf16x8_t qf[QG][KSTEPS];
+#pragma unroll
+    for (int q = 0; q < QG; q++) {
+        const int qrow = min(rlo + wave * 16 * QG + q * 16 + fr, rhi - 1);
+        qpos[q] = a.pos[row0 + qrow];
+        const uint16_t* qp = a.q + (row0 + qrow) * (int64_t)a.nq * HD + (int64_t)h * HD;
+#pragma unroll
+        for (int ks = 0; ks < KSTEPS; ks++) qf[q][ks] = *reinterpret_cast<const bf16x8_t*>(qp + ks * 32 + g * 8);
+    }
+
+    uint4 rk[LPT], rv[LPT];
+    auto gload = [&](int kt) {
+#pragma unroll
+        for (int i = 0; i < LPT; i++) {
+            const int c = tid + 256 * i;
+            const int key = min(kt * KT + c / CPR, kmax);
+            const int ch = c % CPR;
+            rk[i] = *reinterpret_cast<const uint4*>(kb + (int64_t)key * HD + ch * 8);
+            rv[i] = *reinterpret_cast<const uint4*>(vb + (int64_t)key * HD + ch * 8);
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < LPT; i++) {
+            const int c = tid + 256 * i;
+            const int r = c / CPR, ch = c % CPR;
+            *reinterpret_cast<uint4*>(Ks + buf * KT * HD + r * HD + ((ch ^ (r & (CPR - 1))) * 8)) = rk[i];
+            *reinterpret_cast<uint4*>(Vs + buf * KT * HD + r * HD + ch * 8) = rv[i];
+        }
+    };
+
+    f32x4_t oacc[QG][DT];
+#pragma unroll
+    for (int q = 0; q < QG; q++)
+#pragma unroll
+        for (int d = 0; d < DT; d++) oacc[q][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    float m_run[QG], l_run[QG];
+#pragma unroll
+    for (int q = 0; q < QG; q++) {
+        m_run[q] = -INFINITY;
+        l_run[q] = 0.f;
+    }
+    const float sl2 = 1.4426950408889634f / sqrtf((float)HD);   // log2(e) / sqrt(hd)
+
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    int cur = 0;
+    for (int kt = 0; kt < nkt; kt++) {
+        if (kt + 1 < nkt) gload(kt + 1);
+        const uint16_t* K = Ks + cur * KT * HD;
+        const uint16_t* Vt = Vs + cur * KT * HD;
+        if (kt * KT <= wpos) {   // wave-uniform
+            f32x4_t sacc[QG][4];
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+#pragma unroll
+                for (int q = 0; q < QG; q++) sacc[q][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+                const int r = t * 16 + fr;
+#pragma unroll
+                for (int ks = 0; ks < KSTEPS; ks++) {
+                    const int ch = ks * 4 + g;
+                    const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(K + r * HD + ((ch ^ (r & (CPR - 1))) * 8));
+#pragma unroll
+                    for (int q = 0; q < QG; q++)
+                        sacc[q][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[q][ks], sacc[q][t], 0, 0, 0);
+                }
+            }
+            bf16x8_t pa[QG][2];
+#pragma unroll
+            for (int q = 0; q < QG; q++) {
+                float sv[4][4];
+                float mt = -INFINITY;
+#pragma unroll
+                for (int t = 0; t < 4; t++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const int key = kt * KT + t * 16 + g * 4 + r;
+                        const float sc = key <= qpos[q] ? sacc[q][t][r] * sl2 : -INFINITY;
+                        sv[t][r] = sc;
+                        mt = fmaxf(mt, sc);
+                    }
+                mt = xor32_max(xor16_max(mt));
+                const float m_new = fmaxf(m_run[q], mt);   // finite: tile 0 holds key 0 <= every position
+                const float alpha = __builtin_amdgcn_exp2f(m_run[q] - m_new);
+                float ls = 0.f;
+#pragma unroll
+                for (int t = 0; t < 4; t++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const float e = __builtin_amdgcn_exp2f(sv[t][r] - m_new);
+                        sv[t][r] = e;
+                        ls += e;
+                    }
+                ls = xor32_sum(xor16_sum(ls));
+                l_run[q] = l_run[q] * alpha + ls;
+                m_run[q] = m_new;
+                float ar[4];
+#pragma unroll
+                for (int r = 0; r < 4; r++) ar[r] = __shfl(alpha, g * 4 + r, 64);
+#pragma unroll
+                for (int d = 0; d < DT; d++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) oacc[q][d][r] *= ar[r];
+#pragma unroll
+                for (int c = 0; c < 2; c++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        pa[q][c][j] = (__bf16)sv[2 * c][j];
+                        pa[q][c][4 + j] = (__bf16)sv[2 * c + 1][j];
+                    }
+            }
+            const int q4 = fr >> 2, p4 = fr & 3;
+#pragma unroll
+            for (int c = 0; c < 2; c++) {
+#pragma unroll
+                for (int d = 0; d < DT; d++) {
+                    const uint16_t* a0 = Vt + (32 * c + 4 * g + q4) * HD + 16 * d + 4 * p4;
+                    const i16x4_t v0 =
+                        __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4_t*)(a0));
+                    const i16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (__attribute__((address_space(3))) i16x4_t*)(a0 + 16 * HD));
+                    const bf16x8_t vb8 =
+                        __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+                    for (int q = 0; q < QG; q++)
+                        oacc[q][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[q][c], vb8, oacc[q][d], 0, 0, 0);
+                }
+            }
+        }
+        if (kt + 1 < nkt) lstore(cur ^ 1);
+        __syncthreads();
+        cur ^= 1;
+    }
+#pragma unroll
+    for (int q = 0; q < QG; q++) {
+        float lr[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) lr[r] = __shfl(l_run[q], g * 4 + r, 64);
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int row = rlo + wave * 16 * QG + q * 16 + g * 4 + r;
+            if (row >= rhi) continue;
+            uint16_t* orow = a.out + (row0 + row) * (int64_t)a.nq * HD + (int64_t)h * HD;
+#pragma unroll
+            for (int d = 0; d < DT; d++) orow[16 * d + fr] = f2bf(oacc[q][d][r] / lr[r]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Decode attention on MFMA (default decode path).  The q heads of one kv head
 // (G <= 8, padded to 16) play the role of the 16 "query rows" of the prefill
 // kernel above, so GQA decode is a 16 x 32 x HD flash step per wave:
@@ -1574,8 +1764,17 @@ int qie_attention(const void* q, int64_t M, const int32_t* pos, int32_t rows_per
         pa.M = M;
         pa.out = (uint16_t*)out;
         pa.no_tr = getenv("QIE_ATTN_NO_TR") ? 1 : 0;
-        dim3 grid((unsigned)((rows_per_seq + 63) / 64), (unsigned)n_heads, (unsigned)(M / rows_per_seq));
         const size_t shm = (size_t)2 * 2 * 64 * cache->head_dim * 2;
+        if (!getenv("QIE_ATTN_PREFILL_V1") && !pa.no_tr) {   // v1: A/B timing and diagnostics only
+            dim3 g2((unsigned)((rows_per_seq + 127) / 128), (unsigned)n_heads, (unsigned)(M / rows_per_seq));
+            if (cache->head_dim == 128)
+                hipLaunchKernelGGL(attn_prefill_mfma2_kernel<128>, g2, dim3(256), shm, (hipStream_t)stream, pa);
+            else
+                hipLaunchKernelGGL(attn_prefill_mfma2_kernel<64>, g2, dim3(256), shm, (hipStream_t)stream, pa);
+            QIE_LAUNCH_CHECK();
+            return 0;
+        }
+        dim3 grid((unsigned)((rows_per_seq + 63) / 64), (unsigned)n_heads, (unsigned)(M / rows_per_seq));
         if (cache->head_dim == 128)
             hipLaunchKernelGGL(attn_prefill_mfma_kernel<128>, grid, dim3(256), shm, (hipStream_t)stream, pa);
         else

@@ -73,12 +73,14 @@ __device__ __forceinline__ const float* fp8_scales(const uint16_t* w, int64_t ro
     return reinterpret_cast<const float*>(reinterpret_cast<const uint8_t*>(w) + rows * K);
 }
 
-template <int MT, int RPW, int EPI, int U, int XCH, int WT>
-__global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
+template <int MT, int RPW, int EPI, int U, int XCH, int WT, int LB = 256>
+__global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint16_t* xs = reinterpret_cast<uint16_t*>(smem);
     float* red = reinterpret_cast<float*>(smem + (p.xlds ? (size_t)MT * p.K * 2 : 0));
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int NWv = blockDim.x >> 6;         // waves per block: 4, or 5..9 for the one-block-per-CU grid
+    const int64_t TS = (int64_t)blockDim.x * 8;   // x elements per block-wide 16-byte pass
     const int64_t K = p.K;
     constexpr int EB = WT ? 1 : 2;     // bytes per weight
     constexpr int EL = 16 / EB;        // weights per 16-byte lane load
@@ -190,8 +192,8 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
         }
     };
 
-    const int64_t tstride = (int64_t)gridDim.x * 4;
-    const int64_t task0 = (int64_t)blockIdx.x * 4 + wave;
+    const int64_t tstride = (int64_t)gridDim.x * NWv;
+    const int64_t task0 = (int64_t)blockIdx.x * NWv + wave;
     const u32x4* wr[RPW];
     u32x4 wv[U][RPW];
     constexpr bool PF = XCH > 0;
@@ -207,7 +209,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
         uint4 xv[XCH], nv[NV];
 #pragma unroll
         for (int c = 0; c < XCH; c++) {
-            const int64_t k = (int64_t)tid * 8 + c * 2048;
+            const int64_t k = (int64_t)tid * 8 + c * TS;
             const int64_t kc = k < K ? k : K - 8;   // clamped: loads stay unconditional
             xv[c] = *reinterpret_cast<const uint4*>(p.x + kc);
             if (c < NV) nv[c] = *reinterpret_cast<const uint4*>((nrm ? p.norm_w : p.x) + kc);
@@ -229,7 +231,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
             float ss = 0.f;
 #pragma unroll
             for (int c = 0; c < XCH; c++) {
-                if ((int64_t)tid * 8 + c * 2048 >= K) continue;
+                if ((int64_t)tid * 8 + c * TS >= K) continue;
                 float f[8];
                 unpack8(u32x4{xv[c].x, xv[c].y, xv[c].z, xv[c].w}, f);
 #pragma unroll
@@ -238,14 +240,15 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
             ss = wave_sum(ss);
             if (lane == 0) red[wave] = ss;
             __syncthreads();
-            ss = red[0] + red[1] + red[2] + red[3];
+            ss = 0.f;
+            for (int w = 0; w < NWv; w++) ss += red[w];
             const float rms = sqrtf((ss / (float)K) + p.eps);
             const float inv = 1.0f / rms;
             const bool hf = p.numerics == QIE_NUMERICS_HF;
 #pragma unroll
             for (int c = 0; c < XCH; c++) {
 #pragma clang fp contract(off)
-                const int64_t k = (int64_t)tid * 8 + c * 2048;
+                const int64_t k = (int64_t)tid * 8 + c * TS;
                 if (k >= K) continue;
                 float f[8], wf[8];
                 unpack8(u32x4{xv[c].x, xv[c].y, xv[c].z, xv[c].w}, f);
@@ -269,7 +272,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
         if (!staged) {
 #pragma unroll
             for (int c = 0; c < XCH; c++) {
-                const int64_t k = (int64_t)tid * 8 + c * 2048;
+                const int64_t k = (int64_t)tid * 8 + c * TS;
                 if (k < K) *reinterpret_cast<uint4*>(xs + k) = xv[c];
             }
         }
@@ -280,13 +283,13 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
             const uint16_t* xr = p.x + (int64_t)m * p.ldx;
             uint16_t* xo = xs + (int64_t)m * K;
             if (m >= p.M) {
-                for (int64_t k = tid * 8; k < K; k += 2048)
+                for (int64_t k = tid * 8; k < K; k += TS)
                     *reinterpret_cast<uint4*>(xo + k) = make_uint4(0, 0, 0, 0);
                 continue;
             }
             if (p.norm_w) {
                 float ss = 0.f;
-                for (int64_t k = tid * 8; k < K; k += 2048) {
+                for (int64_t k = tid * 8; k < K; k += TS) {
                     uint4 v = *reinterpret_cast<const uint4*>(xr + k);
                     float f[8];
                     unpack8(u32x4{v.x, v.y, v.z, v.w}, f);
@@ -296,12 +299,13 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
                 ss = wave_sum(ss);
                 if (lane == 0) red[wave] = ss;
                 __syncthreads();
-                ss = red[0] + red[1] + red[2] + red[3];
+                ss = 0.f;
+                for (int w = 0; w < NWv; w++) ss += red[w];
                 __syncthreads();
                 const float rms = sqrtf((ss / (float)K) + p.eps);
                 const float inv = 1.0f / rms;
                 const bool hf = p.numerics == QIE_NUMERICS_HF;
-                for (int64_t k = tid * 8; k < K; k += 2048) {
+                for (int64_t k = tid * 8; k < K; k += TS) {
 #pragma clang fp contract(off)
                     uint4 v = *reinterpret_cast<const uint4*>(xr + k);
                     uint4 nw = *reinterpret_cast<const uint4*>(p.norm_w + k);
@@ -324,7 +328,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
                     *reinterpret_cast<uint4*>(xo + k) = make_uint4(o[0], o[1], o[2], o[3]);
                 }
             } else {
-                for (int64_t k = tid * 8; k < K; k += 2048)
+                for (int64_t k = tid * 8; k < K; k += TS)
                     *reinterpret_cast<uint4*>(xo + k) = *reinterpret_cast<const uint4*>(xr + k);
             }
         }
@@ -432,7 +436,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
     }
     if constexpr (EPI == QIE_EPI_STORE) {
         if (p.keys) {
-            __shared__ unsigned long long kb_s[4][MT];
+            __shared__ unsigned long long kb_s[16][MT];
             if (lane == 0) {
 #pragma unroll
                 for (int m = 0; m < MT; m++) kb_s[wave][m] = kbest[m];
@@ -441,7 +445,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
             if (tid < MT && tid < p.M) {
                 unsigned long long b = kb_s[0][tid];
 #pragma unroll
-                for (int w = 1; w < 4; w++) b = kb_s[w][tid] > b ? kb_s[w][tid] : b;
+                for (int w = 1; w < NWv; w++) b = kb_s[w][tid] > b ? kb_s[w][tid] : b;
                 if (b) atomicMax(p.keys + tid, b);
             }
         }
@@ -800,6 +804,14 @@ __global__ __launch_bounds__(256) void skinny_mfma_kernel(GemvParams p) {
     }
 }
 
+// block size bound of the one-block-per-CU GEMV variant (9 waves: Qwen2-7B QKV; O / down use 7)
+constexpr int kGemvBalancedThreads = 576;
+
+static int env_int_gemv(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v ? atoi(v) : dflt;
+}
+
 template <int MT, int RPW, int EPI, int XCH, int WT>
 static int launch_gemv_t(const GemvParams& p, hipStream_t st, int blocks_per_cu) {
     constexpr int U = (RPW >= 4) ? 4 : 8;
@@ -832,8 +844,37 @@ static int launch_gemv_t(const GemvParams& p, hipStream_t st, int blocks_per_cu)
         const int64_t rounds = (p.n_tasks + 4 * cap - 1) / (4 * cap);
         grid64 = std::max<int64_t>(1, (p.n_tasks + 4 * rounds - 1) / (4 * rounds));
     }
+    // One block per CU for mid-sized GEMVs (4..16 row tasks per CU: Qwen2-7B QKV 2,304, O and
+    // down 1,792): 448 four-wave blocks on 256 CUs left 64 CUs with half the waves, and the
+    // whole launch waited for the doubly loaded CUs.  Block = ceil(tasks / CUs) waves, so every
+    // CU streams the same rows.  (SwiGLU and lm_head have > 9 tasks per CU: grid-stride.)
+    int threads = 256;
+    const int64_t cus = device_cu_count();
+    if (MT == 1 && EPI != QIE_EPI_SWIGLU && blocks_per_cu > 0 && p.n_tasks > 4 * cus &&
+        p.n_tasks <= (kGemvBalancedThreads / 64) * cus &&
+        env_int_gemv("QIE_GEMV_BALANCED", 1) != 0) {
+        const int64_t nw = (p.n_tasks + cus - 1) / cus;
+        threads = (int)(64 * nw);
+        grid64 = (p.n_tasks + nw - 1) / nw;
+    }
     const unsigned grid = (unsigned)grid64;
-    hipLaunchKernelGGL((gemv_kernel<MT, RPW, EPI, U, XCH, WT>), dim3(grid), dim3(256), shm, st, p);
+    if (threads > 256) {
+        if constexpr (MT == 1 && EPI != QIE_EPI_SWIGLU) {
+            const void* fb = (const void*)gemv_kernel<MT, RPW, EPI, U, XCH, WT, kGemvBalancedThreads>;
+            if (shm > 65536) {
+                static bool raised_b = false;
+                if (!raised_b) {
+                    QIE_HIP(hipFuncSetAttribute(fb, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+                    raised_b = true;
+                }
+            }
+            hipLaunchKernelGGL((gemv_kernel<MT, RPW, EPI, U, XCH, WT, kGemvBalancedThreads>), dim3(grid), dim3(threads),
+                               shm, st, p);
+            QIE_LAUNCH_CHECK();
+            return 0;
+        }
+    }
+    hipLaunchKernelGGL((gemv_kernel<MT, RPW, EPI, U, XCH, WT>), dim3(grid), dim3(threads), shm, st, p);
     QIE_LAUNCH_CHECK();
     return 0;
 }

@@ -244,9 +244,14 @@ def test_attention_decode(oracle, qlib, hd, nq, nkv, ctxs):
         assert d.max() <= 2 ** -7 * max(1.0, np.abs(G.bf(want[0])).max()) * 2, f"ctx {ctxs[b]}: {d.max()}"
 
 
-@pytest.mark.parametrize("P", [1, 7, 64, 257])
-def test_attention_prefill_causal(oracle, qlib, P):
-    nq, nkv, hd, L, layer, maxc = 14, 2, 64, 1, 0, 512
+@pytest.mark.parametrize("P,hd", [(1, 64), (7, 64), (64, 64), (257, 64), (33, 128), (130, 128), (511, 128)])
+@pytest.mark.parametrize("v1", [False, True])
+def test_attention_prefill_causal(oracle, qlib, P, hd, v1, monkeypatch):
+    """Causal prefill attention (flash, MFMA) vs the oracle's self_attension.cu restatement;
+    v1 (64 rows per block, libm expf) is kept for A/B timing and checked the same way."""
+    if v1:
+        monkeypatch.setenv("QIE_ATTN_PREFILL_V1", "1")
+    nq, nkv, L, layer, maxc = 14, 2, 1, 0, 512
     seq_stride = L * nkv * maxc * hd
     kc_h = rand_bf16(oracle, (1, L, nkv, maxc, hd), seed=P)
     vc_h = rand_bf16(oracle, (1, L, nkv, maxc, hd), seed=P + 1)

@@ -595,6 +595,7 @@ struct PrefillAttnParams {
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef short i16x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int kv16_t __attribute__((ext_vector_type(4)));
 
 template <int HD>
 __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(PrefillAttnParams a) {
@@ -777,7 +778,7 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(PrefillAttnParam
 // expf and IEEE division of v1 (~25 VALU ops per score) bought nothing but VALU time.
 // A wave skips the MFMAs of a tile whose first key lies past its last row's position.
 template <int HD>
-__global__ __launch_bounds__(256) void attn_prefill_mfma2_kernel(PrefillAttnParams a) {
+__global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnParams a) {
     constexpr int KT = 64;
     constexpr int CPR = HD / 8;
     constexpr int KSTEPS = HD / 32;
@@ -789,6 +790,10 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma2_kernel(PrefillAttnPara
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint16_t* Ks = reinterpret_cast<uint16_t*>(smem);
     uint16_t* Vs = reinterpret_cast<uint16_t*>(smem + 2 * KT * HD * 2);
+    // V image chunk swizzle: the 16-B chunk c of key row r sits at c ^ vswz(r).  A
+    // ds_read_b64_tr_b16 half-wave reads 8 rows x 32 B at one column; unswizzled, the rows
+    // (a whole number of 256-B bank rows apart) hit the same banks: 8-way conflicts.
+    auto vswz = [](int r) { return 2 * (r & (CPR / 2 - 1)); };
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int fr = lane & 15, g = lane >> 4;
@@ -817,15 +822,17 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma2_kernel(PrefillAttnPara
         for (int ks = 0; ks < KSTEPS; ks++) qf[q][ks] = *reinterpret_cast<const bf16x8_t*>(qp + ks * 32 + g * 8);
     }
 
-    uint4 rk[LPT], rv[LPT];
+    // staging registers as native 4 x u32 vectors: HIP's union-based uint4 arrays were
+    // left in scratch (144 B/lane) by the compiler across the loop
+    kv16_t rk[LPT], rv[LPT];
     auto gload = [&](int kt) {
 #pragma unroll
         for (int i = 0; i < LPT; i++) {
             const int c = tid + 256 * i;
             const int key = min(kt * KT + c / CPR, kmax);
             const int ch = c % CPR;
-            rk[i] = *reinterpret_cast<const uint4*>(kb + (int64_t)key * HD + ch * 8);
-            rv[i] = *reinterpret_cast<const uint4*>(vb + (int64_t)key * HD + ch * 8);
+            rk[i] = *reinterpret_cast<const kv16_t*>(kb + (int64_t)key * HD + ch * 8);
+            rv[i] = *reinterpret_cast<const kv16_t*>(vb + (int64_t)key * HD + ch * 8);
         }
     };
     auto lstore = [&](int buf) {
@@ -833,8 +840,8 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma2_kernel(PrefillAttnPara
         for (int i = 0; i < LPT; i++) {
             const int c = tid + 256 * i;
             const int r = c / CPR, ch = c % CPR;
-            *reinterpret_cast<uint4*>(Ks + buf * KT * HD + r * HD + ((ch ^ (r & (CPR - 1))) * 8)) = rk[i];
-            *reinterpret_cast<uint4*>(Vs + buf * KT * HD + r * HD + ch * 8) = rv[i];
+            *reinterpret_cast<kv16_t*>(Ks + buf * KT * HD + r * HD + ((ch ^ (r & (CPR - 1))) * 8)) = rk[i];
+            *reinterpret_cast<kv16_t*>(Vs + buf * KT * HD + r * HD + ((ch ^ vswz(r)) * 8)) = rv[i];
         }
     };
 
@@ -924,7 +931,9 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma2_kernel(PrefillAttnPara
             for (int c = 0; c < 2; c++) {
 #pragma unroll
                 for (int d = 0; d < DT; d++) {
-                    const uint16_t* a0 = Vt + (32 * c + 4 * g + q4) * HD + 16 * d + 4 * p4;
+                    // rows vr and vr + 16 share vswz: one column offset serves both reads
+                    const int vr = 32 * c + 4 * g + q4;
+                    const uint16_t* a0 = Vt + vr * HD + (((2 * d + (p4 >> 1)) ^ vswz(vr)) * 8) + (p4 & 1) * 4;
                     const i16x4_t v0 =
                         __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4_t*)(a0));
                     const i16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(

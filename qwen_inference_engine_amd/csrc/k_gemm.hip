@@ -236,6 +236,197 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Large prefill GEMM (bf16 weights, K % 32 == 0, enough 256x256 tiles to fill the chip):
+// 256x256 block tile, 8 waves as 2 (M) x 4 (N), 128x64 per wave = 8x4 accumulators of
+// v_mfma_f32_16x16x32_bf16.  Both operands go global -> LDS by LDS-DMA
+// (global_load_lds_dwordx4: one wave-instruction = 16 rows x 64 B, the LDS image
+// lane-linear, the chunk swizzle applied to the SOURCE address) into a ring of four
+// 32-deep k-tiles (4 x 32 KB): three k-tiles stay in flight across the raw s_barrier that
+// opens each k-step and are retired by a counted vmcnt, never vmcnt(0) in the main loop
+// (cdna_hip_programming.md §5 'Pipelining across barriers', 'What does break it').  One
+// workgroup (2 waves per SIMD) per CU; the bijective XCD remap keeps the M tiles that
+// share a weight tile on one XCD, so each weight tile comes from HBM into one L2 once.
+namespace big {
+constexpr int BM = 256, BN = 256, BK = 32, SLOTS = 4;
+constexpr int SLOT_BYTES = (BM + BN) * BK * 2;   // 32 KB: A rows then B rows, 64 B each
+}  // namespace big
+
+// chunk swizzle of 64-B LDS rows: the 16-B chunk c of row r sits at position c ^ swz(r).
+// With it the 16 lanes of each ds_read_b128 lane group ({0-3,12-15,20-27}, ...) reading
+// rows fr (and chunk g) of a 16-row fragment land on 16 distinct bank slots.
+__device__ __forceinline__ int big_swz(int r) { return ((r >> 2) & 1) * 3; }
+
+__device__ __forceinline__ void glds16(const void* src, void* lds) {
+    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src),
+                                     (__attribute__((address_space(3))) void*)(lds), 16, 0, 0);
+}
+
+// weight row feeding tile column c (0..255) of column tile nt; SwiGLU tiles interleave
+// 32 gate rows and the 32 up rows of the same outputs per 64-column wave slice
+template <int EPI>
+__device__ __forceinline__ const uint16_t* big_wrow(const GemmParams& p, int64_t nt, int c) {
+    if constexpr (EPI == QIE_EPI_SWIGLU) {
+        const int64_t j = nt * 128 + 32 * (c >> 6) + (c & 31);
+        const int64_t jj = j < p.N ? j : p.N - 1;
+        return ((c >> 5) & 1 ? p.w1 : p.w0) + jj * p.K;
+    } else {
+        const int64_t r = nt * 256 + c;
+        const int64_t rr = r < p.N ? r : p.N - 1;
+        if (rr < p.n0) return p.w0 + rr * p.K;
+        if (rr < p.n01) return p.w1 + (rr - p.n0) * p.K;
+        return p.w2 + (rr - p.n01) * p.K;
+    }
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p, int n_mt) {
+#pragma clang fp contract(off)
+    constexpr int TM = big::BM, TK = big::BK, NSL = big::SLOTS, SB = big::SLOT_BYTES;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    const int fr = lane & 15, g = lane >> 4;
+    // bijective XCD remap (cdna_hip_programming.md §5 'XCD swizzle must be bijective')
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int q8 = nwg >> 3, r8 = nwg & 7, xcd = orig & 7;
+    const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+    const int64_t mt = wid % n_mt, nt = wid / n_mt;
+    const int64_t m0 = mt * TM;
+
+    // staging: wave-instruction i (0, 1) of this wave moves rows [32 wave + 16 i, +16) of the
+    // A tile and of the B tile; lane -> row (lane >> 2), LDS chunk (lane & 3)
+    const uint16_t* asrc[2];
+    const uint16_t* bsrc[2];
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+        const int r = 32 * wave + 16 * i + (lane >> 2);
+        const int c = (lane & 3) ^ big_swz(r);
+        int64_t ar = m0 + r;
+        ar = ar < p.M ? ar : p.M - 1;   // rows past M: re-read row M-1, never stored
+        asrc[i] = p.A + ar * p.lda + c * 8;
+        bsrc[i] = big_wrow<EPI>(p, nt, r) + c * 8;
+    }
+    const int nk = (int)(p.K / TK);
+    auto issue = [&](int kt) {
+        unsigned char* slot = smem + (kt & (NSL - 1)) * SB;
+        const int64_t k0 = (int64_t)kt * TK;
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            glds16(asrc[i] + k0, slot + (32 * wave + 16 * i) * (TK * 2));
+            glds16(bsrc[i] + k0, slot + TM * TK * 2 + (32 * wave + 16 * i) * (TK * 2));
+        }
+    };
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    issue(0);
+    if (nk > 1) issue(1);
+    if (nk > 2) issue(2);
+    for (int kt = 0; kt < nk; kt++) {
+        // this wave's DMAs of tile kt have landed once at most the later tiles' are pending
+        if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();            // ... and every other wave's; slot kt-1 is free
+        asm volatile("" ::: "memory");
+        if (kt + 3 < nk) issue(kt + 3);          // into the slot of tile kt - 1
+        const uint16_t* As = reinterpret_cast<const uint16_t*>(smem + (kt & (NSL - 1)) * SB);
+        const uint16_t* Bs = As + TM * TK;
+        bf16x8 af[8], bfr[4];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int row = wm * 128 + i * 16 + fr;
+            af[i] = *reinterpret_cast<const bf16x8*>(As + row * TK + ((g ^ big_swz(row)) * 8));
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int row = wn * 64 + j * 16 + fr;
+            bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + row * TK + ((g ^ big_swz(row)) * 8));
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+
+    // ---------------- epilogue.  C/D map: col = lane & 15, row = 4*(lane >> 4) + r.
+    if constexpr (EPI == QIE_EPI_SWIGLU) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+#pragma unroll
+            for (int jj = 0; jj < 2; jj++) {
+                const int64_t col = nt * 128 + 32 * wn + 16 * jj + fr;
+                if (col >= p.N) continue;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int64_t row = m0 + wm * 128 + i * 16 + g * 4 + r;
+                    if (row >= p.M) continue;
+                    const float gg = rbf(acc[i][jj][r]);
+                    const float uu = rbf(acc[i][jj + 2][r]);
+                    const float av = rbf(gg * (1.0f / (1.0f + expf(-gg))));
+                    p.C[row * p.ldc + col] = f2bf(uu * av);
+                }
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int64_t col = nt * 256 + wn * 64 + j * 16 + fr;
+            if (col >= p.N) continue;
+            float bias = 0.f;
+            if constexpr (EPI == QIE_EPI_STORE) {
+                const uint16_t* b = col < p.n0 ? p.b0 : (col < p.n01 ? p.b1 : p.b2);
+                if (b) bias = bf2f(b[col < p.n0 ? col : (col < p.n01 ? col - p.n0 : col - p.n01)]);
+            }
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int64_t row = m0 + wm * 128 + i * 16 + g * 4 + r;
+                    if (row >= p.M) continue;
+                    if constexpr (EPI == QIE_EPI_F32) {
+                        reinterpret_cast<float*>(p.C)[row * p.ldc + col] = acc[i][j][r];
+                        continue;
+                    }
+                    uint16_t* dst = p.C + row * p.ldc + col;
+                    if constexpr (EPI == QIE_EPI_RESIDUAL)
+                        *dst = f2bf(bf2f(*dst) + rbf(acc[i][j][r]));
+                    else
+                        *dst = f2bf(acc[i][j][r] + bias);
+                }
+            }
+        }
+    }
+}
+
+template <int EPI>
+static int launch_gemm_big_t(const GemmParams& p, int n_mt, int n_tiles, hipStream_t st) {
+    const void* fn = (const void*)gemm_big_kernel<EPI>;
+    static bool raised = false;
+    if (!raised) {
+        QIE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, big::SLOTS * big::SLOT_BYTES));
+        raised = true;
+    }
+    hipLaunchKernelGGL((gemm_big_kernel<EPI>), dim3((unsigned)n_tiles), dim3(512), big::SLOTS * big::SLOT_BYTES, st, p,
+                       n_mt);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+
+static int launch_gemm_big(int epi, const GemmParams& p, int n_mt, int n_tiles, hipStream_t st) {
+    if (epi == QIE_EPI_SWIGLU) return launch_gemm_big_t<QIE_EPI_SWIGLU>(p, n_mt, n_tiles, st);
+    if (epi == QIE_EPI_RESIDUAL) return launch_gemm_big_t<QIE_EPI_RESIDUAL>(p, n_mt, n_tiles, st);
+    if (epi == QIE_EPI_F32) return launch_gemm_big_t<QIE_EPI_F32>(p, n_mt, n_tiles, st);
+    return launch_gemm_big_t<QIE_EPI_STORE>(p, n_mt, n_tiles, st);
+}
+
 template <int WT>
 static int launch_gemm(int epi, unsigned gm, const GemmParams& p, size_t shm, hipStream_t st) {
     if (epi == QIE_EPI_SWIGLU) {
@@ -275,6 +466,16 @@ int gemm(const qie_linear_args* a, hipStream_t st) {
     const size_t shm = (size_t)2 * (BM + BN) * BK * 2;
     const unsigned gm = (unsigned)cdiv(a->M, BM);
     QIE_REQUIRE(a->K % 8 == 0, "qie_linear: GEMM needs K %% 8 == 0");
+    if (!(a->flags & QIE_LINEAR_FP8) && a->K % big::BK == 0 && a->ldx % 8 == 0) {
+        // 256x256 LDS-DMA kernel when its tiles fill the chip at least twice over (QIE_GEMM_BIG:
+        // 1 forces it, 0 disables it — tests and A/B timing)
+        const int64_t cols = a->epilogue == QIE_EPI_SWIGLU ? 2 * a->N : a->N;
+        const int64_t n_mt = cdiv(a->M, big::BM), n_nt = cdiv(cols, big::BN);
+        const char* ev = getenv("QIE_GEMM_BIG");
+        const int force = ev ? atoi(ev) : -1;
+        if (force == 1 || (force != 0 && a->M >= big::BM && n_mt * n_nt >= 2 * device_cu_count()))
+            return launch_gemm_big(a->epilogue, p, (int)n_mt, (int)(n_mt * n_nt), st);
+    }
     if (a->flags & QIE_LINEAR_FP8) return launch_gemm<1>(a->epilogue, gm, p, shm, st);
     return launch_gemm<0>(a->epilogue, gm, p, shm, st);
 }

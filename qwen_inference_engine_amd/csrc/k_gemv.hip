@@ -850,7 +850,7 @@ static int launch_gemv_t(const GemvParams& p, hipStream_t st, int blocks_per_cu)
     // CU streams the same rows.  (SwiGLU and lm_head have > 9 tasks per CU: grid-stride.)
     int threads = 256;
     const int64_t cus = device_cu_count();
-    if (MT == 1 && EPI != QIE_EPI_SWIGLU && blocks_per_cu > 0 && p.n_tasks > 4 * cus &&
+    if (MT == 1 && WT == 0 && EPI != QIE_EPI_SWIGLU && blocks_per_cu > 0 && p.n_tasks > 4 * cus &&
         p.n_tasks <= (kGemvBalancedThreads / 64) * cus &&
         env_int_gemv("QIE_GEMV_BALANCED", 1) != 0) {
         const int64_t nw = (p.n_tasks + cus - 1) / cus;
@@ -859,7 +859,7 @@ static int launch_gemv_t(const GemvParams& p, hipStream_t st, int blocks_per_cu)
     }
     const unsigned grid = (unsigned)grid64;
     if (threads > 256) {
-        if constexpr (MT == 1 && EPI != QIE_EPI_SWIGLU) {
+        if constexpr (MT == 1 && WT == 0 && EPI != QIE_EPI_SWIGLU) {
             const void* fb = (const void*)gemv_kernel<MT, RPW, EPI, U, XCH, WT, kGemvBalancedThreads>;
             if (shm > 65536) {
                 static bool raised_b = false;

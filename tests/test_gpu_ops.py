@@ -131,6 +131,57 @@ def test_linear_swiglu(oracle, qlib, M, K, I):
     assert not ((d > 2) & ~ill).any(), f"well-conditioned element off by {d[~ill].max()} ulps"
 
 
+@pytest.mark.parametrize("M,K", [(256, 896), (300, 96), (520, 32), (257, 3584)])
+@pytest.mark.parametrize("epi", ["store3", "residual", "swiglu", "f32"])
+def test_linear_big_gemm(oracle, qlib, M, K, epi, monkeypatch):
+    """The 256x256 LDS-DMA prefill GEMM (forced with QIE_GEMM_BIG=1 at test sizes; the
+    engine picks it when its tiles fill the chip twice): every epilogue, ragged M and N
+    (clamped rows never stored), K of 1, 3 and 28+ k-tiles (ring prologue / drain)."""
+    monkeypatch.setenv("QIE_GEMM_BIG", "1")
+    x = rand_bf16(oracle, (M, K), seed=M + K)
+    if epi == "store3":
+        n = (200, 72, 40)
+        ws = [rand_bf16(oracle, (r, K), 0.05, seed=30 + i) for i, r in enumerate(n)]
+        bs = [rand_bf16(oracle, (r,), 0.1, seed=40 + i) for i, r in enumerate(n)]
+        N = sum(n)
+        want = np.concatenate([oracle.matmul(x, w, b) for w, b in zip(ws, bs)], axis=1)
+        y = G.zeros_bf16(M, N)
+        _linear(qlib, G.dev(x), [(G.dev(w), r) for w, r in zip(ws, n)], [G.dev(b) for b in bs], M, K, N, y,
+                _lib.QIE_EPI_STORE)
+        scale = np.concatenate([_abs_scale(oracle, x, w) for w in ws], axis=1)
+        G.assert_sum_close(G.host_bf16(y), want, scale, what=f"big store M={M} K={K}")
+    elif epi == "residual":
+        N = 320
+        w = rand_bf16(oracle, (N, K), 0.02, seed=4)
+        res = rand_bf16(oracle, (M, N), seed=5)
+        want = oracle.resadd(res, oracle.matmul(x, w))
+        y = G.dev(res)
+        _linear(qlib, G.dev(x), [(G.dev(w), N)], [], M, K, N, y, _lib.QIE_EPI_RESIDUAL)
+        acc = G.bf(oracle.matmul(x, w)).astype(np.float64)
+        tol = 2.0 ** -7 * (np.abs(acc) + np.abs(G.bf(want))) + 1e-5 * _abs_scale(oracle, x, w)
+        assert (np.abs(G.bf(G.host_bf16(y)).astype(np.float64) - G.bf(want)) <= tol).all()
+    elif epi == "swiglu":
+        I = 200
+        wg = rand_bf16(oracle, (I, K), 0.08, seed=7)
+        wu = rand_bf16(oracle, (I, K), 0.08, seed=8)
+        want = oracle.silu_mul(oracle.matmul(x, wg), oracle.matmul(x, wu))
+        y = G.zeros_bf16(M, I)
+        _linear(qlib, G.dev(x), [(G.dev(wg), I), (G.dev(wu), I)], [], M, K, I, y, _lib.QIE_EPI_SWIGLU)
+        got = G.host_bf16(y)
+        d = G.ulp_diff(got, want)
+        gs = G.bf(oracle.matmul(x, wg)).astype(np.float64)
+        u = np.abs(G.bf(oracle.matmul(x, wu)).astype(np.float64))
+        ill = (np.abs(gs) < 1e-2 * _abs_scale(oracle, x, wg)) | (u < 1e-2 * _abs_scale(oracle, x, wu)) | (gs < -4)
+        assert (d == 0).mean() > 0.97 and not ((d > 2) & ~ill).any()
+    else:
+        N = 264
+        w = rand_bf16(oracle, (N, K), 0.05, seed=9)
+        y = G.zeros((M, N), np.float32)
+        _linear(qlib, G.dev(x), [(G.dev(w), N)], [], M, K, N, y, _lib.QIE_EPI_F32)
+        want = oracle.bf16_to_f32(x).astype(np.float64) @ oracle.bf16_to_f32(w).astype(np.float64).T
+        assert np.abs(G.host(y) - want).max() <= 1e-5 * _abs_scale(oracle, x, w).max() + 1e-6
+
+
 @pytest.mark.parametrize("M", [1, 3, 8])
 @pytest.mark.parametrize("num", ["ref", "hf"])
 def test_linear_fused_norm_and_argmax(oracle, qlib, M, num):

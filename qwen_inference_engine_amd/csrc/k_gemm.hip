@@ -248,8 +248,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
 // workgroup (2 waves per SIMD) per CU; the bijective XCD remap keeps the M tiles that
 // share a weight tile on one XCD, so each weight tile comes from HBM into one L2 once.
 namespace big {
-constexpr int BM = 256, BN = 256, BK = 32, SLOTS = 4;
-constexpr int SLOT_BYTES = (BM + BN) * BK * 2;   // 32 KB: A rows then B rows, 64 B each
+constexpr int BM = 256, BK = 32, SLOTS = 4;
+// slot = A rows then B rows, 64 B each: 32 KB at BN 256, 24 KB at BN 128
+constexpr int slot_bytes(int bn) { return (BM + bn) * BK * 2; }
 }  // namespace big
 
 // chunk swizzle of 64-B LDS rows: the 16-B chunk c of row r sits at position c ^ swz(r).
@@ -264,14 +265,16 @@ __device__ __forceinline__ void glds16(const void* src, void* lds) {
 
 // weight row feeding tile column c (0..255) of column tile nt; SwiGLU tiles interleave
 // 32 gate rows and the 32 up rows of the same outputs per 64-column wave slice
-template <int EPI>
+template <int EPI, int BNT>
 __device__ __forceinline__ const uint16_t* big_wrow(const GemmParams& p, int64_t nt, int c) {
     if constexpr (EPI == QIE_EPI_SWIGLU) {
-        const int64_t j = nt * 128 + 32 * (c >> 6) + (c & 31);
+        constexpr int HALF = BNT / 8;   // gate (then up) rows per 1/4-tile wave slice
+        const int ws = c / (BNT / 4), q = c % (BNT / 4);
+        const int64_t j = nt * (BNT / 2) + ws * HALF + (q % HALF);
         const int64_t jj = j < p.N ? j : p.N - 1;
-        return ((c >> 5) & 1 ? p.w1 : p.w0) + jj * p.K;
+        return (q >= HALF ? p.w1 : p.w0) + jj * p.K;
     } else {
-        const int64_t r = nt * 256 + c;
+        const int64_t r = nt * BNT + c;
         const int64_t rr = r < p.N ? r : p.N - 1;
         if (rr < p.n0) return p.w0 + rr * p.K;
         if (rr < p.n01) return p.w1 + (rr - p.n0) * p.K;
@@ -279,10 +282,13 @@ __device__ __forceinline__ const uint16_t* big_wrow(const GemmParams& p, int64_t
     }
 }
 
-template <int EPI>
+template <int EPI, int BNT>
 __global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p, int n_mt) {
 #pragma clang fp contract(off)
-    constexpr int TM = big::BM, TK = big::BK, NSL = big::SLOTS, SB = big::SLOT_BYTES;
+    constexpr int TM = big::BM, TK = big::BK, NSL = big::SLOTS, SB = big::slot_bytes(BNT);
+    constexpr int NJ = BNT / 64;            // 16-column fragments per wave (4 waves along N)
+    constexpr int NBI = BNT / 128;          // B wave-instructions per k-tile per wave
+    constexpr int LPK = 2 + NBI;            // LDS-DMA instructions per k-tile per wave
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -298,7 +304,7 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p, int n_mt) {
     // staging: wave-instruction i (0, 1) of this wave moves rows [32 wave + 16 i, +16) of the
     // A tile and of the B tile; lane -> row (lane >> 2), LDS chunk (lane & 3)
     const uint16_t* asrc[2];
-    const uint16_t* bsrc[2];
+    const uint16_t* bsrc[NBI];
 #pragma unroll
     for (int i = 0; i < 2; i++) {
         const int r = 32 * wave + 16 * i + (lane >> 2);
@@ -306,53 +312,63 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p, int n_mt) {
         int64_t ar = m0 + r;
         ar = ar < p.M ? ar : p.M - 1;   // rows past M: re-read row M-1, never stored
         asrc[i] = p.A + ar * p.lda + c * 8;
-        bsrc[i] = big_wrow<EPI>(p, nt, r) + c * 8;
+    }
+#pragma unroll
+    for (int i = 0; i < NBI; i++) {
+        const int r = 16 * NBI * wave + 16 * i + (lane >> 2);
+        const int c = (lane & 3) ^ big_swz(r);
+        bsrc[i] = big_wrow<EPI, BNT>(p, nt, r) + c * 8;
     }
     const int nk = (int)(p.K / TK);
     auto issue = [&](int kt) {
         unsigned char* slot = smem + (kt & (NSL - 1)) * SB;
         const int64_t k0 = (int64_t)kt * TK;
 #pragma unroll
-        for (int i = 0; i < 2; i++) {
-            glds16(asrc[i] + k0, slot + (32 * wave + 16 * i) * (TK * 2));
-            glds16(bsrc[i] + k0, slot + TM * TK * 2 + (32 * wave + 16 * i) * (TK * 2));
-        }
+        for (int i = 0; i < 2; i++) glds16(asrc[i] + k0, slot + (32 * wave + 16 * i) * (TK * 2));
+#pragma unroll
+        for (int i = 0; i < NBI; i++) glds16(bsrc[i] + k0, slot + TM * TK * 2 + (16 * NBI * wave + 16 * i) * (TK * 2));
     };
 
-    f32x4 acc[8][4];
+    f32x4 acc[8][NJ];
 #pragma unroll
     for (int i = 0; i < 8; i++)
 #pragma unroll
-        for (int j = 0; j < 4; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < NJ; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     issue(0);
     if (nk > 1) issue(1);
     if (nk > 2) issue(2);
     for (int kt = 0; kt < nk; kt++) {
         // this wave's DMAs of tile kt have landed once at most the later tiles' are pending
-        if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (kt + 2 < nk) {
+            if constexpr (LPK == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        } else if (kt + 1 < nk) {
+            if constexpr (LPK == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         __builtin_amdgcn_s_barrier();            // ... and every other wave's; slot kt-1 is free
         asm volatile("" ::: "memory");
         if (kt + 3 < nk) issue(kt + 3);          // into the slot of tile kt - 1
         const uint16_t* As = reinterpret_cast<const uint16_t*>(smem + (kt & (NSL - 1)) * SB);
         const uint16_t* Bs = As + TM * TK;
-        bf16x8 af[8], bfr[4];
+        bf16x8 af[8], bfr[NJ];
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const int row = wm * 128 + i * 16 + fr;
             af[i] = *reinterpret_cast<const bf16x8*>(As + row * TK + ((g ^ big_swz(row)) * 8));
         }
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int row = wn * 64 + j * 16 + fr;
+        for (int j = 0; j < NJ; j++) {
+            const int row = wn * (BNT / 4) + j * 16 + fr;
             bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + row * TK + ((g ^ big_swz(row)) * 8));
         }
 #pragma unroll
         for (int i = 0; i < 8; i++)
 #pragma unroll
-            for (int j = 0; j < 4; j++)
+            for (int j = 0; j < NJ; j++)
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
 
@@ -361,15 +377,15 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p, int n_mt) {
 #pragma unroll
         for (int i = 0; i < 8; i++) {
 #pragma unroll
-            for (int jj = 0; jj < 2; jj++) {
-                const int64_t col = nt * 128 + 32 * wn + 16 * jj + fr;
+            for (int jj = 0; jj < NJ / 2; jj++) {
+                const int64_t col = nt * (BNT / 2) + (BNT / 8) * wn + 16 * jj + fr;
                 if (col >= p.N) continue;
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
                     const int64_t row = m0 + wm * 128 + i * 16 + g * 4 + r;
                     if (row >= p.M) continue;
                     const float gg = rbf(acc[i][jj][r]);
-                    const float uu = rbf(acc[i][jj + 2][r]);
+                    const float uu = rbf(acc[i][jj + NJ / 2][r]);
                     const float av = rbf(gg * (1.0f / (1.0f + expf(-gg))));
                     p.C[row * p.ldc + col] = f2bf(uu * av);
                 }
@@ -377,8 +393,8 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p, int n_mt) {
         }
     } else {
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int64_t col = nt * 256 + wn * 64 + j * 16 + fr;
+        for (int j = 0; j < NJ; j++) {
+            const int64_t col = nt * BNT + wn * (BNT / 4) + j * 16 + fr;
             if (col >= p.N) continue;
             float bias = 0.f;
             if constexpr (EPI == QIE_EPI_STORE) {
@@ -406,25 +422,26 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p, int n_mt) {
     }
 }
 
-template <int EPI>
+template <int EPI, int BNT>
 static int launch_gemm_big_t(const GemmParams& p, int n_mt, int n_tiles, hipStream_t st) {
-    const void* fn = (const void*)gemm_big_kernel<EPI>;
+    const void* fn = (const void*)gemm_big_kernel<EPI, BNT>;
+    constexpr size_t shm = (size_t)big::SLOTS * big::slot_bytes(BNT);
     static bool raised = false;
     if (!raised) {
-        QIE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, big::SLOTS * big::SLOT_BYTES));
+        QIE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
         raised = true;
     }
-    hipLaunchKernelGGL((gemm_big_kernel<EPI>), dim3((unsigned)n_tiles), dim3(512), big::SLOTS * big::SLOT_BYTES, st, p,
-                       n_mt);
+    hipLaunchKernelGGL((gemm_big_kernel<EPI, BNT>), dim3((unsigned)n_tiles), dim3(512), shm, st, p, n_mt);
     QIE_LAUNCH_CHECK();
     return 0;
 }
 
+template <int BNT>
 static int launch_gemm_big(int epi, const GemmParams& p, int n_mt, int n_tiles, hipStream_t st) {
-    if (epi == QIE_EPI_SWIGLU) return launch_gemm_big_t<QIE_EPI_SWIGLU>(p, n_mt, n_tiles, st);
-    if (epi == QIE_EPI_RESIDUAL) return launch_gemm_big_t<QIE_EPI_RESIDUAL>(p, n_mt, n_tiles, st);
-    if (epi == QIE_EPI_F32) return launch_gemm_big_t<QIE_EPI_F32>(p, n_mt, n_tiles, st);
-    return launch_gemm_big_t<QIE_EPI_STORE>(p, n_mt, n_tiles, st);
+    if (epi == QIE_EPI_SWIGLU) return launch_gemm_big_t<QIE_EPI_SWIGLU, BNT>(p, n_mt, n_tiles, st);
+    if (epi == QIE_EPI_RESIDUAL) return launch_gemm_big_t<QIE_EPI_RESIDUAL, BNT>(p, n_mt, n_tiles, st);
+    if (epi == QIE_EPI_F32) return launch_gemm_big_t<QIE_EPI_F32, BNT>(p, n_mt, n_tiles, st);
+    return launch_gemm_big_t<QIE_EPI_STORE, BNT>(p, n_mt, n_tiles, st);
 }
 
 template <int WT>
@@ -467,14 +484,20 @@ int gemm(const qie_linear_args* a, hipStream_t st) {
     const unsigned gm = (unsigned)cdiv(a->M, BM);
     QIE_REQUIRE(a->K % 8 == 0, "qie_linear: GEMM needs K %% 8 == 0");
     if (!(a->flags & QIE_LINEAR_FP8) && a->K % big::BK == 0 && a->ldx % 8 == 0) {
-        // 256x256 LDS-DMA kernel when its tiles fill the chip at least twice over (QIE_GEMM_BIG:
-        // 1 forces it, 0 disables it — tests and A/B timing)
+        // LDS-DMA kernel: 256x256 tiles when they fill the chip at least twice over, else
+        // 256x128 when those fill >= 3/4 of it in one round (Qwen2-7B O and down projections
+        // at 2,048 rows: 112 vs 224 tiles on 256 CUs).  QIE_GEMM_BIG: 1 / 2 force the
+        // 256 / 128-column tile, 0 disables the kernel (tests and A/B timing).
         const int64_t cols = a->epilogue == QIE_EPI_SWIGLU ? 2 * a->N : a->N;
-        const int64_t n_mt = cdiv(a->M, big::BM), n_nt = cdiv(cols, big::BN);
+        const int64_t n_mt = cdiv(a->M, big::BM);
+        const int64_t t256 = n_mt * cdiv(cols, 256), t128 = n_mt * cdiv(cols, 128);
+        const int64_t cus = device_cu_count();
         const char* ev = getenv("QIE_GEMM_BIG");
         const int force = ev ? atoi(ev) : -1;
-        if (force == 1 || (force != 0 && a->M >= big::BM && n_mt * n_nt >= 2 * device_cu_count()))
-            return launch_gemm_big(a->epilogue, p, (int)n_mt, (int)(n_mt * n_nt), st);
+        if (force == 1 || (force < 0 && a->M >= big::BM && t256 >= 2 * cus))
+            return launch_gemm_big<256>(a->epilogue, p, (int)n_mt, (int)t256, st);
+        if (force == 2 || (force < 0 && a->M >= big::BM && t128 >= (3 * cus) / 4 && t128 <= cus))
+            return launch_gemm_big<128>(a->epilogue, p, (int)n_mt, (int)t128, st);
     }
     if (a->flags & QIE_LINEAR_FP8) return launch_gemm<1>(a->epilogue, gm, p, shm, st);
     return launch_gemm<0>(a->epilogue, gm, p, shm, st);

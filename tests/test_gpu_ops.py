@@ -133,11 +133,12 @@ def test_linear_swiglu(oracle, qlib, M, K, I):
 
 @pytest.mark.parametrize("M,K", [(256, 896), (300, 96), (520, 32), (257, 3584)])
 @pytest.mark.parametrize("epi", ["store3", "residual", "swiglu", "f32"])
-def test_linear_big_gemm(oracle, qlib, M, K, epi, monkeypatch):
-    """The 256x256 LDS-DMA prefill GEMM (forced with QIE_GEMM_BIG=1 at test sizes; the
-    engine picks it when its tiles fill the chip twice): every epilogue, ragged M and N
+@pytest.mark.parametrize("tile", ["1", "2"])
+def test_linear_big_gemm(oracle, qlib, M, K, epi, tile, monkeypatch):
+    """The LDS-DMA prefill GEMM, 256x256 (QIE_GEMM_BIG=1) and 256x128 (=2) tiles, forced at
+    test sizes (the engine picks them by tile count): every epilogue, ragged M and N
     (clamped rows never stored), K of 1, 3 and 28+ k-tiles (ring prologue / drain)."""
-    monkeypatch.setenv("QIE_GEMM_BIG", "1")
+    monkeypatch.setenv("QIE_GEMM_BIG", tile)
     x = rand_bf16(oracle, (M, K), seed=M + K)
     if epi == "store3":
         n = (200, 72, 40)

@@ -1439,7 +1439,6 @@ __global__ __launch_bounds__(256) void attn_decode_mfma2_kernel(DecodeAttnParams
     __shared__ __attribute__((aligned(16))) uint16_t kv_new[2][HD];
     __shared__ __attribute__((aligned(16))) uint16_t v_s[4][kDecMStep * DW];
     __shared__ __attribute__((aligned(16))) float s_s[16][kDecMStep + 4];
-    __shared__ float cw[kMaxGroup][kDecMaxSplits];
     __shared__ int last_flag;
 
     const int64_t m = blockIdx.y;
@@ -1649,67 +1648,48 @@ __global__ __launch_bounds__(256) void attn_decode_mfma2_kernel(DecodeAttnParams
     if (tid == 0 && !(a.dbg & 4)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    // each (head, d4) item issues its first 16 partial loads together with the m / l loads
+    // Per-thread online combine: thread (head gi, d4) loads the (m, l) of EVERY split of its
+    // head together with its 16-byte slice of every split's partial O (one batch of JB
+    // splits = one round trip; ctx <= JB * 128 keys in one), then merges them itself — no
+    // per-head wave pass, LDS weight table or barrier between the two load rounds.
+    constexpr int JB = 24;
     const bool has_item = tid < G * (HD / 4);
     const int gi = has_item ? tid / (HD / 4) : 0, d4 = tid % (HD / 4);
-    const float4* src4 =
-        reinterpret_cast<const float4*>(a.part_o) + ((m * nq + g * G + gi) * (int64_t)a.nsplit_max) * (HD / 4) + d4;
-    float4 v[16];
-#pragma unroll
-    for (int jj = 0; jj < 16; jj++) v[jj] = src4[(int64_t)min(jj, nsplit - 1) * (HD / 4)];
-    __builtin_amdgcn_sched_barrier(0);
-    for (int gh = wave; gh < G; gh += 4) {   // cw[h][j] = exp(m_j - M) / sum_j l_j exp(m_j - M)
-        const int64_t base = (m * nq + g * G + gh) * (int64_t)a.nsplit_max;
-        float mm = -INFINITY;
-        float ml[2][2];   // (m, l) of splits lane and lane + 64: one 8-B load each, no 2nd round trip
-#pragma unroll
-        for (int q = 0; q < 2; q++) {
-            const int j = lane + 64 * q;
-            const float2 v2 = j < nsplit ? *reinterpret_cast<const float2*>(&a.part_ml[(base + j) * 2])
-                                         : make_float2(-INFINITY, 0.f);
-            ml[q][0] = v2.x;
-            ml[q][1] = v2.y;
-            mm = fmaxf(mm, v2.x);
-        }
-        for (int j = lane + 128; j < nsplit; j += 64) mm = fmaxf(mm, a.part_ml[(base + j) * 2]);
-        mm = wave_max(mm);
-        float lv = 0.f;
-#pragma unroll
-        for (int q = 0; q < 2; q++) {
-            const int j = lane + 64 * q;
-            if (j >= nsplit) continue;
-            const float c = __expf(ml[q][0] - mm);
-            cw[gh][j] = c;
-            lv += ml[q][1] * c;
-        }
-        for (int j = lane + 128; j < nsplit; j += 64) {
-            const float c = __expf(a.part_ml[(base + j) * 2] - mm);
-            cw[gh][j] = c;
-            lv += a.part_ml[(base + j) * 2 + 1] * c;
-        }
-        lv = wave_sum(lv);
-        const float inv = 1.0f / lv;
-        for (int j = lane; j < nsplit; j += 64) cw[gh][j] *= inv;
-    }
-    __syncthreads();
+    const int64_t hbase = (m * nq + g * G + gi) * (int64_t)a.nsplit_max;
+    const float4* src4 = reinterpret_cast<const float4*>(a.part_o) + hbase * (HD / 4) + d4;
+    const float2* ml2 = reinterpret_cast<const float2*>(a.part_ml) + hbase;
+    float mx = -INFINITY, ls = 0.f;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int j0 = 0; j0 < nsplit; j0 += 16) {
-        if (j0 > 0) {
+    for (int j0 = 0; j0 < nsplit; j0 += JB) {
+        float4 v[JB];
+        float2 w[JB];
 #pragma unroll
-            for (int jj = 0; jj < 16; jj++) v[jj] = src4[(int64_t)min(j0 + jj, nsplit - 1) * (HD / 4)];
+        for (int jj = 0; jj < JB; jj++) {
+            const int j = min(j0 + jj, nsplit - 1);
+            v[jj] = src4[(int64_t)j * (HD / 4)];
+            w[jj] = ml2[j];
         }
+        float mb = mx;
 #pragma unroll
-        for (int jj = 0; jj < 16; jj++) {
-            const float c = j0 + jj < nsplit ? cw[gi][j0 + jj] : 0.f;
+        for (int jj = 0; jj < JB; jj++) mb = fmaxf(mb, j0 + jj < nsplit ? w[jj].x : -INFINITY);
+        const float sc = __expf(mx - mb);   // 0 on the first batch (mx = -inf, mb finite)
+        ls *= sc;
+        acc.x *= sc; acc.y *= sc; acc.z *= sc; acc.w *= sc;
+#pragma unroll
+        for (int jj = 0; jj < JB; jj++) {
+            const float c = j0 + jj < nsplit ? __expf(w[jj].x - mb) : 0.f;
+            ls = fmaf(w[jj].y, c, ls);
             acc.x = fmaf(c, v[jj].x, acc.x);
             acc.y = fmaf(c, v[jj].y, acc.y);
             acc.z = fmaf(c, v[jj].z, acc.z);
             acc.w = fmaf(c, v[jj].w, acc.w);
         }
+        mx = mb;
     }
     if (has_item) {
+        const float inv = 1.0f / ls;
         uint16_t* dst = a.out + m * (int64_t)nq * HD + (int64_t)(g * G + gi) * HD + d4 * 4;
-        *reinterpret_cast<uint2*>(dst) = make_uint2(pack2(acc.x, acc.y), pack2(acc.z, acc.w));
+        *reinterpret_cast<uint2*>(dst) = make_uint2(pack2(acc.x * inv, acc.y * inv), pack2(acc.z * inv, acc.w * inv));
     }
     if (tid == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

@@ -23,15 +23,20 @@ def main():
     ids = np.random.default_rng(1).integers(0, spec.vocab, P)
     b.prefill(0, ids)
     b.decode(256, want_ids=False)          # ctx ~2300
-    variants = [("attn", 5, {}), ("attn", 5, {"QIE_DEC_VALU": "1"}), ("attn", 5, {"QIE_DEC_MFMA1": "1"})]
-    for sp in ("16", "24", "48"):
-        variants.append(("attn", 5, {"QIE_DEC_SPLITS": sp}))
-    variants += [("attn", 5, {"QIE_DEC_DBG": d}) for d in ("1", "6", "8", "16", "64")]
-    for which in (0, 1, 2, 3, 4):
-        variants.append((NAMES[which], which, {}))
-        variants.append((NAMES[which], which, {"QIE_GEMV_XFIRST": "0"}))
-        for bpc in ("0", "16"):
-            variants.append((NAMES[which], which, {"QIE_GEMV_BLOCKS_PER_CU": bpc}))
+    sets = os.environ.get("UB_SET", "attn,gemv").split(",")
+    variants = []
+    if "attn" in sets:
+        variants += [("attn", 5, {}), ("attn", 5, {"QIE_DEC_MFMA1": "1"})]
+        for sp in ("8", "16", "24", "48"):
+            variants.append(("attn", 5, {"QIE_DEC_SPLITS": sp}))
+        variants += [("attn", 5, {"QIE_DEC_DBG": d}) for d in ("1", "6", "8", "16", "64")]
+    if "gemv" in sets:
+        for which in (0, 1, 2, 3, 4):
+            variants.append((NAMES[which], which, {}))
+            variants.append((NAMES[which], which, {"QIE_GEMV_BALANCED": "0"}))
+            variants.append((NAMES[which], which, {"QIE_GEMV_XFIRST": "0"}))
+            for bpc in ("0", "16"):
+                variants.append((NAMES[which], which, {"QIE_GEMV_BLOCKS_PER_CU": bpc}))
     res = {}
     for rnd in range(3):
         for name, which, env in variants:

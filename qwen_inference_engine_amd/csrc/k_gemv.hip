@@ -482,90 +482,6 @@ __global__ __launch_bounds__(256) void skinny_mfma_kernel(GemvParams p) {
     const int fr = lane & 15, g = lane >> 4;
     const int arow = fr < M ? fr : M - 1;   // A row of this lane (rows >= M: garbage, never stored)
 
-    // ---------------- prologue: the M activation rows -> LDS (optionally RMS-normed)
-    if (XL) {
-        if (p.norm_w) {
-            // pass 1: every row's sum of squares at once (loads of all rows in flight,
-            // clamped rows past M), ONE exchange — not a barrier pair per row
-            float ss[16];
-#pragma unroll
-            for (int m = 0; m < 16; m++) ss[m] = 0.f;
-            for (int64_t k = tid * 8; k < K; k += 2048) {
-                uint4 v[16];
-#pragma unroll
-                for (int m = 0; m < 16; m++)
-                    v[m] = *reinterpret_cast<const uint4*>(p.x + (int64_t)(m < M ? m : M - 1) * p.ldx + k);
-#pragma unroll
-                for (int m = 0; m < 16; m++) {
-                    if (m >= M) continue;   // uniform, ALU only (the loads are above)
-                    float f[8];
-                    unpack8(u32x4{v[m].x, v[m].y, v[m].z, v[m].w}, f);
-#pragma unroll
-                    for (int j = 0; j < 8; j++) ss[m] += f[j] * f[j];
-                }
-            }
-#pragma unroll
-            for (int m = 0; m < 16; m++) {
-                if (m >= M) continue;
-                const float t = wave_sum(ss[m]);
-                if (lane == 0) red[wave * 16 + m] = t;
-            }
-            __syncthreads();
-            const bool hf = p.numerics == QIE_NUMERICS_HF;
-            float rms[16], inv[16];
-#pragma unroll
-            for (int m = 0; m < 16; m++) {
-                const int mm = m < M ? m : 0;
-                const float sm = red[mm] + red[16 + mm] + red[32 + mm] + red[48 + mm];
-                rms[m] = sqrtf((sm / (float)K) + p.eps);
-                inv[m] = 1.0f / rms[m];
-            }
-            // pass 2: all rows of a chunk at once (loads unconditional and clamped; the
-            // per-row math under uniform branches).  REF's f / rms uses the FMA-corrected
-            // quotient (Markstein): correctly rounded, i.e. equal to the division, for
-            // normal operands — |f| outside [1e-30, 1e30] takes the real division.
-            for (int64_t k = tid * 8; k < K; k += 2048) {
-                const uint4 nw = *reinterpret_cast<const uint4*>(p.norm_w + k);
-                uint4 v[16];
-#pragma unroll
-                for (int m = 0; m < 16; m++)
-                    v[m] = *reinterpret_cast<const uint4*>(p.x + (int64_t)(m < M ? m : M - 1) * p.ldx + k);
-                float wf[8];
-                unpack8(u32x4{nw.x, nw.y, nw.z, nw.w}, wf);
-#pragma unroll
-                for (int m = 0; m < 16; m++) {
-                    if (m >= M) continue;
-                    float f[8];
-                    unpack8(u32x4{v[m].x, v[m].y, v[m].z, v[m].w}, f);
-                    uint32_t o[4];
-                    if (hf) {
-#pragma unroll
-                        for (int j = 0; j < 4; j++)
-                            o[j] = pack2(wf[2 * j] * rbf(f[2 * j] * inv[m]), wf[2 * j + 1] * rbf(f[2 * j + 1] * inv[m]));
-                    } else {
-                        float y[8];
-#pragma unroll
-                        for (int j = 0; j < 8; j++) {
-                            const float q = f[j] * inv[m];
-                            float d = fmaf(fmaf(-q, rms[m], f[j]), inv[m], q);
-                            const float af = fabsf(f[j]);
-                            if (af != 0.f && (af < 1e-30f || af > 1e30f)) d = f[j] / rms[m];
-                            y[j] = d * wf[j];
-                        }
-#pragma unroll
-                        for (int j = 0; j < 4; j++) o[j] = pack2(y[2 * j], y[2 * j + 1]);
-                    }
-                    *reinterpret_cast<uint4*>(xs + (int64_t)m * KP + k) = make_uint4(o[0], o[1], o[2], o[3]);
-                }
-            }
-        } else {
-            for (int m = 0; m < M; m++)
-                for (int64_t k = tid * 8; k < K; k += 2048)
-                    *reinterpret_cast<uint4*>(xs + (int64_t)m * KP + k) =
-                        *reinterpret_cast<const uint4*>(p.x + (int64_t)m * p.ldx + k);
-        }
-        __syncthreads();
-    }
     auto xa = [&](int64_t k) -> uint4 {   // 8 activations of this lane's A row at k
         return XL ? *reinterpret_cast<const uint4*>(xs + (int64_t)arow * KP + k)
                   : *reinterpret_cast<const uint4*>(p.x + (int64_t)arow * p.ldx + k);
@@ -769,6 +685,92 @@ __global__ __launch_bounds__(256) void skinny_mfma_kernel(GemvParams p) {
     // join); the last one or two steps are peeled so nothing past step S - 1 is fetched
     Step sa, sb;
     issue(sa, 0);
+    // ---------------- prologue: the M activation rows -> LDS (optionally RMS-normed).  It runs
+    // AFTER the first step's weight loads are issued (weights do not depend on x), so the
+    // weight stream's first HBM round trip overlaps the prologue's loads and reductions.
+    if (XL) {
+        if (p.norm_w) {
+            // pass 1: every row's sum of squares at once (loads of all rows in flight,
+            // clamped rows past M), ONE exchange — not a barrier pair per row
+            float ss[16];
+#pragma unroll
+            for (int m = 0; m < 16; m++) ss[m] = 0.f;
+            for (int64_t k = tid * 8; k < K; k += 2048) {
+                uint4 v[16];
+#pragma unroll
+                for (int m = 0; m < 16; m++)
+                    v[m] = *reinterpret_cast<const uint4*>(p.x + (int64_t)(m < M ? m : M - 1) * p.ldx + k);
+#pragma unroll
+                for (int m = 0; m < 16; m++) {
+                    if (m >= M) continue;   // uniform, ALU only (the loads are above)
+                    float f[8];
+                    unpack8(u32x4{v[m].x, v[m].y, v[m].z, v[m].w}, f);
+#pragma unroll
+                    for (int j = 0; j < 8; j++) ss[m] += f[j] * f[j];
+                }
+            }
+#pragma unroll
+            for (int m = 0; m < 16; m++) {
+                if (m >= M) continue;
+                const float t = wave_sum(ss[m]);
+                if (lane == 0) red[wave * 16 + m] = t;
+            }
+            __syncthreads();
+            const bool hf = p.numerics == QIE_NUMERICS_HF;
+            float rms[16], inv[16];
+#pragma unroll
+            for (int m = 0; m < 16; m++) {
+                const int mm = m < M ? m : 0;
+                const float sm = red[mm] + red[16 + mm] + red[32 + mm] + red[48 + mm];
+                rms[m] = sqrtf((sm / (float)K) + p.eps);
+                inv[m] = 1.0f / rms[m];
+            }
+            // pass 2: all rows of a chunk at once (loads unconditional and clamped; the
+            // per-row math under uniform branches).  REF's f / rms uses the FMA-corrected
+            // quotient (Markstein): correctly rounded, i.e. equal to the division, for
+            // normal operands — |f| outside [1e-30, 1e30] takes the real division.
+            for (int64_t k = tid * 8; k < K; k += 2048) {
+                const uint4 nw = *reinterpret_cast<const uint4*>(p.norm_w + k);
+                uint4 v[16];
+#pragma unroll
+                for (int m = 0; m < 16; m++)
+                    v[m] = *reinterpret_cast<const uint4*>(p.x + (int64_t)(m < M ? m : M - 1) * p.ldx + k);
+                float wf[8];
+                unpack8(u32x4{nw.x, nw.y, nw.z, nw.w}, wf);
+#pragma unroll
+                for (int m = 0; m < 16; m++) {
+                    if (m >= M) continue;
+                    float f[8];
+                    unpack8(u32x4{v[m].x, v[m].y, v[m].z, v[m].w}, f);
+                    uint32_t o[4];
+                    if (hf) {
+#pragma unroll
+                        for (int j = 0; j < 4; j++)
+                            o[j] = pack2(wf[2 * j] * rbf(f[2 * j] * inv[m]), wf[2 * j + 1] * rbf(f[2 * j + 1] * inv[m]));
+                    } else {
+                        float y[8];
+#pragma unroll
+                        for (int j = 0; j < 8; j++) {
+                            const float q = f[j] * inv[m];
+                            float d = fmaf(fmaf(-q, rms[m], f[j]), inv[m], q);
+                            const float af = fabsf(f[j]);
+                            if (af != 0.f && (af < 1e-30f || af > 1e30f)) d = f[j] / rms[m];
+                            y[j] = d * wf[j];
+                        }
+#pragma unroll
+                        for (int j = 0; j < 4; j++) o[j] = pack2(y[2 * j], y[2 * j + 1]);
+                    }
+                    *reinterpret_cast<uint4*>(xs + (int64_t)m * KP + k) = make_uint4(o[0], o[1], o[2], o[3]);
+                }
+            }
+        } else {
+            for (int m = 0; m < M; m++)
+                for (int64_t k = tid * 8; k < K; k += 2048)
+                    *reinterpret_cast<uint4*>(xs + (int64_t)m * KP + k) =
+                        *reinterpret_cast<const uint4*>(p.x + (int64_t)m * p.ldx + k);
+        }
+        __syncthreads();
+    }
     int64_t s = 0;
     for (; s + 2 < S; s += 2) {
         issue(sb, s + 1);

@@ -10,23 +10,22 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ROLE_7B = {   # Qwen2-7B call sites by (grid blocks, static LDS bytes; dynamic LDS is not reported)
-    "gemv_kernel [grid 2048, lds 0]": "decode gate/up GEMV (+RMSNorm, SwiGLU)  [dominant]",
-    "gemv_kernel [grid 448, lds 0]": "decode down GEMV and O-proj GEMV (+residual; same grid)",
-    "gemv_kernel [grid 576, lds 512]": "decode QKV GEMV (+RMSNorm, bias)",
-    "gemv_kernel [grid 2048, lds 512]": "lm_head GEMV (+final RMSNorm, arg-max keys)",
-    "gemv_kernel [grid 448, lds 512]": "bench live timing of down / O-proj (store epilogue)",
-    "gemm_kernel [grid 16, lds 0]": "prefill GEMMs (MFMA 128x128 tiles)",
-}
+# Qwen2-7B call sites: kernel template (qie:: and "void " stripped) + workgroups x threads
 ROLE = {
-    "gemv_kernel<1, 2, 2, 8, false>": "decode gate/up GEMV (+RMSNorm, SwiGLU)  [dominant]",
-    "gemv_kernel<1, 2, 1, 8, false>": "decode O-proj / down GEMV (+residual)",
-    "gemv_kernel<1, 2, 0, 8, false>": "decode QKV GEMV (+RMSNorm, bias) / lm_head (+arg-max)",
-    "attn_decode_mfma_kernel<128>": "decode attention (fused qk-norm/RoPE/KV append, split-K)",
-    "attn_prefill_mfma_kernel<128>": "prefill flash attention (MFMA)",
-    "gemm_kernel<0>": "prefill GEMM (store/bias)",
-    "gemm_kernel<1>": "prefill GEMM (+residual)",
-    "gemm_kernel<2>": "prefill GEMM (gate/up + SwiGLU)",
+    "gemv_kernel<1, 2, 2, 8, 2, 0, 256> [g 677 x 256]": "decode gate/up GEMV (+RMSNorm, SwiGLU)  [dominant]",
+    "gemv_kernel<1, 2, 1, 8, 10, 0, 576> [g 256 x 448]": "decode down GEMV (+residual), one block per CU",
+    "gemv_kernel<1, 2, 0, 8, 2, 0, 576> [g 256 x 576]": "decode QKV GEMV (+RMSNorm, bias), one block per CU",
+    "gemv_kernel<1, 2, 1, 8, 2, 0, 576> [g 256 x 448]": "decode O-proj GEMV (+residual), one block per CU",
+    "gemv_kernel<1, 2, 0, 8, 2, 0, 256> [g 761 x 256]": "lm_head GEMV (+final RMSNorm, arg-max keys)",
+    "attn_decode_mfma2_kernel<128>": "decode attention (fused qk-norm/RoPE/KV append, split-K, in-launch combine)",
+    "attn_prefill_mfma2_kernel<128>": "prefill flash attention (MFMA, 32 rows/wave)",
+    "gemm_big_kernel<2, 256>": "prefill gate/up GEMM (256x256 LDS-DMA, SwiGLU)",
+    "gemm_big_kernel<1, 128>": "prefill O / down GEMM (256x128 LDS-DMA, +residual)",
+    "gemm_kernel<0, 0>": "prefill QKV GEMM (128x128, +bias)",
+    "finalize_kernel": "token -> history, position++, next embedding row",
+    "gemv_kernel<1, 2, 0, 8, 10, 0, 576> [g 256 x 448]": "bench live timing of down (store epilogue)",
+    "gemv_kernel<1, 2, 0, 8, 2, 0, 576> [g 256 x 448]": "bench live timing of O-proj (store epilogue)",
+    "synth_kernel": "synthetic weight fill (setup)",
 }
 
 
@@ -41,9 +40,10 @@ def main(tag="r01", src="gpurun_out/prof"):
     groups = collections.defaultdict(list)
     for r in trace:
         key = short(r["Kernel_Name"])
-        if key.startswith("gemv_kernel") or key.startswith("gemm_kernel"):
-            # instantiations / call sites apart: grid and LDS bytes identify the GEMV (K sizes LDS)
-            key += f" [grid {int(r['Grid_Size_X']) // 256}, lds {r['LDS_Block_Size']}]"
+        if key.startswith("gemv_kernel"):
+            # call sites apart: workgroups x threads identify the GEMV
+            wg = int(r["Workgroup_Size_X"])
+            key += f" [g {int(r['Grid_Size_X']) // wg} x {wg}]"
         groups[key].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     total = sum(sum(v) for v in groups.values())
     lines = [f"# rocprofv3 kernel summary ({tag})", "",
@@ -53,7 +53,7 @@ def main(tag="r01", src="gpurun_out/prof"):
              "64 timed hipGraph decode steps + bench's live kernel timings).", "",
              "| kernel | role | calls | avg us | median us | total ms | % |", "|---|---|---|---|---|---|---|"]
     for name, v in sorted(groups.items(), key=lambda kv: -sum(kv[1])):
-        lines.append(f"| `{name}` | {ROLE.get(name, ROLE_7B.get(name, ''))} | {len(v)} | {statistics.mean(v):.2f} | "
+        lines.append(f"| `{name}` | {ROLE.get(name, '')} | {len(v)} | {statistics.mean(v):.2f} | "
                      f"{statistics.median(v):.2f} | {sum(v) / 1e3:.3f} | {100 * sum(v) / total:.2f} |")
     lines += ["", "Raw per-kernel stats (rocprofv3 `--stats`, template arguments folded): "
               f"`{tag}_kernel_stats.csv`."]

@@ -467,8 +467,13 @@ template <int EPI, int WT, int XL>
 __global__ __launch_bounds__(256) void skinny_mfma_kernel(GemvParams p) {
 #pragma clang fp contract(off)
     constexpr int NB = EPI == QIE_EPI_SWIGLU ? 2 : 1;   // B tiles per block (gate, up)
-    constexpr int KSTEP = WT ? 64 : 32;                   // k per 16-byte lane load
-    constexpr int U = (XL && NB == 1) ? 8 : 4;            // units per step (x2 buffers in flight)
+    // A unit = 64 k of each of the tile's 16 weight rows: a lane loads 32 contiguous bytes
+    // of its row (bf16: two 16-B vectors, two MFMA k-steps; fp8: one 16-B vector of 16
+    // codes), so one unit reads whole 128-B lines per row (bf16; fp8 64 B) instead of the
+    // 64-B half lines of a 32-k unit.
+    constexpr int KSTEP = 64;
+    constexpr int WV = WT ? 1 : 2;                        // 16-B weight vectors per lane per unit
+    constexpr int U = WT ? ((XL && NB == 1) ? 8 : 4) : ((XL && NB == 1) ? 4 : 2);   // units per step
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int64_t K = p.K;
     const int M = p.M;
@@ -513,10 +518,10 @@ __global__ __launch_bounds__(256) void skinny_mfma_kernel(GemvParams p) {
     // global load sits under a branch: the steps form one stream per wave, double-
     // buffered in registers, so the next step's loads (next tile included) are in
     // flight while this step's MFMAs, the cross-wave reduction and the epilogue run.
-    constexpr int AW = WT ? 2 : 1;   // 16-B A fragments per unit
+    constexpr int AW = 2;            // 16-B A fragments per unit (k 16g..16g+7, 16g+8..16g+15)
     constexpr int EB = WT ? 1 : 2;
     struct Step {
-        u32x4 wv[U][NB];
+        u32x4 wv[U][NB][WV];
         uint4 av[XL ? 1 : U][AW];
         float wsc[NB];
         float ep[4];       // residual values (rows 4 g + r) or the bias (ep[0])
@@ -575,9 +580,12 @@ __global__ __launch_bounds__(256) void skinny_mfma_kernel(GemvParams p) {
             const int64_t uu = st.u0 + u < ue ? st.u0 + u : ue - 1;
 #pragma unroll
             for (int b = 0; b < NB; b++)   // bytes [uu * 64 + 16 g, +16) of the row, both formats
-                st.wv[u][b] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wrow[b]) + uu * 4 + g);
+#pragma unroll
+                for (int h = 0; h < WV; h++)
+                    st.wv[u][b][h] =
+                        __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wrow[b]) + uu * (4 * WV) + WV * g + h);
             if constexpr (!XL) {
-                const int64_t kk = uu * KSTEP + (WT ? 16 : 8) * g;
+                const int64_t kk = uu * KSTEP + 16 * g;
 #pragma unroll
                 for (int h = 0; h < AW; h++) st.av[u][h] = xa(kk + 8 * h);
             }
@@ -591,7 +599,7 @@ __global__ __launch_bounds__(256) void skinny_mfma_kernel(GemvParams p) {
         for (int u = 0; u < U; u++) {
             const bool live = st.u0 + u < ue;   // dead steps multiply a zero A fragment
             const int64_t uu = live ? st.u0 + u : ue - 1;
-            const int64_t kk = uu * KSTEP + (WT ? 16 : 8) * g;
+            const int64_t kk = uu * KSTEP + 16 * g;
             uint4 ar[AW];
 #pragma unroll
             for (int h = 0; h < AW; h++) {
@@ -599,21 +607,25 @@ __global__ __launch_bounds__(256) void skinny_mfma_kernel(GemvParams p) {
                 ar[h] = live ? v : make_uint4(0, 0, 0, 0);
             }
             if constexpr (WT == 0) {
-                const bf16x8_t a = __builtin_bit_cast(bf16x8_t, ar[0]);
+                const bf16x8_t a0 = __builtin_bit_cast(bf16x8_t, ar[0]);
+                const bf16x8_t a1 = __builtin_bit_cast(bf16x8_t, ar[1]);
 #pragma unroll
-                for (int b = 0; b < NB; b++)
-                    acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8_t, st.wv[u][b]),
+                for (int b = 0; b < NB; b++) {
+                    acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, __builtin_bit_cast(bf16x8_t, st.wv[u][b][0]),
                                                                      acc[b], 0, 0, 0);
+                    acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, __builtin_bit_cast(bf16x8_t, st.wv[u][b][1]),
+                                                                     acc[b], 0, 0, 0);
+                }
             } else {
                 const bf16x8_t a0 = __builtin_bit_cast(bf16x8_t, ar[0]);
                 const bf16x8_t a1 = __builtin_bit_cast(bf16x8_t, ar[AW - 1]);
 #pragma unroll
                 for (int b = 0; b < NB; b++) {
                     float f[16];
-                    fp8x4_to_f32(st.wv[u][b].x, f);
-                    fp8x4_to_f32(st.wv[u][b].y, f + 4);
-                    fp8x4_to_f32(st.wv[u][b].z, f + 8);
-                    fp8x4_to_f32(st.wv[u][b].w, f + 12);
+                    fp8x4_to_f32(st.wv[u][b][0].x, f);
+                    fp8x4_to_f32(st.wv[u][b][0].y, f + 4);
+                    fp8x4_to_f32(st.wv[u][b][0].z, f + 8);
+                    fp8x4_to_f32(st.wv[u][b][0].w, f + 12);
                     const uint4 lo = make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]),
                                                 pack2(f[6], f[7]));
                     const uint4 hi = make_uint4(pack2(f[8], f[9]), pack2(f[10], f[11]), pack2(f[12], f[13]),
@@ -984,7 +996,7 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
     p.key_col0 = a->key_col0;
     if (a->M >= 2 && a->M <= 16 && env_int("QIE_SKINNY_MFMA", 1) != 0) {
         const bool fp8w = (a->flags & QIE_LINEAR_FP8) != 0;
-        const int kstep = fp8w ? 64 : 32;
+        const int kstep = 64;
         const bool lds_ok = (size_t)a->M * (a->K + 8) * 2 <= kSkinnyLdsCap;
         if (a->K % kstep == 0 && (lds_ok || !a->norm_w)) {
             p.M = (int)a->M;

@@ -75,6 +75,7 @@ struct qie_batch {
     uint16_t* q = nullptr;
     uint16_t* att = nullptr;
     uint16_t* h = nullptr;
+    uint16_t* xn = nullptr;     // [B][H] RMS-normed rows feeding the batched (B >= 2) projections
     uint16_t* logits = nullptr;
     void* attn_ws = nullptr;
     void* dec_ws = nullptr;     // fused decode attention: split partials + zeroed counters
@@ -283,6 +284,21 @@ static int row_parallel(qie_batch* b, qie_linear_args& a, uint16_t* x, float* pa
     return qie_residual_add_f32(x, part, n, e->stream);
 }
 
+// Batched rows (2 <= M <= 16, the skinny MFMA kernel): RMSNorm the M rows once into b->xn
+// (qie_rmsnorm, normalization.cu:5-25 semantics) and feed the projection plain rows.  The
+// skinny kernel's fused norm prologue recomputed every row's norm in every workgroup and
+// cost 13-16 us per launch at B = 8 (tools/ubench_b8.py, QIE_SKINNY_DBG); M = 1 keeps the
+// GEMV's fused x-first prologue.  QIE_PRENORM=0 restores the fused form (A/B).
+static int prenorm(qie_batch* b, qie_linear_args& a, int64_t M) {
+    static const int on = getenv("QIE_PRENORM") ? atoi(getenv("QIE_PRENORM")) : 1;
+    if (!on || M < 2 || M > 16 || !a.norm_w) return 0;
+    QIE_TRY(qie_rmsnorm(a.x, a.norm_w, b->xn, M, a.K, a.norm_eps, a.numerics, b->e->stream));
+    a.x = b->xn;
+    a.ldx = a.K;
+    a.norm_w = nullptr;
+    return 0;
+}
+
 static int enqueue_layer_decode(qie_batch* b, int l) {
     qie_engine* e = b->e;
     const qie_model_spec& s = e->spec;
@@ -301,6 +317,7 @@ static int enqueue_layer_decode(qie_batch* b, int l) {
     a.y = b->qkv; a.ldy = QKVD;
     a.epilogue = QIE_EPI_STORE;
     a.norm_w = L.attn_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
+    QIE_TRY(prenorm(b, a, B));
     QIE_TRY(gemv(&a, st));
 
     QIE_TRY(qie_attention_decode(b->qkv, B, b->d_pos, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, e->sh.nq,
@@ -320,6 +337,7 @@ static int enqueue_layer_decode(qie_batch* b, int l) {
     a.y = b->h; a.ldy = I;
     a.epilogue = QIE_EPI_SWIGLU;
     a.norm_w = L.ffn_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
+    QIE_TRY(prenorm(b, a, B));
     QIE_TRY(gemv(&a, st));
 
     a = lin_base(e);
@@ -368,6 +386,7 @@ static int enqueue_head(qie_batch* b, const uint16_t* x, int64_t ldx, int m0, in
     a.y = b->logits + (int64_t)m0 * Vl; a.ldy = Vl;
     a.epilogue = QIE_EPI_STORE;
     a.norm_w = e->w.final_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
+    QIE_TRY(prenorm(b, a, M));
     const bool greedy = is_greedy(smp);
     if (greedy) {
         a.argmax_keys = (uint64_t*)(b->d_keys + m0);
@@ -790,6 +809,7 @@ int qie_batch_create(qie_engine* e, int32_t batch, int32_t max_ctx, qie_batch** 
     A((void**)&b->q, batch * QD * 2);
     A((void**)&b->att, batch * QD * 2);
     A((void**)&b->h, batch * (int64_t)sh.ffn * 2);
+    A((void**)&b->xn, batch * H * 2);
     A((void**)&b->logits, batch * (int64_t)sh.vocab * 2);
     A(&b->attn_ws, (size_t)qie_attention_workspace_bytes(batch, sh.nq, s.head_dim, max_ctx));
     A(&b->samp_ws, (size_t)qie_sample_workspace_bytes(batch, s.vocab));
@@ -829,7 +849,7 @@ void qie_batch_destroy(qie_batch* b) {
     void* ps[] = {b->kc, b->vc, b->d_pos, b->d_step, b->d_hist, b->d_ids, b->d_keys, b->x_res, b->qkv, b->q,
                   b->att, b->h, b->logits, b->attn_ws, b->dec_ws, b->samp_ws, b->pf_x, b->pf_hn, b->pf_qkv, b->pf_q,
                   b->pf_att, b->pf_h, b->pf_pos, b->pf_ids, b->pf_attn_ws, b->part, b->logits_full,
-                  b->gather_tmp, b->pf_part};
+                  b->gather_tmp, b->pf_part, b->xn};
     for (void* p : ps)
         if (p) hipFree(p);
     delete b;
@@ -1042,6 +1062,11 @@ int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* av
         return fail(-22, "qie_batch_time_kernel: unknown kernel %d", which);
     }
     qie_kv_cache cache{b->kc, b->vc, b->seq_stride, s.n_layers, sh.nkv, s.head_dim, b->max_ctx};
+    if (B >= 2 && a.norm_w && !(getenv("QIE_PRENORM") && atoi(getenv("QIE_PRENORM")) == 0)) {
+        a.x = b->xn;   // as the batched step runs it: rows normed once by prenorm(), plain GEMV
+        a.ldx = a.K;
+        a.norm_w = nullptr;
+    }
     if (which == 5) {
         std::vector<int32_t> pos(B);
         hipMemcpy(pos.data(), b->d_pos, B * 4, hipMemcpyDeviceToHost);

@@ -46,6 +46,8 @@ struct GemvParams {
     unsigned long long* keys;
     int64_t key_col0;
     int64_t n_tasks;
+    int dbg;           // skinny kernel timing experiments (QIE_SKINNY_DBG): 1 plain x copy instead of the
+                       // fused norm, 2 stop after the prologue, 4 no prologue at all
 };
 
 __device__ __forceinline__ void fma8(float& acc, const float* xf, u32x4 w) {
@@ -700,8 +702,8 @@ __global__ __launch_bounds__(256) void skinny_mfma_kernel(GemvParams p) {
     // ---------------- prologue: the M activation rows -> LDS (optionally RMS-normed).  It runs
     // AFTER the first step's weight loads are issued (weights do not depend on x), so the
     // weight stream's first HBM round trip overlaps the prologue's loads and reductions.
-    if (XL) {
-        if (p.norm_w) {
+    if (XL && !(p.dbg & 4)) {
+        if (p.norm_w && !(p.dbg & 1)) {
             // pass 1: every row's sum of squares at once (loads of all rows in flight,
             // clamped rows past M), ONE exchange — not a barrier pair per row
             float ss[16];
@@ -782,6 +784,10 @@ __global__ __launch_bounds__(256) void skinny_mfma_kernel(GemvParams p) {
                         *reinterpret_cast<const uint4*>(p.x + (int64_t)m * p.ldx + k);
         }
         __syncthreads();
+    }
+    if (p.dbg & 2) {
+        if (tid == 0 && p.dbg == 0x7fffffff) p.y[0] = xs[0];
+        return;
     }
     int64_t s = 0;
     for (; s + 2 < S; s += 2) {
@@ -994,6 +1000,7 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
     p.M = (int)a->M;
     p.keys = (unsigned long long*)a->argmax_keys;
     p.key_col0 = a->key_col0;
+    p.dbg = 0;
     if (a->M >= 2 && a->M <= 16 && env_int("QIE_SKINNY_MFMA", 1) != 0) {
         const bool fp8w = (a->flags & QIE_LINEAR_FP8) != 0;
         const int kstep = 64;
@@ -1001,6 +1008,7 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
         if (a->K % kstep == 0 && (lds_ok || !a->norm_w)) {
             p.M = (int)a->M;
             p.xlds = lds_ok ? 1 : 0;
+            p.dbg = env_int("QIE_SKINNY_DBG", 0);
             return launch_skinny(p, a->epilogue, fp8w, st);
         }
     }

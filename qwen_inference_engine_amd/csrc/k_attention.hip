@@ -18,6 +18,14 @@
 #include "qie_common.hpp"
 #include "../../include/qie/qie_ops.h"
 
+#ifndef QIE_TRY
+#define QIE_TRY(expr)                  \
+    do {                               \
+        const int _rc = (expr);        \
+        if (_rc) return _rc;           \
+    } while (0)
+#endif
+
 #include <cstdlib>
 
 namespace qie {
@@ -225,6 +233,7 @@ struct DecodeAttnParams {
     float* part_ml;           // [B][nq][nsplit_max][2]
     unsigned* counters;       // [B][nkv], zero at rest
     uint16_t* out;            // [B][nq * HD]
+    int fused;                // 1: inside attn_o_fused_kernel (always the split path + combine)
 };
 
 // Splits per (row, kv head): ~16 at long context (>= 64 keys each), more only when
@@ -1425,8 +1434,10 @@ __device__ __forceinline__ void dec_pro_finish(const DecodeAttnParams& a, DecPro
     }
 }
 
+// Body of the decode attention for workgroup (bx, by); true when this workgroup wrote a
+// combined (row, kv head) output (its stores are write-through, sc1).
 template <int HD>
-__global__ __launch_bounds__(256) void attn_decode_mfma2_kernel(DecodeAttnParams a) {
+__device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a, const int bx, const int by) {
 #pragma clang fp contract(off)
     constexpr int LPT = HD / 8;          // prologue: lanes per head row
     constexpr int KSTEPS = HD / 32;      // MFMA k-steps over d for S
@@ -1441,13 +1452,13 @@ __global__ __launch_bounds__(256) void attn_decode_mfma2_kernel(DecodeAttnParams
     __shared__ __attribute__((aligned(16))) float s_s[16][kDecMStep + 4];
     __shared__ int last_flag;
 
-    const int64_t m = blockIdx.y;
-    const int g = blockIdx.x / a.nsplit_max, s = blockIdx.x % a.nsplit_max;
+    const int64_t m = by;
+    const int g = bx / a.nsplit_max, s = bx % a.nsplit_max;
     const int G = a.nq / a.nkv;
     const int p = a.pos[m], ctx = p + 1;
     const int chunk = decm_chunk(ctx, a.splits_target);
     const int nsplit = (ctx + chunk - 1) / chunk;
-    if (s >= nsplit || (a.dbg & 64)) return;
+    if (s >= nsplit || (a.dbg & 64)) return false;
     const int t0 = s * chunk, t1 = min(ctx, t0 + chunk);
     const int nstep = (t1 - t0 + kDecMStep - 1) / kDecMStep;
     const bool has_new = (t1 == ctx);
@@ -1487,7 +1498,7 @@ __global__ __launch_bounds__(256) void attn_decode_mfma2_kernel(DecodeAttnParams
     __syncthreads();
     if (a.dbg & 8) {
         if (tid == 0) a.out[m] = (uint16_t)(kf[0][0].x + vr[VCH - 1].y + kf[1][KSTEPS - 1].z);
-        return;
+        return false;
     }
 
     bf16x8_t qb[KSTEPS];
@@ -1597,7 +1608,7 @@ __global__ __launch_bounds__(256) void attn_decode_mfma2_kernel(DecodeAttnParams
     }
     if (a.dbg & 16) {
         if (tid == 0) a.out[m] = (uint16_t)(oacc[0][0] + m_run);
-        return;
+        return false;
     }
 
     // ---------------- this wave's d-slice of the split result (rows = heads 4 gq + r)
@@ -1605,7 +1616,7 @@ __global__ __launch_bounds__(256) void attn_decode_mfma2_kernel(DecodeAttnParams
     float lr[4];
 #pragma unroll
     for (int r = 0; r < 4; r++) lr[r] = __shfl(l_run, gq * 4 + r, 64);
-    if (nsplit == 1) {
+    if (nsplit == 1 && !a.fused) {
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             const int h = 4 * gq + r;
@@ -1615,7 +1626,7 @@ __global__ __launch_bounds__(256) void attn_decode_mfma2_kernel(DecodeAttnParams
                 a.out[m * (int64_t)nq * HD + (int64_t)(g * G + h) * HD + wave * DW + 16 * d + fr] =
                     f2bf(oacc[d][r] / lr[r]);
         }
-        return;
+        return false;
     }
 #pragma unroll
     for (int r = 0; r < 4; r++) {
@@ -1637,14 +1648,14 @@ __global__ __launch_bounds__(256) void attn_decode_mfma2_kernel(DecodeAttnParams
     // ---------------- publish this split; the last arriver combines (acquire)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
     __syncthreads();
-    if (a.dbg & 1) return;
+    if (a.dbg & 1) return false;
     unsigned* cnt = a.counters + m * a.nkv + g;
     if (tid == 0) {
         const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         last_flag = (old == (unsigned)nsplit - 1) ? 1 : 0;
     }
     __syncthreads();
-    if (!last_flag) return;
+    if (!last_flag) return false;
     if (tid == 0 && !(a.dbg & 4)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1689,9 +1700,150 @@ __global__ __launch_bounds__(256) void attn_decode_mfma2_kernel(DecodeAttnParams
     if (has_item) {
         const float inv = 1.0f / ls;
         uint16_t* dst = a.out + m * (int64_t)nq * HD + (int64_t)(g * G + gi) * HD + d4 * 4;
-        *reinterpret_cast<uint2*>(dst) = make_uint2(pack2(acc.x * inv, acc.y * inv), pack2(acc.z * inv, acc.w * inv));
+        // write-through 8-B store: the fused O-proj workgroups read it with sc1 loads
+        const unsigned long long pk = (unsigned long long)pack2(acc.x * inv, acc.y * inv) |
+                                      ((unsigned long long)pack2(acc.z * inv, acc.w * inv) << 32);
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(dst), pk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (tid == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+}
+
+template <int HD>
+__global__ __launch_bounds__(256) void attn_decode_mfma2_kernel(DecodeAttnParams a) {
+    attn_decode_mfma2_body<HD>(a, blockIdx.x, blockIdx.y);
+}
+
+// ---------------------------------------------------------------------------
+// Decode attention + O-projection in ONE launch (batch 1, bf16 weights): workgroups take a
+// ticket at entry; tickets [0, n_attn) run the attention above, the rest own two O-proj
+// rows per wave.  An O workgroup issues its weight rows BEFORE waiting for the attention,
+// so the W_o stream overlaps the attention's round trips and the attention -> O launch
+// boundary disappears.  Deadlock-free by construction: every attention ticket was taken by
+// a running workgroup before any O workgroup can wait.  Hand-off: the combining attention
+// workgroups store the output write-through (sc1), drain, then add to `done`; the O side
+// polls `done` (relaxed, bounded by a 20 ms give-up that sets `err`) and reads the row with
+// sc1 loads — cdna_hip_programming.md Guideline 16 / MI355X_MICROARCH.md § visibility,
+// 'atomic add + sc1 loads' form.  The last workgroup to finish zeroes the counters.
+// Per-row arithmetic is the GEMV's (lane chunks k = 8 lane + 512 u, wave butterfly,
+// x = bf16(x + bf16(acc))), so results equal the unfused path bit for bit.
+// counter words: ticket [0], fin [16], err [32], done replica r at [64 + 16 r] (64-B apart:
+// the O workgroups poll the replica of their XCD group, blockIdx % 8, not one hot line)
+constexpr int kFuseCtrWords = 64 + 16 * 8;
+constexpr int kFuseRows = 4;    // O-proj rows per wave
+struct AttnOParams {
+    const uint16_t* wo;       // [H][QD] bf16
+    uint16_t* x;              // residual stream row [H]
+    int64_t H, QD;
+    unsigned* ctr;            // [kFuseCtrWords]: ticket, fin, err, 8 per-XCD `done` replicas (zero at rest)
+    int n_attn;
+    int prefetch;             // 1: W_o rows loaded before the wait (A/B: QIE_FUSE_PF)
+    int sleep;                // poll back-off (QIE_FUSE_SLEEP, s_sleep units of 64 cycles)
+};
+
+template <int HD>
+__global__ __launch_bounds__(256) void attn_o_fused_kernel(DecodeAttnParams a, AttnOParams o) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
+    uint16_t* xs = reinterpret_cast<uint16_t*>(dsm);   // [QD] attention output row
+    __shared__ int role_s;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) role_s = (int)__hip_atomic_fetch_add(&o.ctr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int t = role_s;
+    if (t < o.n_attn) {
+        if (attn_decode_mfma2_body<HD>(a, t, 0)) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
+            __syncthreads();
+            if (tid == 0) {
+#pragma unroll
+                for (int r = 0; r < 8; r++)
+                    __hip_atomic_fetch_add(&o.ctr[64 + 16 * r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    } else {
+        typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+        constexpr int R = kFuseRows;
+        const int64_t task = (int64_t)(t - o.n_attn) * 4 + wave;
+        const u32x4v* wr[R];
+#pragma unroll
+        for (int i = 0; i < R; i++) {
+            const int64_t r = task * R + i < o.H ? task * R + i : o.H - 1;
+            wr[i] = reinterpret_cast<const u32x4v*>(o.wo + r * o.QD);
+        }
+        constexpr int U = 8;   // 512-element chunks per row: QD <= 4096
+        u32x4v wv[U][R];
+        auto load_w = [&]() {
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int64_t k = (int64_t)lane * 8 + u * 512;
+                const int64_t kc = (k < o.QD ? k : o.QD - 8) / 8;
+#pragma unroll
+                for (int i = 0; i < R; i++) wv[u][i] = __builtin_nontemporal_load(wr[i] + kc);
+            }
+        };
+        if (o.prefetch) load_w();
+        if (tid == 0) {
+            const unsigned target = (unsigned)a.nkv;
+            const unsigned* rep = &o.ctr[64 + 16 * (blockIdx.x & 7)];
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (__hip_atomic_load(rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                for (int z = 0; z < o.sleep; z++) __builtin_amdgcn_s_sleep(1);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000ull) {   // 20 ms at 100 MHz: give up
+                    __hip_atomic_store(&o.ctr[32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+        if (!o.prefetch) load_w();
+        for (int64_t k = (int64_t)tid * 4; k < o.QD; k += 1024)
+            *reinterpret_cast<unsigned long long*>(xs + k) = __hip_atomic_load(
+                reinterpret_cast<const unsigned long long*>(a.out + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        float acc[R];
+#pragma unroll
+        for (int i = 0; i < R; i++) acc[i] = 0.f;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int64_t k = (int64_t)lane * 8 + u * 512;
+            if (k < o.QD) {
+                const uint4 xv = *reinterpret_cast<const uint4*>(xs + k);
+                const uint32_t xw[4] = {xv.x, xv.y, xv.z, xv.w};
+                float xf[8];
+#pragma unroll
+                for (int j = 0; j < 4; j++) { xf[2 * j] = bf_lo(xw[j]); xf[2 * j + 1] = bf_hi(xw[j]); }
+#pragma unroll
+                for (int i = 0; i < R; i++) {
+                    const uint32_t wq[4] = {wv[u][i].x, wv[u][i].y, wv[u][i].z, wv[u][i].w};
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        acc[i] = fmaf(xf[2 * j], bf_lo(wq[j]), acc[i]);
+                        acc[i] = fmaf(xf[2 * j + 1], bf_hi(wq[j]), acc[i]);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < R; i++) acc[i] = wave_sum(acc[i]);
+        if (lane == 0) {
+#pragma clang fp contract(off)
+#pragma unroll
+            for (int i = 0; i < R; i++) {
+                const int64_t r = task * R + i;
+                if (r < o.H) o.x[r] = f2bf(bf2f(o.x[r]) + rbf(acc[i]));
+            }
+        }
+    }
+    if (tid == 0) {
+        const unsigned f = __hip_atomic_fetch_add(&o.ctr[16], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (f == gridDim.x - 1) {   // every workgroup has finished: reset for the next launch
+            __hip_atomic_store(&o.ctr[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&o.ctr[16], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int r = 0; r < 8; r++)
+                __hip_atomic_store(&o.ctr[64 + 16 * r], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 // Diagnostics: lane l reads the 8 bytes at element 4*l of an LDS array holding
@@ -1713,6 +1865,41 @@ static int attn_nsplit(int64_t M, int32_t max_ctx) {
     if (ns > cap) ns = cap;
     if (ns < 1) ns = 1;
     return ns;
+}
+
+static int fill_dec_params(DecodeAttnParams& a, const void* qkv, int64_t B, const int32_t* pos, const void* q_norm,
+                           const void* k_norm, const float* rope_cos, const float* rope_sin, int32_t n_heads,
+                           const qie_kv_cache* cache, int32_t layer, float eps, int32_t numerics, void* out, void* ws) {
+    a.qkv = (const uint16_t*)qkv;
+    a.pos = pos;
+    a.q_norm = (const uint16_t*)q_norm;
+    a.k_norm = (const uint16_t*)k_norm;
+    a.cs = rope_cos;
+    a.sn = rope_sin;
+    a.kc = (uint16_t*)cache->k;
+    a.vc = (uint16_t*)cache->v;
+    a.seq_stride = cache->seq_stride;
+    a.layer = layer;
+    a.nkv = cache->n_kv_heads;
+    a.nq = n_heads;
+    a.max_ctx = cache->max_ctx;
+    const bool valu = getenv("QIE_DEC_VALU") && atoi(getenv("QIE_DEC_VALU")) != 0;   // A/B timing only
+    const char* se = getenv("QIE_DEC_SPLITS");
+    const int senv = se ? std::min(atoi(se), kDecMaxSplits) : 0;
+    a.splits_target = senv > 0 ? senv : (valu ? kDecSplits : kDecMSplits);
+    a.dbg = getenv("QIE_DEC_DBG") ? atoi(getenv("QIE_DEC_DBG")) : 0;
+    a.nsplit_max = valu ? dec_nsplit_target(cache->max_ctx, cache->head_dim, a.splits_target)
+                        : std::min(a.splits_target, (cache->max_ctx + kDecMStep - 1) / kDecMStep);
+    QIE_REQUIRE(a.nsplit_max <= kDecMaxSplits, "qie_attention_decode: max_ctx %d too long", cache->max_ctx);
+    a.eps = eps;
+    a.numerics = numerics;
+    const int64_t cnt = ((B * a.nkv * 4 + 255) / 256) * 256;
+    a.counters = (unsigned*)ws;
+    a.part_o = (float*)((char*)ws + cnt);
+    a.part_ml = a.part_o + B * n_heads * (int64_t)a.nsplit_max * cache->head_dim;
+    a.out = (uint16_t*)out;
+    a.fused = 0;
+    return 0;
 }
 
 }  // namespace qie
@@ -1829,34 +2016,9 @@ int qie_attention_decode(const void* qkv, int64_t B, const int32_t* pos, const v
                 "qie_attention_decode: n_heads/n_kv_heads must be an integer <= %d", kMaxGroup);
     QIE_REQUIRE(layer >= 0 && layer < cache->n_layers, "qie_attention_decode: bad layer");
     DecodeAttnParams a;
-    a.qkv = (const uint16_t*)qkv;
-    a.pos = pos;
-    a.q_norm = (const uint16_t*)q_norm;
-    a.k_norm = (const uint16_t*)k_norm;
-    a.cs = rope_cos;
-    a.sn = rope_sin;
-    a.kc = (uint16_t*)cache->k;
-    a.vc = (uint16_t*)cache->v;
-    a.seq_stride = cache->seq_stride;
-    a.layer = layer;
-    a.nkv = cache->n_kv_heads;
-    a.nq = n_heads;
-    a.max_ctx = cache->max_ctx;
+    QIE_TRY(fill_dec_params(a, qkv, B, pos, q_norm, k_norm, rope_cos, rope_sin, n_heads, cache, layer, eps, numerics,
+                            out, ws));
     const bool valu = getenv("QIE_DEC_VALU") && atoi(getenv("QIE_DEC_VALU")) != 0;   // A/B timing only
-    const char* se = getenv("QIE_DEC_SPLITS");
-    const int senv = se ? std::min(atoi(se), kDecMaxSplits) : 0;
-    a.splits_target = senv > 0 ? senv : (valu ? kDecSplits : kDecMSplits);
-    a.dbg = getenv("QIE_DEC_DBG") ? atoi(getenv("QIE_DEC_DBG")) : 0;
-    a.nsplit_max = valu ? dec_nsplit_target(cache->max_ctx, cache->head_dim, a.splits_target)
-                        : std::min(a.splits_target, (cache->max_ctx + kDecMStep - 1) / kDecMStep);
-    QIE_REQUIRE(a.nsplit_max <= kDecMaxSplits, "qie_attention_decode: max_ctx %d too long", cache->max_ctx);
-    a.eps = eps;
-    a.numerics = numerics;
-    const int64_t cnt = ((B * a.nkv * 4 + 255) / 256) * 256;
-    a.counters = (unsigned*)ws;
-    a.part_o = (float*)((char*)ws + cnt);
-    a.part_ml = a.part_o + B * n_heads * (int64_t)a.nsplit_max * cache->head_dim;
-    a.out = (uint16_t*)out;
     dim3 grid((unsigned)(a.nkv * a.nsplit_max), (unsigned)B);
     const int G = n_heads / cache->n_kv_heads;
     using K = void (*)(DecodeAttnParams);
@@ -1887,3 +2049,44 @@ int qie_attention_decode(const void* qkv, int64_t B, const int32_t* pos, const v
 }
 
 }  // extern "C"
+
+namespace qie {
+// Decode attention + O-projection + residual in one launch (attn_o_fused_kernel); batch 1,
+// bf16 W_o [H][QD] with QD <= 4096; ctr = 4 zeroed unsigned counters owned by the caller.
+int attention_o_fused(const void* qkv, const int32_t* pos, const void* q_norm, const void* k_norm,
+                      const float* rope_cos, const float* rope_sin, int32_t n_heads, const qie_kv_cache* cache,
+                      int32_t layer, float eps, int32_t numerics, void* att_out, void* ws, const void* wo, void* x,
+                      int64_t H, unsigned* ctr, void* stream) {
+    QIE_REQUIRE(qkv && pos && cache && cache->k && cache->v && rope_cos && rope_sin && att_out && ws && wo && x && ctr,
+                "attention_o_fused: bad arguments");
+    QIE_REQUIRE(cache->head_dim == 64 || cache->head_dim == 128, "attention_o_fused: head_dim 64 or 128");
+    QIE_REQUIRE(n_heads % cache->n_kv_heads == 0 && n_heads / cache->n_kv_heads <= kMaxGroup,
+                "attention_o_fused: bad head grouping");
+    QIE_REQUIRE(layer >= 0 && layer < cache->n_layers, "attention_o_fused: bad layer");
+    const int64_t QD = (int64_t)n_heads * cache->head_dim;
+    QIE_REQUIRE(QD <= 4096 && QD % 8 == 0, "attention_o_fused: QD %lld unsupported", (long long)QD);
+    DecodeAttnParams a;
+    QIE_TRY(fill_dec_params(a, qkv, 1, pos, q_norm, k_norm, rope_cos, rope_sin, n_heads, cache, layer, eps, numerics,
+                            att_out, ws));
+    a.fused = 1;
+    AttnOParams o;
+    o.wo = (const uint16_t*)wo;
+    o.x = (uint16_t*)x;
+    o.H = H;
+    o.QD = QD;
+    o.ctr = ctr;
+    o.n_attn = a.nkv * a.nsplit_max;
+    o.prefetch = getenv("QIE_FUSE_PF") ? atoi(getenv("QIE_FUSE_PF")) : 1;
+    o.sleep = getenv("QIE_FUSE_SLEEP") ? atoi(getenv("QIE_FUSE_SLEEP")) : 16;
+    const int n_o = (int)((H + 4 * kFuseRows - 1) / (4 * kFuseRows));
+    const size_t shm = (size_t)QD * 2;
+    if (cache->head_dim == 128)
+        hipLaunchKernelGGL(attn_o_fused_kernel<128>, dim3((unsigned)(o.n_attn + n_o)), dim3(256), shm, (hipStream_t)stream,
+                           a, o);
+    else
+        hipLaunchKernelGGL(attn_o_fused_kernel<64>, dim3((unsigned)(o.n_attn + n_o)), dim3(256), shm, (hipStream_t)stream,
+                           a, o);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+}  // namespace qie

@@ -102,6 +102,27 @@ void qie_engine_destroy(qie_engine* e);
 int qie_batch_create(qie_engine* e, int32_t batch, int32_t max_ctx, qie_batch** out);
 void qie_batch_destroy(qie_batch* b);
 
+/* Paged KV cache with a device block table.  Replaces the
+ * reference's per-sequence linked page list — create_page_list /
+ * allocate_page_buffers / free_page_list (iengine.cu:73-109) walked by
+ * kv_copy_layer_to_cache_prefill/decode (include_cuda.cu:165-279) and the
+ * batch_metadata slots (iengine.cuh:27-37).  A pool of n_pages pages of
+ * page_tokens tokens (a power of two >= 128; 0 = 128) shared by the B slots;
+ * n_pages 0 = enough for every slot at max_ctx.  Pages are taken on demand by
+ * qie_prefill / qie_decode* / qie_batch_set_position and returned by
+ * qie_batch_release; running out of pages fails the call (-28, nothing launched).
+ * Page 0 is a scratch page that idle slots write into. */
+int qie_batch_create_paged(qie_engine* e, int32_t batch, int32_t max_ctx, int32_t page_tokens,
+                           int32_t n_pages, qie_batch** out);
+/* Ends sequence `seq`: its pages go back to the pool (paged) and the slot idles —
+ * it still runs through every decode step on the scratch page, its outputs are
+ * meaningless — until the next qie_prefill into it.  Any batch. */
+int qie_batch_release(qie_batch* b, int32_t seq);
+/* Pool state: free pages, pages per slot (host [B], may be NULL), page_tokens. */
+int qie_batch_page_stats(qie_batch* b, int32_t* free_pages, int32_t* pages_per_seq, int32_t* page_tokens);
+/* The n first block-table entries of `seq` (host copy); paged batches only. */
+int qie_batch_block_table(qie_batch* b, int32_t seq, int32_t* host_pages, int32_t n);
+
 /* Prefill sequence `seq` with n prompt ids (host array); writes its KV rows
  * 0..n-1, samples the first generated token (host *next_id, may be NULL) and
  * makes it the sequence's current token at position n. */

@@ -108,16 +108,26 @@ int qie_linear(const qie_linear_args* args, void* stream);
  *   qkv rows [M, (nq + 2*nkv)*hd] (projection output, bias already added)
  *   -> q_out [M, nq*hd] (qk-norm'd, rotated)
  *   -> K cache row (qk-norm'd, rotated) and V cache row at position pos[m].
- * KV cache layout (qie): per sequence [L][nkv][max_ctx][hd] bf16, sequence s
- * at kc + s*seq_stride; row m belongs to sequence m / rows_per_seq.
- * (The reference's pages are [4 tok][L][kvdim] linked through managed memory,
- * iengine.cu:73-109; qie keeps each (layer, kv head) contiguous for coalesced
- * streaming reads.) */
+ * KV cache layout (qie), two forms:
+ *   contiguous (block_table == NULL): per sequence [L][nkv][max_ctx][hd] bf16,
+ *     sequence s at k + s*seq_stride;
+ *   paged (block_table != NULL): a pool of pages of page_tokens tokens (a power
+ *     of two, multiple of 128), page p at k + p*seq_stride holding
+ *     [L][nkv][page_tokens][hd]; token t of sequence s lives in page
+ *     block_table[s*max_pages + t/page_tokens] at row t % page_tokens.
+ * Row m belongs to sequence m / rows_per_seq.
+ * (The reference's pages are [4 tok][L][kvdim] nodes of a linked list in managed
+ * memory, iengine.cu:73-109, walked by include_cuda.cu:165-279; qie replaces the
+ * list with a device block table and keeps each (layer, kv head) run of a page
+ * contiguous, so a 128-key attention step streams one run of one page.) */
 typedef struct qie_kv_cache {
-    void* k;                 /* base of sequence 0's K cache                           */
+    void* k;                 /* contiguous: sequence 0's K cache; paged: page 0       */
     void* v;
-    int64_t seq_stride;      /* elements between sequences                             */
+    int64_t seq_stride;      /* elements between sequences (contiguous) / pages (paged) */
     int32_t n_layers, n_kv_heads, head_dim, max_ctx;
+    const int32_t* block_table;   /* device [n_seq][max_pages] page ids, or NULL       */
+    int32_t page_tokens;          /* paged only                                         */
+    int32_t max_pages;            /* paged only: block_table row stride                 */
 } qie_kv_cache;
 
 int qie_qkv_post(const void* qkv, int64_t M, const int32_t* pos, int32_t rows_per_seq,

@@ -63,7 +63,8 @@ class LinearArgsC(C.Structure):
 class KvCacheC(C.Structure):
     _fields_ = [("k", C.c_void_p), ("v", C.c_void_p), ("seq_stride", C.c_int64),
                 ("n_layers", C.c_int32), ("n_kv_heads", C.c_int32), ("head_dim", C.c_int32),
-                ("max_ctx", C.c_int32)]
+                ("max_ctx", C.c_int32), ("block_table", C.c_void_p), ("page_tokens", C.c_int32),
+                ("max_pages", C.c_int32)]
 
 
 class EngineOptsC(C.Structure):
@@ -143,6 +144,10 @@ SIGNATURES = [
     ("qie_engine_destroy", None, [_P]),
     ("qie_batch_create", C.c_int, [_P, _I32, _I32, C.POINTER(_P)]),
     ("qie_batch_destroy", None, [_P]),
+    ("qie_batch_create_paged", C.c_int, [_P, _I32, _I32, _I32, _I32, C.POINTER(_P)]),
+    ("qie_batch_release", C.c_int, [_P, _I32]),
+    ("qie_batch_page_stats", C.c_int, [_P, _PI32, _PI32, _PI32]),
+    ("qie_batch_block_table", C.c_int, [_P, _I32, _PI32, _I32]),
     ("qie_prefill", C.c_int, [_P, _I32, _PI32, _I32, C.POINTER(SamplingC), _PI32]),
     ("qie_decode_step", C.c_int, [_P, C.POINTER(SamplingC), _PI32]),
     ("qie_decode", C.c_int, [_P, _I32, C.POINTER(SamplingC), _PI32]),

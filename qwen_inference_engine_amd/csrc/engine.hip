@@ -97,6 +97,13 @@ struct qie_batch {
              *pf_h = nullptr;
     int32_t *pf_pos = nullptr, *pf_ids = nullptr;
     void* pf_attn_ws = nullptr;
+    // paged KV (qie_batch_create_paged): pool pages of page_tokens tokens, block table
+    // [B][max_pages] on device and host, free list, pages held per slot
+    int page_tokens = 0, max_pages = 0, n_pages = 0;
+    int32_t* d_table = nullptr;
+    std::vector<int32_t> h_table, free_pages, held;
+    std::vector<char> idle;
+    bool table_dirty = false;
     // decode graph
     hipGraphExec_t gexec = nullptr;
     qie_sampling gs{};
@@ -157,11 +164,66 @@ static int dmalloc(void** p, size_t bytes) {
     return 0;
 }
 
-#define QIE_TRY(expr)                 \
-    do {                              \
-        int _rc = (expr);             \
-        if (_rc != 0) return _rc;     \
-    } while (0)
+// KV descriptor of the batch's sequences seq0.. (kernels see them as sequences 0..)
+static qie_kv_cache batch_cache(const qie_batch* b, int seq0) {
+    const qie_engine* e = b->e;
+    qie_kv_cache c{};
+    c.n_layers = e->spec.n_layers;
+    c.n_kv_heads = e->sh.nkv;
+    c.head_dim = e->spec.head_dim;
+    c.max_ctx = b->max_ctx;
+    c.seq_stride = b->seq_stride;
+    if (b->d_table) {
+        c.k = b->kc;
+        c.v = b->vc;
+        c.block_table = b->d_table + (int64_t)seq0 * b->max_pages;
+        c.page_tokens = b->page_tokens;
+        c.max_pages = b->max_pages;
+    } else {
+        c.k = b->kc + (int64_t)seq0 * b->seq_stride;
+        c.v = b->vc + (int64_t)seq0 * b->seq_stride;
+    }
+    return c;
+}
+
+// ------------------------------------------------------------ page pool
+// Host-side allocator of the paged batch.  Decisions are deterministic, so the
+// tensor-parallel ranks (each holding its own heads' pages) stay in step.
+static int ensure_pages(qie_batch* b, int seq, int64_t ntok) {
+    if (!b->d_table) return 0;
+    const int64_t need = (ntok + b->page_tokens - 1) / b->page_tokens;
+    QIE_REQUIRE(need <= b->max_pages, "KV pages: %lld tokens exceed max_ctx %d", (long long)ntok, b->max_ctx);
+    int64_t extra = need - b->held[seq];
+    QIE_REQUIRE(extra <= (int64_t)b->free_pages.size(), "KV pages: sequence %d needs %lld more pages, %zu free",
+                seq, (long long)extra, b->free_pages.size());
+    for (; b->held[seq] < need; b->held[seq]++) {
+        b->h_table[(int64_t)seq * b->max_pages + b->held[seq]] = b->free_pages.back();
+        b->free_pages.pop_back();
+        b->table_dirty = true;
+    }
+    return 0;
+}
+
+static void drop_pages(qie_batch* b, int seq) {
+    if (!b->d_table) return;
+    for (int i = b->held[seq] - 1; i >= 0; i--) {
+        int32_t& t = b->h_table[(int64_t)seq * b->max_pages + i];
+        b->free_pages.push_back(t);
+        t = 0;   // scratch page
+    }
+    b->held[seq] = 0;
+    b->table_dirty = true;
+}
+
+// uploads the host table (ordered after everything already on the stream)
+static int flush_table(qie_batch* b) {
+    if (!b->d_table || !b->table_dirty) return 0;
+    QIE_HIP(hipStreamSynchronize(b->e->stream));
+    QIE_HIP(hipMemcpy(b->d_table, b->h_table.data(), b->h_table.size() * 4, hipMemcpyHostToDevice));
+    b->table_dirty = false;
+    return 0;
+}
+
 
 static int build_rope(qie_engine* e) {
     const int hd = e->spec.head_dim, half = hd / 2, rows = e->opts.max_ctx;
@@ -312,7 +374,7 @@ static bool fuse_attn_o(const qie_batch* b) {
     const qie_engine* e = b->e;
     const char* ev = getenv("QIE_FUSE_AO");
     if (!ev || atoi(ev) == 0) return false;
-    return b->B == 1 && e->sh.tp == 1 && !e->fp8 && (int64_t)e->sh.nq * e->spec.head_dim <= 4096 &&
+    return b->B == 1 && e->sh.tp == 1 && !e->fp8 && !b->d_table && (int64_t)e->sh.nq * e->spec.head_dim <= 4096 &&
            e->spec.hidden % 2 == 0;
 }
 
@@ -334,7 +396,7 @@ static int enqueue_layer_decode(qie_batch* b, int l) {
     hipStream_t st = e->stream;
     const int64_t H = s.hidden, hd = s.head_dim, QD = (int64_t)e->sh.nq * hd, KD = (int64_t)e->sh.nkv * hd;
     const int64_t QKVD = QD + 2 * KD, I = e->sh.ffn, B = b->B;
-    qie_kv_cache cache{b->kc, b->vc, b->seq_stride, s.n_layers, e->sh.nkv, s.head_dim, b->max_ctx};
+    const qie_kv_cache cache = batch_cache(b, 0);
 
     qie_linear_args a = lin_base(e);
     a.x = b->x_res; a.ldx = H;
@@ -814,7 +876,8 @@ void qie_engine_destroy(qie_engine* e) {
     delete e;
 }
 
-int qie_batch_create(qie_engine* e, int32_t batch, int32_t max_ctx, qie_batch** out) {
+static int batch_create(qie_engine* e, int32_t batch, int32_t max_ctx, int32_t page_tokens, int32_t n_pages,
+                        qie_batch** out) {
     QIE_REQUIRE(e && out && batch > 0 && batch <= 8 && max_ctx > 1, "qie_batch_create: bad arguments (B <= 8)");
     QIE_REQUIRE(e->have_weights, "qie_batch_create: engine has no weights");
     QIE_REQUIRE(max_ctx <= e->rope_rows, "qie_batch_create: max_ctx %d > engine max_ctx %d", max_ctx, e->rope_rows);
@@ -825,13 +888,28 @@ int qie_batch_create(qie_engine* e, int32_t batch, int32_t max_ctx, qie_batch** 
     b->max_ctx = max_ctx;
     const TpShard& sh = e->sh;
     const int64_t H = s.hidden, hd = s.head_dim, QD = (int64_t)sh.nq * hd, KD = (int64_t)sh.nkv * hd;
-    b->seq_stride = (int64_t)s.n_layers * sh.nkv * max_ctx * hd;   // this rank's kv heads only
+    int64_t n_runs = batch;   // sequences (contiguous) or pages (paged) in the K and V pools
+    if (page_tokens > 0) {
+        b->page_tokens = page_tokens;
+        b->max_pages = (max_ctx + page_tokens - 1) / page_tokens;
+        b->n_pages = n_pages > 0 ? n_pages : batch * b->max_pages + 1;
+        b->seq_stride = (int64_t)s.n_layers * sh.nkv * page_tokens * hd;   // elements per page
+        n_runs = b->n_pages;
+        b->h_table.assign((size_t)batch * b->max_pages, 0);
+        for (int p = b->n_pages - 1; p >= 1; p--) b->free_pages.push_back(p);   // page 1 handed out first
+        b->held.assign(batch, 0);
+        b->table_dirty = true;
+    } else {
+        b->seq_stride = (int64_t)s.n_layers * sh.nkv * max_ctx * hd;   // this rank's kv heads only
+    }
+    b->idle.assign(batch, 0);
     int rc = 0;
     auto A = [&](void** p, size_t bytes) {
         if (!rc) rc = dmalloc(p, bytes);
     };
-    A((void**)&b->kc, (size_t)batch * b->seq_stride * 2);
-    A((void**)&b->vc, (size_t)batch * b->seq_stride * 2);
+    A((void**)&b->kc, (size_t)n_runs * b->seq_stride * 2);
+    A((void**)&b->vc, (size_t)n_runs * b->seq_stride * 2);
+    if (page_tokens > 0) A((void**)&b->d_table, b->h_table.size() * 4);
     A((void**)&b->d_pos, batch * 4);
     A((void**)&b->d_step, batch * 4);
     A((void**)&b->d_hist, (size_t)batch * max_ctx * 4);
@@ -857,8 +935,8 @@ int qie_batch_create(qie_engine* e, int32_t batch, int32_t max_ctx, qie_batch** 
     if (!rc) {
         hipMemsetAsync(b->dec_ws, 0, (size_t)dec_ws, e->stream);
         hipMemsetAsync(b->fuse_ctr, 0, 1024, e->stream);
-        hipMemsetAsync(b->kc, 0, (size_t)batch * b->seq_stride * 2, e->stream);
-        hipMemsetAsync(b->vc, 0, (size_t)batch * b->seq_stride * 2, e->stream);
+        hipMemsetAsync(b->kc, 0, (size_t)n_runs * b->seq_stride * 2, e->stream);
+        hipMemsetAsync(b->vc, 0, (size_t)n_runs * b->seq_stride * 2, e->stream);
         hipMemsetAsync(b->d_keys, 0, batch * 8, e->stream);
         hipMemsetAsync(b->d_pos, 0, batch * 4, e->stream);
         hipMemsetAsync(b->d_step, 0, batch * 4, e->stream);
@@ -873,7 +951,57 @@ int qie_batch_create(qie_engine* e, int32_t batch, int32_t max_ctx, qie_batch** 
         return rc;
     }
     b->h_pos.assign(batch, 0);
+    if (!rc) rc = flush_table(b);
+    if (rc) {
+        qie_batch_destroy(b);
+        return rc;
+    }
     *out = b;
+    return 0;
+}
+
+int qie_batch_create(qie_engine* e, int32_t batch, int32_t max_ctx, qie_batch** out) {
+    return batch_create(e, batch, max_ctx, 0, 0, out);
+}
+
+int qie_batch_create_paged(qie_engine* e, int32_t batch, int32_t max_ctx, int32_t page_tokens, int32_t n_pages,
+                           qie_batch** out) {
+    if (page_tokens == 0) page_tokens = 128;
+    QIE_REQUIRE(page_tokens >= 128 && (page_tokens & (page_tokens - 1)) == 0,
+                "qie_batch_create_paged: page_tokens %d must be a power of two >= 128", page_tokens);
+    QIE_REQUIRE(n_pages >= 0, "qie_batch_create_paged: bad n_pages");
+    QIE_REQUIRE(n_pages == 0 || n_pages >= 2, "qie_batch_create_paged: need the scratch page and one more");
+    return batch_create(e, batch, max_ctx, page_tokens, n_pages, out);
+}
+
+int qie_batch_release(qie_batch* b, int32_t seq) {
+    QIE_REQUIRE(b && seq >= 0 && seq < b->B, "qie_batch_release: bad arguments");
+    drop_pages(b, seq);
+    b->idle[seq] = 1;
+    QIE_TRY(flush_table(b));
+    qie_engine* e = b->e;
+    hipLaunchKernelGGL(set_state_kernel, dim3(1), dim3(256), 0, e->stream, seq, 0, 0, 0, b->d_pos, b->d_step, b->d_hist,
+                       b->max_ctx, (const uint4*)e->w.embed, (uint4*)b->x_res, (int64_t)e->spec.hidden / 8, 1);
+    QIE_LAUNCH_CHECK();
+    QIE_HIP(hipStreamSynchronize(e->stream));
+    b->h_pos[seq] = 0;
+    return 0;
+}
+
+int qie_batch_page_stats(qie_batch* b, int32_t* free_pages, int32_t* pages_per_seq, int32_t* page_tokens) {
+    QIE_REQUIRE(b, "qie_batch_page_stats: null batch");
+    if (free_pages) *free_pages = (int32_t)b->free_pages.size();
+    if (pages_per_seq)
+        for (int m = 0; m < b->B; m++) pages_per_seq[m] = b->d_table ? b->held[m] : 0;
+    if (page_tokens) *page_tokens = b->page_tokens;
+    return 0;
+}
+
+int qie_batch_block_table(qie_batch* b, int32_t seq, int32_t* host_pages, int32_t n) {
+    QIE_REQUIRE(b && b->d_table && host_pages && seq >= 0 && seq < b->B && n >= 0 && n <= b->max_pages,
+                "qie_batch_block_table: bad arguments (paged batch, n <= max_pages)");
+    QIE_HIP(hipStreamSynchronize(b->e->stream));
+    QIE_HIP(hipMemcpy(host_pages, b->d_table + (int64_t)seq * b->max_pages, (size_t)n * 4, hipMemcpyDeviceToHost));
     return 0;
 }
 
@@ -881,7 +1009,7 @@ void qie_batch_destroy(qie_batch* b) {
     if (!b) return;
     if (b->e && b->e->stream) hipStreamSynchronize(b->e->stream);
     if (b->gexec) hipGraphExecDestroy(b->gexec);
-    void* ps[] = {b->kc, b->vc, b->d_pos, b->d_step, b->d_hist, b->d_ids, b->d_keys, b->x_res, b->qkv, b->q,
+    void* ps[] = {b->kc, b->vc, b->d_table, b->d_pos, b->d_step, b->d_hist, b->d_ids, b->d_keys, b->x_res, b->qkv, b->q,
                   b->att, b->h, b->logits, b->attn_ws, b->dec_ws, b->samp_ws, b->pf_x, b->pf_hn, b->pf_qkv, b->pf_q,
                   b->pf_att, b->pf_h, b->pf_pos, b->pf_ids, b->pf_attn_ws, b->part, b->logits_full,
                   b->gather_tmp, b->pf_part, b->xn, b->fuse_ctr};
@@ -899,6 +1027,10 @@ int qie_prefill(qie_batch* b, int32_t seq, const int32_t* ids, int32_t n, const 
         QIE_REQUIRE(ids[i] >= 0 && ids[i] < s.vocab, "qie_prefill: token id %d out of range", ids[i]);
     hipStream_t st = e->stream;
     QIE_TRY(ensure_prefill_scratch(b, n));
+    drop_pages(b, seq);   // a prefill starts a new sequence in the slot
+    QIE_TRY(ensure_pages(b, seq, n));
+    QIE_TRY(flush_table(b));
+    b->idle[seq] = 0;
     const TpShard& sh = e->sh;
     const int64_t H = s.hidden, hd = s.head_dim, QD = (int64_t)sh.nq * hd, KD = (int64_t)sh.nkv * hd;
     const int64_t QKVD = QD + 2 * KD, I = sh.ffn;
@@ -907,8 +1039,7 @@ int qie_prefill(qie_batch* b, int32_t seq, const int32_t* ids, int32_t n, const 
     hipLaunchKernelGGL(copy_ids_kernel, dim3((n + 255) / 256), dim3(256), 0, st, b->pf_ids,
                        b->d_hist + (int64_t)seq * b->max_ctx, n);
     QIE_TRY(qie_embedding(e->w.embed, b->pf_ids, b->pf_x, n, H, st));
-    qie_kv_cache cache{b->kc + (int64_t)seq * b->seq_stride, b->vc + (int64_t)seq * b->seq_stride, b->seq_stride,
-                       s.n_layers, sh.nkv, s.head_dim, b->max_ctx};
+    const qie_kv_cache cache = batch_cache(b, seq);
     for (int l = 0; l < s.n_layers; l++) {
         const qie_layer_weights& L = e->layers[l];
         QIE_TRY(qie_rmsnorm(b->pf_x, L.attn_norm, b->pf_hn, n, H, s.rms_eps, s.numerics, st));
@@ -980,10 +1111,40 @@ static int launch_step(qie_batch* b, const qie_sampling* smp) {
     return 0;
 }
 
+// Before n_steps decode steps: every live sequence fits max_ctx and holds the pages the
+// steps write (positions h_pos .. h_pos + n_steps - 1); idle slots are rewound to
+// position 0 when they would run past max_ctx.  Nothing is launched on failure.
+static int prepare_steps(qie_batch* b, int n_steps, const char* who) {
+    for (int m = 0; m < b->B; m++)
+        if (!b->idle[m])
+            QIE_REQUIRE(b->h_pos[m] + n_steps < b->max_ctx, "%s: sequence %d would exceed max_ctx %d", who, m,
+                        b->max_ctx);
+    if (b->d_table) {
+        int64_t need = 0;
+        for (int m = 0; m < b->B; m++)
+            if (!b->idle[m])
+                need += std::max<int64_t>(0, (b->h_pos[m] + n_steps + b->page_tokens - 1) / b->page_tokens - b->held[m]);
+        QIE_REQUIRE(need <= (int64_t)b->free_pages.size(), "%s: KV pool exhausted (%lld pages needed, %zu free)", who,
+                    (long long)need, b->free_pages.size());
+        for (int m = 0; m < b->B; m++)
+            if (!b->idle[m]) QIE_TRY(ensure_pages(b, m, b->h_pos[m] + n_steps));
+        QIE_TRY(flush_table(b));
+    }
+    qie_engine* e = b->e;
+    for (int m = 0; m < b->B; m++)
+        if (b->idle[m] && b->h_pos[m] + n_steps >= b->max_ctx) {
+            hipLaunchKernelGGL(set_state_kernel, dim3(1), dim3(256), 0, e->stream, m, 0, 0, 0, b->d_pos, b->d_step,
+                               b->d_hist, b->max_ctx, (const uint4*)e->w.embed, (uint4*)b->x_res,
+                               (int64_t)e->spec.hidden / 8, 1);
+            QIE_LAUNCH_CHECK();
+            b->h_pos[m] = 0;
+        }
+    return 0;
+}
+
 int qie_decode_step(qie_batch* b, const qie_sampling* smp, int32_t* next_ids) {
     QIE_REQUIRE(b, "qie_decode_step: null batch");
-    for (int m = 0; m < b->B; m++)
-        QIE_REQUIRE(b->h_pos[m] + 1 < b->max_ctx, "qie_decode_step: sequence %d is full (max_ctx %d)", m, b->max_ctx);
+    QIE_TRY(prepare_steps(b, 1, "qie_decode_step"));
     QIE_TRY(launch_step(b, smp));
     for (int m = 0; m < b->B; m++) b->h_pos[m] += 1;
     return sync_ids(b, next_ids);
@@ -991,9 +1152,8 @@ int qie_decode_step(qie_batch* b, const qie_sampling* smp, int32_t* next_ids) {
 
 int qie_decode(qie_batch* b, int32_t n_steps, const qie_sampling* smp, int32_t* out_ids) {
     QIE_REQUIRE(b && n_steps >= 0, "qie_decode: bad arguments");
+    QIE_TRY(prepare_steps(b, n_steps, "qie_decode"));
     std::vector<int32_t> p0 = b->h_pos;
-    for (int m = 0; m < b->B; m++)
-        QIE_REQUIRE(b->h_pos[m] + n_steps < b->max_ctx, "qie_decode: sequence %d would exceed max_ctx", m);
     for (int i = 0; i < n_steps; i++) {
         QIE_TRY(launch_step(b, smp));
         for (int m = 0; m < b->B; m++) b->h_pos[m] += 1;
@@ -1042,6 +1202,9 @@ int qie_batch_set_position(qie_batch* b, int32_t seq, int32_t pos, int32_t token
     QIE_REQUIRE(b && seq >= 0 && seq < b->B && pos >= 0 && pos + 1 < b->max_ctx && token >= 0 &&
                     token < b->e->spec.vocab,
                 "qie_batch_set_position: bad arguments");
+    QIE_TRY(ensure_pages(b, seq, (int64_t)pos + 1));
+    QIE_TRY(flush_table(b));
+    b->idle[seq] = 0;
     qie_engine* e = b->e;
     hipLaunchKernelGGL(set_state_kernel, dim3(1), dim3(256), 0, e->stream, seq, pos, pos, token, b->d_pos, b->d_step,
                        b->d_hist, b->max_ctx, (const uint4*)e->w.embed, (uint4*)b->x_res,
@@ -1097,7 +1260,7 @@ int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* av
         hipFree(scratch);
         return fail(-22, "qie_batch_time_kernel: unknown kernel %d", which);
     }
-    qie_kv_cache cache{b->kc, b->vc, b->seq_stride, s.n_layers, sh.nkv, s.head_dim, b->max_ctx};
+    const qie_kv_cache cache = batch_cache(b, 0);
     if (B >= 2 && a.norm_w && !(getenv("QIE_PRENORM") && atoi(getenv("QIE_PRENORM")) == 0)) {
         a.x = b->xn;   // as the batched step runs it: rows normed once by prenorm(), plain GEMV
         a.ldx = a.K;

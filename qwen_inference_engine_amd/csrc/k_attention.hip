@@ -18,13 +18,6 @@
 #include "qie_common.hpp"
 #include "../../include/qie/qie_ops.h"
 
-#ifndef QIE_TRY
-#define QIE_TRY(expr)                  \
-    do {                               \
-        const int _rc = (expr);        \
-        if (_rc) return _rc;           \
-    } while (0)
-#endif
 
 #include <cstdlib>
 
@@ -36,7 +29,7 @@ struct AttnParams {
     int rows_per_seq;
     const uint16_t* kc;
     const uint16_t* vc;
-    int64_t seq_stride;
+    KvMap km;
     int layer, nkv, nq, max_ctx;
     int nsplit;
     float* part_o;    // [M][nq][nsplit][HD]
@@ -46,7 +39,7 @@ struct AttnParams {
 
 constexpr int kMaxGroup = 8;
 
-template <int HD>
+template <int HD, bool PG>
 __global__ __launch_bounds__(256) void attn_split_kernel(AttnParams a) {
     constexpr int LPT = HD / 8;   // lanes per key row
     constexpr int TPW = 64 / LPT; // keys per wave step
@@ -91,13 +84,14 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnParams a) {
         for (int j = 0; j < 8; j++) o[gi][j] = 0.f;
     }
     const float scale = sqrtf((float)HD);
-    const int64_t head_off = (((int64_t)a.layer * a.nkv + g) * a.max_ctx) * HD;
-    const uint16_t* kb = a.kc + seq * a.seq_stride + head_off + dl * 8;
-    const uint16_t* vb = a.vc + seq * a.seq_stride + head_off + dl * 8;
+    const int64_t head_off = kv_run_off(a.km, (int64_t)a.layer * a.nkv + g, HD);
+    const uint16_t* kb = a.kc + head_off + dl * 8;
+    const uint16_t* vb = a.vc + head_off + dl * 8;
 
     for (int t = t0 + wave * TPW + sub; t < t1; t += 4 * TPW) {
-        uint4 kv = *reinterpret_cast<const uint4*>(kb + (int64_t)t * HD);
-        uint4 vv = *reinterpret_cast<const uint4*>(vb + (int64_t)t * HD);
+        const int64_t to = kv_tok<PG>(a.km, seq, t, HD);
+        uint4 kv = *reinterpret_cast<const uint4*>(kb + to);
+        uint4 vv = *reinterpret_cast<const uint4*>(vb + to);
         float kf[8], vf[8];
         uint32_t kw[4] = {kv.x, kv.y, kv.z, kv.w}, vw[4] = {vv.x, vv.y, vv.z, vv.w};
 #pragma unroll
@@ -222,7 +216,7 @@ struct DecodeAttnParams {
     const float* sn;
     uint16_t* kc;
     uint16_t* vc;
-    int64_t seq_stride;
+    KvMap km;
     int layer, nkv, nq, max_ctx, nsplit_max;
     int splits_target;        // ~splits per (row, kv head) at long context
     int dbg;                  // timing experiments only (QIE_DEC_DBG): 1 no combine, 2 no release, 4 no acquire,
@@ -308,9 +302,9 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnParams a) {
     const int QKVD = (a.nq + 2 * a.nkv) * HD;
     const uint16_t* row = a.qkv + m * (int64_t)QKVD;
     const bool hf = a.numerics == QIE_NUMERICS_HF;
-    const int64_t head_off = (((int64_t)a.layer * a.nkv + g) * a.max_ctx) * HD;
-    uint16_t* kb = a.kc + m * a.seq_stride + head_off;
-    uint16_t* vb = a.vc + m * a.seq_stride + head_off;
+    const int64_t head_off = kv_run_off(a.km, (int64_t)a.layer * a.nkv + g, HD);
+    uint16_t* kb = a.kc + m * a.km.stride + head_off;
+    uint16_t* vb = a.vc + m * a.km.stride + head_off;
 
     // ---------------- issue all loads.  Prologue operands first (vmcnt retires in
     // order, so waiting for them does not wait for the K/V rows).  Groups past G + 1
@@ -594,7 +588,7 @@ struct PrefillAttnParams {
     int rows_per_seq;
     const uint16_t* kc;
     const uint16_t* vc;
-    int64_t seq_stride;
+    KvMap km;
     int layer, nkv, nq, max_ctx;
     int64_t M;
     uint16_t* out;
@@ -626,9 +620,9 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(PrefillAttnParam
     const int64_t row0 = (int64_t)seq * a.rows_per_seq;
     const int rlo = qt * 64, rhi = min(a.rows_per_seq, rlo + 64);
     const int G = a.nq / a.nkv, kvh = h / G;
-    const int64_t head_off = (((int64_t)a.layer * a.nkv + kvh) * a.max_ctx) * HD;
-    const uint16_t* kb = a.kc + seq * a.seq_stride + head_off;
-    const uint16_t* vb = a.vc + seq * a.seq_stride + head_off;
+    const int64_t head_off = kv_run_off(a.km, (int64_t)a.layer * a.nkv + kvh, HD);
+    const uint16_t* kb = a.kc + seq * a.km.stride + head_off;
+    const uint16_t* vb = a.vc + seq * a.km.stride + head_off;
     const int kmax = a.pos[row0 + rhi - 1];                // last key any row of the block needs
     const int nkt = kmax / KT + 1;
 
@@ -786,7 +780,7 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(PrefillAttnParam
 // compiles with -use_fast_math, i.e. __expf / __fdividef, so the libm
 // expf and IEEE division of v1 (~25 VALU ops per score) bought nothing but VALU time.
 // A wave skips the MFMAs of a tile whose first key lies past its last row's position.
-template <int HD>
+template <int HD, bool PG>
 __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnParams a) {
     constexpr int KT = 64;
     constexpr int CPR = HD / 8;
@@ -812,9 +806,9 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
     const int64_t row0 = (int64_t)seq * a.rows_per_seq;
     const int rlo = qt * BQ, rhi = min(a.rows_per_seq, rlo + BQ);
     const int G = a.nq / a.nkv, kvh = h / G;
-    const int64_t head_off = (((int64_t)a.layer * a.nkv + kvh) * a.max_ctx) * HD;
-    const uint16_t* kb = a.kc + seq * a.seq_stride + head_off;
-    const uint16_t* vb = a.vc + seq * a.seq_stride + head_off;
+    const int64_t head_off = kv_run_off(a.km, (int64_t)a.layer * a.nkv + kvh, HD);
+    const uint16_t* kb = a.kc + head_off;
+    const uint16_t* vb = a.vc + head_off;
     const int kmax = a.pos[row0 + rhi - 1];
     const int nkt = kmax / KT + 1;
     // positions are non-decreasing within a sequence: the wave's last row bounds its keys
@@ -835,13 +829,16 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
     // left in scratch (144 B/lane) by the compiler across the loop
     kv16_t rk[LPT], rv[LPT];
     auto gload = [&](int kt) {
+        // a 64-key tile never straddles a page (page_tokens is a multiple of 128)
+        const int64_t tb = kv_tok<PG>(a.km, seq, kt * KT, HD);
 #pragma unroll
         for (int i = 0; i < LPT; i++) {
             const int c = tid + 256 * i;
             const int key = min(kt * KT + c / CPR, kmax);
             const int ch = c % CPR;
-            rk[i] = *reinterpret_cast<const kv16_t*>(kb + (int64_t)key * HD + ch * 8);
-            rv[i] = *reinterpret_cast<const kv16_t*>(vb + (int64_t)key * HD + ch * 8);
+            const int64_t o = tb + (int64_t)(key - kt * KT) * HD + ch * 8;
+            rk[i] = *reinterpret_cast<const kv16_t*>(kb + o);
+            rv[i] = *reinterpret_cast<const kv16_t*>(vb + o);
         }
     };
     auto lstore = [&](int buf) {
@@ -1029,9 +1026,9 @@ __global__ __launch_bounds__(256) void attn_decode_mfma_kernel(DecodeAttnParams 
     const int QKVD = (a.nq + 2 * a.nkv) * HD;
     const uint16_t* row = a.qkv + m * (int64_t)QKVD;
     const bool hf = a.numerics == QIE_NUMERICS_HF;
-    const int64_t head_off = (((int64_t)a.layer * a.nkv + g) * a.max_ctx) * HD;
-    uint16_t* kb = a.kc + m * a.seq_stride + head_off;
-    uint16_t* vb = a.vc + m * a.seq_stride + head_off;
+    const int64_t head_off = kv_run_off(a.km, (int64_t)a.layer * a.nkv + g, HD);
+    uint16_t* kb = a.kc + m * a.km.stride + head_off;
+    uint16_t* vb = a.vc + m * a.km.stride + head_off;
 
     // ---------------- issue all loads: prologue operands first, then step 0's K/V
     const bool is_q = grp < G, is_k = grp == G, is_v = grp == G + 1;
@@ -1387,7 +1384,7 @@ __device__ __forceinline__ DecPro dec_pro_issue(const DecodeAttnParams& a, const
 // qk-norm + RoPE of the q heads and the new k, then q -> LDS (bf16), new k/v -> cache
 // and LDS.  Branch-free (only the stores are predicated), see attn_decode_kernel.
 template <int HD>
-__device__ __forceinline__ void dec_pro_finish(const DecodeAttnParams& a, DecPro& d, int dl, int grp, int p,
+__device__ __forceinline__ void dec_pro_finish(const DecodeAttnParams& a, DecPro& d, int dl, int grp, int64_t poff,
                                                uint16_t* kb, uint16_t* vb, uint16_t (*q_s)[HD],
                                                uint16_t (*kv_new)[HD]) {
 #pragma clang fp contract(off)
@@ -1428,7 +1425,7 @@ __device__ __forceinline__ void dec_pro_finish(const DecodeAttnParams& a, DecPro
     if (d.is_q) {
         *reinterpret_cast<uint4*>(&q_s[grp][dl * 8]) = packed;
     } else if (d.pro) {
-        uint16_t* dst = (d.is_k ? kb : vb) + (int64_t)p * HD + dl * 8;
+        uint16_t* dst = (d.is_k ? kb : vb) + poff + dl * 8;
         *reinterpret_cast<uint4*>(dst) = packed;
         *reinterpret_cast<uint4*>(&kv_new[d.is_k ? 0 : 1][dl * 8]) = packed;
     }
@@ -1436,7 +1433,7 @@ __device__ __forceinline__ void dec_pro_finish(const DecodeAttnParams& a, DecPro
 
 // Body of the decode attention for workgroup (bx, by); true when this workgroup wrote a
 // combined (row, kv head) output (its stores are write-through, sc1).
-template <int HD>
+template <int HD, bool PG>
 __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a, const int bx, const int by) {
 #pragma clang fp contract(off)
     constexpr int LPT = HD / 8;          // prologue: lanes per head row
@@ -1467,9 +1464,9 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
     const int grp = tid / LPT, dl = tid % LPT;
     const int QKVD = (a.nq + 2 * a.nkv) * HD;
     const uint16_t* row = a.qkv + m * (int64_t)QKVD;
-    const int64_t head_off = (((int64_t)a.layer * a.nkv + g) * a.max_ctx) * HD;
-    uint16_t* kb = a.kc + m * a.seq_stride + head_off;
-    uint16_t* vb = a.vc + m * a.seq_stride + head_off;
+    const int64_t head_off = kv_run_off(a.km, (int64_t)a.layer * a.nkv + g, HD);
+    uint16_t* kb = a.kc + head_off;
+    uint16_t* vb = a.vc + head_off;
 
     // ---------------- loads: prologue operands, then step 0's K tiles and V slice
     DecPro pr = dec_pro_issue<HD>(a, row, g, G, grp, dl, p, has_new);
@@ -1477,22 +1474,24 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
     uint4 kf[2][KSTEPS], vr[VCH];
     auto load_step = [&](int st) {
         const int kb0 = t0 + st * kDecMStep;
+        // a 128-key step never straddles a page (chunks and pages are multiples of 128)
+        const int64_t so = kv_tok<PG>(a.km, m, kb0, HD);
 #pragma unroll
         for (int t = 0; t < 2; t++) {
             const int key = min(kb0 + 32 * wave + 16 * t + fr, t1 - 1);
 #pragma unroll
             for (int ks = 0; ks < KSTEPS; ks++)
-                kf[t][ks] = *reinterpret_cast<const uint4*>(kb + (int64_t)key * HD + 32 * ks + 8 * gq);
+                kf[t][ks] = *reinterpret_cast<const uint4*>(kb + so + (int64_t)(key - kb0) * HD + 32 * ks + 8 * gq);
         }
 #pragma unroll
         for (int i = 0; i < VCH; i++) {
             const int c = lane + 64 * i;
             const int key = min(kb0 + c / CPW, t1 - 1);
-            vr[i] = *reinterpret_cast<const uint4*>(vb + (int64_t)key * HD + wave * DW + (c % CPW) * 8);
+            vr[i] = *reinterpret_cast<const uint4*>(vb + so + (int64_t)(key - kb0) * HD + wave * DW + (c % CPW) * 8);
         }
     };
     load_step(0);
-    dec_pro_finish<HD>(a, pr, dl, grp, p, kb, vb, q_s, kv_new);
+    dec_pro_finish<HD>(a, pr, dl, grp, kv_tok<PG>(a.km, m, p, HD), kb, vb, q_s, kv_new);
     for (int idx = tid; idx < (16 - G) * CPR; idx += 256)   // padded q rows
         *reinterpret_cast<uint4*>(&q_s[G + idx / CPR][(idx % CPR) * 8]) = make_uint4(0, 0, 0, 0);
     __syncthreads();
@@ -1709,9 +1708,9 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
     return true;
 }
 
-template <int HD>
+template <int HD, bool PG>
 __global__ __launch_bounds__(256) void attn_decode_mfma2_kernel(DecodeAttnParams a) {
-    attn_decode_mfma2_body<HD>(a, blockIdx.x, blockIdx.y);
+    attn_decode_mfma2_body<HD, PG>(a, blockIdx.x, blockIdx.y);
 }
 
 // ---------------------------------------------------------------------------
@@ -1751,7 +1750,7 @@ __global__ __launch_bounds__(256) void attn_o_fused_kernel(DecodeAttnParams a, A
     __syncthreads();
     const int t = role_s;
     if (t < o.n_attn) {
-        if (attn_decode_mfma2_body<HD>(a, t, 0)) {
+        if (attn_decode_mfma2_body<HD, false>(a, t, 0)) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
             __syncthreads();
             if (tid == 0) {
@@ -1878,7 +1877,7 @@ static int fill_dec_params(DecodeAttnParams& a, const void* qkv, int64_t B, cons
     a.sn = rope_sin;
     a.kc = (uint16_t*)cache->k;
     a.vc = (uint16_t*)cache->v;
-    a.seq_stride = cache->seq_stride;
+    QIE_TRY(kv_map_make(cache, &a.km, "qie_attention_decode"));
     a.layer = layer;
     a.nkv = cache->n_kv_heads;
     a.nq = n_heads;
@@ -1932,7 +1931,7 @@ int qie_attention(const void* q, int64_t M, const int32_t* pos, int32_t rows_per
         pa.rows_per_seq = rows_per_seq;
         pa.kc = (const uint16_t*)cache->k;
         pa.vc = (const uint16_t*)cache->v;
-        pa.seq_stride = cache->seq_stride;
+        QIE_TRY(kv_map_make(cache, &pa.km, "qie_attention"));
         pa.layer = layer;
         pa.nkv = cache->n_kv_heads;
         pa.nq = n_heads;
@@ -1941,12 +1940,12 @@ int qie_attention(const void* q, int64_t M, const int32_t* pos, int32_t rows_per
         pa.out = (uint16_t*)out;
         pa.no_tr = getenv("QIE_ATTN_NO_TR") ? 1 : 0;
         const size_t shm = (size_t)2 * 2 * 64 * cache->head_dim * 2;
-        if (!getenv("QIE_ATTN_PREFILL_V1") && !pa.no_tr) {   // v1: A/B timing and diagnostics only
+        const bool pg = pa.km.table != nullptr;
+        if ((!getenv("QIE_ATTN_PREFILL_V1") && !pa.no_tr) || pg) {   // v1: A/B timing and diagnostics only
             dim3 g2((unsigned)((rows_per_seq + 127) / 128), (unsigned)n_heads, (unsigned)(M / rows_per_seq));
-            if (cache->head_dim == 128)
-                hipLaunchKernelGGL(attn_prefill_mfma2_kernel<128>, g2, dim3(256), shm, (hipStream_t)stream, pa);
-            else
-                hipLaunchKernelGGL(attn_prefill_mfma2_kernel<64>, g2, dim3(256), shm, (hipStream_t)stream, pa);
+            auto k2 = cache->head_dim == 128 ? (pg ? attn_prefill_mfma2_kernel<128, true> : attn_prefill_mfma2_kernel<128, false>)
+                                             : (pg ? attn_prefill_mfma2_kernel<64, true> : attn_prefill_mfma2_kernel<64, false>);
+            hipLaunchKernelGGL(k2, g2, dim3(256), shm, (hipStream_t)stream, pa);
             QIE_LAUNCH_CHECK();
             return 0;
         }
@@ -1964,7 +1963,7 @@ int qie_attention(const void* q, int64_t M, const int32_t* pos, int32_t rows_per
     a.rows_per_seq = rows_per_seq;
     a.kc = (const uint16_t*)cache->k;
     a.vc = (const uint16_t*)cache->v;
-    a.seq_stride = cache->seq_stride;
+    QIE_TRY(kv_map_make(cache, &a.km, "qie_attention"));
     a.layer = layer;
     a.nkv = cache->n_kv_heads;
     a.nq = n_heads;
@@ -1977,12 +1976,13 @@ int qie_attention(const void* q, int64_t M, const int32_t* pos, int32_t rows_per
     QIE_REQUIRE(a.nsplit == 1 || ws, "qie_attention: workspace required");
     hipStream_t st = (hipStream_t)stream;
     dim3 grid((unsigned)(a.nkv * a.nsplit), (unsigned)M);
+    const bool pg = a.km.table != nullptr;
     if (cache->head_dim == 128) {
-        hipLaunchKernelGGL(attn_split_kernel<128>, grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL((pg ? attn_split_kernel<128, true> : attn_split_kernel<128, false>), grid, dim3(256), 0, st, a);
         QIE_LAUNCH_CHECK();
         if (a.nsplit > 1) hipLaunchKernelGGL(attn_combine_kernel<128>, dim3(n_heads, (unsigned)M), dim3(128), 0, st, a);
     } else {
-        hipLaunchKernelGGL(attn_split_kernel<64>, grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL((pg ? attn_split_kernel<64, true> : attn_split_kernel<64, false>), grid, dim3(256), 0, st, a);
         QIE_LAUNCH_CHECK();
         if (a.nsplit > 1) hipLaunchKernelGGL(attn_combine_kernel<64>, dim3(n_heads, (unsigned)M), dim3(64), 0, st, a);
     }
@@ -2031,11 +2031,11 @@ int qie_attention_decode(const void* qkv, int64_t B, const int32_t* pos, const v
                                      attn_decode_kernel<64, 5>, attn_decode_kernel<64, 6>,
                                      attn_decode_kernel<64, 7>, attn_decode_kernel<64, 8>};
     const bool v1 = getenv("QIE_DEC_MFMA1") && atoi(getenv("QIE_DEC_MFMA1")) != 0;   // A/B timing only
-    if (!valu && !v1) {
-        if (cache->head_dim == 128)
-            hipLaunchKernelGGL(attn_decode_mfma2_kernel<128>, grid, dim3(256), 0, (hipStream_t)stream, a);
-        else
-            hipLaunchKernelGGL(attn_decode_mfma2_kernel<64>, grid, dim3(256), 0, (hipStream_t)stream, a);
+    const bool pg = a.km.table != nullptr;
+    if ((!valu && !v1) || pg) {   // the legacy A/B kernels address contiguous caches only
+        auto k2 = cache->head_dim == 128 ? (pg ? attn_decode_mfma2_kernel<128, true> : attn_decode_mfma2_kernel<128, false>)
+                                         : (pg ? attn_decode_mfma2_kernel<64, true> : attn_decode_mfma2_kernel<64, false>);
+        hipLaunchKernelGGL(k2, grid, dim3(256), 0, (hipStream_t)stream, a);
     } else if (!valu) {
         if (cache->head_dim == 128)
             hipLaunchKernelGGL(attn_decode_mfma_kernel<128>, grid, dim3(256), 0, (hipStream_t)stream, a);
@@ -2068,6 +2068,7 @@ int attention_o_fused(const void* qkv, const int32_t* pos, const void* q_norm, c
     DecodeAttnParams a;
     QIE_TRY(fill_dec_params(a, qkv, 1, pos, q_norm, k_norm, rope_cos, rope_sin, n_heads, cache, layer, eps, numerics,
                             att_out, ws));
+    QIE_REQUIRE(!a.km.table, "attention_o_fused: contiguous KV caches only");
     a.fused = 1;
     AttnOParams o;
     o.wo = (const uint16_t*)wo;

@@ -141,13 +141,14 @@ struct QkvPostArgs {
     int nq, nkv, hd;
     uint16_t* kc;
     uint16_t* vc;
-    int64_t seq_stride;
-    int layer, max_ctx;
+    KvMap km;
+    int layer;
     float eps;
     int numerics;
     uint16_t* q_out;
 };
 
+template <bool PG>
 __global__ __launch_bounds__(256) void qkv_post_kernel(QkvPostArgs a) {
 #pragma clang fp contract(off)
     const int64_t m = blockIdx.x;
@@ -176,14 +177,12 @@ __global__ __launch_bounds__(256) void qkv_post_kernel(QkvPostArgs a) {
         } else if (h < a.nq + a.nkv) {
             const int g = h - a.nq;
             src = row + QD + g * hd;
-            dst = a.kc + seq * a.seq_stride +
-                  (((int64_t)a.layer * a.nkv + g) * a.max_ctx + p) * (int64_t)hd;
+            dst = a.kc + kv_run_off(a.km, (int64_t)a.layer * a.nkv + g, hd) + kv_tok<PG>(a.km, seq, p, hd);
             nw = a.k_norm;
         } else {
             const int g = h - a.nq - a.nkv;
             src = row + QD + KD + g * hd;
-            dst = a.vc + seq * a.seq_stride +
-                  (((int64_t)a.layer * a.nkv + g) * a.max_ctx + p) * (int64_t)hd;
+            dst = a.vc + kv_run_off(a.km, (int64_t)a.layer * a.nkv + g, hd) + kv_tok<PG>(a.km, seq, p, hd);
             rope = false;
         }
         float x0 = active ? bf2f(src[i0]) : 0.f;
@@ -345,6 +344,34 @@ static inline uint16_t host_f2bf(float f) {
 
 using namespace qie;
 
+namespace qie {
+int kv_map_make(const qie_kv_cache* c, KvMap* out, const char* who) {
+    QIE_REQUIRE(c && c->k && c->v && c->n_layers > 0 && c->n_kv_heads > 0 && c->head_dim > 0 && c->max_ctx > 0,
+                "%s: bad KV cache descriptor", who);
+    const int64_t lh = (int64_t)c->n_layers * c->n_kv_heads * c->head_dim;
+    KvMap m{};
+    if (c->block_table) {
+        const int T = c->page_tokens;
+        QIE_REQUIRE(T >= 128 && (T & (T - 1)) == 0, "%s: page_tokens %d must be a power of two >= 128", who, T);
+        QIE_REQUIRE(c->max_pages >= (c->max_ctx + T - 1) / T, "%s: max_pages %d < ceil(max_ctx %d / %d)", who,
+                    c->max_pages, c->max_ctx, T);
+        QIE_REQUIRE(c->seq_stride >= lh * T, "%s: page stride %lld < one page", who, (long long)c->seq_stride);
+        m.table = c->block_table;
+        m.run = T;
+        m.shift = __builtin_ctz((unsigned)T);
+        m.max_pages = c->max_pages;
+    } else {
+        m.table = nullptr;
+        m.run = c->max_ctx;
+        m.shift = 0;
+        m.max_pages = 0;
+    }
+    m.stride = c->seq_stride;
+    *out = m;
+    return 0;
+}
+}  // namespace qie
+
 extern "C" {
 
 const char* qie_last_error(void) { return g_last_error.c_str(); }
@@ -466,13 +493,13 @@ int qie_qkv_post(const void* qkv, int64_t M, const int32_t* pos, int32_t rows_pe
     a.hd = cache->head_dim;
     a.kc = (uint16_t*)cache->k;
     a.vc = (uint16_t*)cache->v;
-    a.seq_stride = cache->seq_stride;
+    QIE_TRY(kv_map_make(cache, &a.km, "qie_qkv_post"));
     a.layer = layer;
-    a.max_ctx = cache->max_ctx;
     a.eps = eps;
     a.numerics = numerics;
     a.q_out = (uint16_t*)q_out;
-    hipLaunchKernelGGL(qkv_post_kernel, dim3((unsigned)M), dim3(256), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL((a.km.table ? qkv_post_kernel<true> : qkv_post_kernel<false>), dim3((unsigned)M), dim3(256), 0,
+                       (hipStream_t)stream, a);
     QIE_LAUNCH_CHECK();
     return 0;
 }

@@ -8,6 +8,8 @@
 
 #include "../../include/qie/qie_types.h"
 
+struct qie_kv_cache;
+
 namespace qie {
 
 // ----------------------------------------------------------------- errors
@@ -34,6 +36,14 @@ int fail(int code, const char* fmt, ...);
     do {                                                                       \
         if (!(cond)) return ::qie::fail(-22, __VA_ARGS__);                     \
     } while (0)
+
+#ifndef QIE_TRY
+#define QIE_TRY(expr)                                                          \
+    do {                                                                       \
+        const int _rc = (expr);                                                \
+        if (_rc) return _rc;                                                   \
+    } while (0)
+#endif
 
 constexpr int kWave = 64;
 
@@ -114,6 +124,35 @@ __device__ __forceinline__ const T* launder_ptr(const T* p) {
 __device__ __forceinline__ uint64_t launder_u64(uint64_t v) {
     asm volatile("" : "+v"(v));
     return v;
+}
+
+// ------------------------------------------------------- KV cache addressing
+// qie_kv_cache in kernel form.  A (layer, kv head) run holds `run` consecutive tokens:
+// max_ctx of one sequence (contiguous) or page_tokens of one page (paged).  The run of
+// (lg = layer*nkv + kv head) starts at base + lg*run*hd; kv_tok adds the offset of
+// token `tok` of sequence `seq` (paged: through the block table, page = tok >> shift).
+struct KvMap {
+    const int32_t* table;   // paged: [n_seq][max_pages]; null: contiguous
+    int64_t stride;         // elements between sequences (contiguous) / pages (paged)
+    int run;                // tokens per (layer, kv head) run
+    int shift;              // paged: log2(page_tokens)
+    int max_pages;
+};
+
+template <bool PG>
+__device__ __forceinline__ int64_t kv_tok(const KvMap& k, int64_t seq, int tok, int hd) {
+    if constexpr (PG)
+        return (int64_t)k.table[seq * k.max_pages + (tok >> k.shift)] * k.stride +
+               (int64_t)(tok & ((1 << k.shift) - 1)) * hd;
+    else
+        return seq * k.stride + (int64_t)tok * hd;
+}
+// Validated KvMap of a public cache descriptor (k_misc.hip); `who` names the caller.
+int kv_map_make(const qie_kv_cache* c, KvMap* out, const char* who);
+
+// run-relative offset of the first element of (layer, kv head) lg
+__host__ __device__ __forceinline__ int64_t kv_run_off(const KvMap& k, int64_t lg, int hd) {
+    return lg * k.run * (int64_t)hd;
 }
 
 // ------------------------------------------------------ cross-lane reductions

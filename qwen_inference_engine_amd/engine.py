@@ -146,8 +146,11 @@ class Engine:
     def sync(self) -> None:
         _lib.check(self.lib.qie_engine_sync(self.h), "qie_engine_sync")
 
-    def batch(self, batch: int = 1, max_ctx: Optional[int] = None) -> "Batch":
-        return Batch(self, batch, max_ctx or self.max_ctx)
+    def batch(self, batch: int = 1, max_ctx: Optional[int] = None, page_tokens: Optional[int] = None,
+              n_pages: int = 0) -> "Batch":
+        """B sequence slots.  page_tokens selects the paged KV cache (device block table over
+        a pool of n_pages pages, 0 = enough for every slot at max_ctx); None = contiguous."""
+        return Batch(self, batch, max_ctx or self.max_ctx, page_tokens, n_pages)
 
     def close(self) -> None:
         if getattr(self, "h", None):
@@ -162,13 +165,19 @@ class Engine:
 
 
 class Batch:
-    def __init__(self, engine: Engine, batch: int, max_ctx: int):
+    def __init__(self, engine: Engine, batch: int, max_ctx: int, page_tokens: Optional[int] = None,
+                 n_pages: int = 0):
         self.e = engine
         self.lib = engine.lib
         self.B = batch
         self.max_ctx = max_ctx
+        self.paged = page_tokens is not None
         h = C.c_void_p()
-        _lib.check(self.lib.qie_batch_create(engine.h, batch, max_ctx, C.byref(h)), "qie_batch_create")
+        if self.paged:
+            _lib.check(self.lib.qie_batch_create_paged(engine.h, batch, max_ctx, page_tokens, n_pages, C.byref(h)),
+                       "qie_batch_create_paged")
+        else:
+            _lib.check(self.lib.qie_batch_create(engine.h, batch, max_ctx, C.byref(h)), "qie_batch_create")
         self.h = h
 
     def prefill(self, seq: int, ids: Sequence[int], sampling: Sampling = GREEDY) -> int:
@@ -210,6 +219,24 @@ class Batch:
 
     def set_position(self, seq: int, pos: int, token: int) -> None:
         _lib.check(self.lib.qie_batch_set_position(self.h, seq, pos, token), "qie_batch_set_position")
+
+    def release(self, seq: int) -> None:
+        """End sequence `seq`: its KV pages return to the pool; the slot idles until the next prefill."""
+        _lib.check(self.lib.qie_batch_release(self.h, seq), "qie_batch_release")
+
+    def page_stats(self):
+        """(free pages, pages held per slot, page_tokens); zeros for a contiguous batch."""
+        free, pt = C.c_int32(), C.c_int32()
+        per = np.zeros(self.B, dtype=np.int32)
+        _lib.check(self.lib.qie_batch_page_stats(self.h, C.byref(free), per.ctypes.data_as(C.POINTER(C.c_int32)),
+                                                 C.byref(pt)), "qie_batch_page_stats")
+        return free.value, per, pt.value
+
+    def block_table(self, seq: int, n: int) -> np.ndarray:
+        out = np.zeros(n, dtype=np.int32)
+        _lib.check(self.lib.qie_batch_block_table(self.h, seq, out.ctypes.data_as(C.POINTER(C.c_int32)), n),
+                   "qie_batch_block_table")
+        return out
 
     def time_kernel(self, which: int = 0, iters: int = 20):
         us, by = C.c_double(), C.c_double()

@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--cpu-decode", type=int, default=8)
     ap.add_argument("--fp8", action="store_true",
                     help="linear weights + lm_head as OCP e4m3 with power-of-two row scales")
+    ap.add_argument("--page-tokens", type=int, default=0,
+                    help="paged KV cache (device block table) with pages of this many tokens; 0 = contiguous")
     ap.add_argument("--tp", action="store_true",
                     help="tensor-parallel over all ranks (RCCL) instead of independent replicas")
     return ap.parse_args()
@@ -72,7 +74,7 @@ def main():
         comm = Q.Comm.rccl(bytes.fromhex(uid), world, rank, local)
     eng = Q.Engine(spec, device=local, max_ctx=max_ctx, use_graph=not a.no_graph, comm=comm, weight_fp8=a.fp8)
     eng.init_synthetic(W.SynthParams(seed=0))
-    batch = eng.batch(B, max_ctx)
+    batch = eng.batch(B, max_ctx, page_tokens=a.page_tokens or None)
     prompts = np.random.default_rng(1 + rank).integers(0, spec.vocab, size=(B, P), dtype=np.int32)
 
     # ---------------- prefill (first call warms up; best of the timed ones)
@@ -136,7 +138,7 @@ def main():
         "config": {"workload": f"{spec.name} {'fp8' if a.fp8 else 'bf16'} decode, batch={B}, prompt={P}, gen={a.gen}",
                    "batch_per_gpu": B, "prompt": P, "gen": a.gen,
                    "parallelism": (f"tp{world}" if comm else f"replicas{world}") if world > 1 else "single",
-                   "graph": not a.no_graph},
+                   "graph": not a.no_graph, "kv": f"paged{a.page_tokens}" if a.page_tokens else "contiguous"},
         "prefill_tok_s": round(prefill_tok_s, 1),
         "prefill_ms": round(t_prefill * 1e3, 3),
         "roofline": {"bound": "hbm", "kernel": "gate_up_gemv (rms + gate/up GEMV + SwiGLU, layer 0)",

@@ -135,4 +135,28 @@ inline int llm(batch_metadata* seq, const qie_sampling* sampling = nullptr) {
 
 inline void destroy_sequence(batch_metadata* s) { delete s; }
 
+// Page list (iengine.cuh:39-49, iengine.cu:73-109).  The reference gives each sequence a
+// linked list of 4-token pages in managed memory (create_page_list, then
+// allocate_page_buffers per node as the sequence grows, free_page_list at the end).  In
+// qie every slot of a paged batch (qie_batch_create_paged) draws pages on demand from
+// one pool behind a device block table, so a page_table here is only the slot's handle:
+// create_page_list reserves nothing up front, free_page_list returns the slot's pages.
+struct page_table {
+    qie_batch* batch = nullptr;
+    int slot = 0;
+};
+
+inline page_table* create_page_list(qie_batch* paged_batch, int slot) {
+    auto* p = new page_table();
+    p->batch = paged_batch;
+    p->slot = slot;
+    return p;
+}
+
+inline void free_page_list(page_table* head) {
+    if (!head) return;
+    if (qie_batch_release(head->batch, head->slot) != 0) std::fprintf(stderr, "free_page_list: %s\n", qie_last_error());
+    delete head;
+}
+
 }  // namespace qie_compat

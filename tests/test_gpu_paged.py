@@ -240,3 +240,32 @@ def test_paged_release_reuse_and_exhaustion():
     with pytest.raises(_lib.QieError):
         small.decode(40)   # would cross into a second page: pool exhausted, nothing launched
     assert small.positions()[0] == 103
+
+
+def test_continuous_batcher_matches_isolated_runs():
+    """The serving loop (qwen_inference_engine_amd.scheduler): 6 requests through 3 slots of
+    a paged batch whose pool (5 usable pages) holds fewer than all of them, so requests
+    wait, join mid-run and reuse released pages.  Slot rows are independent, so every
+    request's tokens must equal — bit for bit — the same request run alone in slot 0 of
+    a fresh 3-slot contiguous batch."""
+    from qwen_inference_engine_amd.scheduler import ContinuousBatcher
+    eng = Q.Engine(SPEC, max_ctx=512).init_synthetic(SYN)
+    lens = [30, 150, 7, 90, 200, 60]
+    new = [40, 20, 100, 1, 30, 64]
+    prompts = [list(rng(50 + i).integers(0, SPEC.vocab, n)) for i, n in enumerate(lens)]
+    cb = ContinuousBatcher(eng, slots=3, max_ctx=512, page_tokens=128, n_pages=6)
+    rids = [cb.submit(p, n) for p, n in zip(prompts, new)]
+    saw_wait = False
+    while not cb.idle():
+        cb.step()
+        saw_wait |= len(cb.waiting) > 0 and any(s is not None for s in cb.slots)
+    got = {rid: cb.requests[rid].tokens for rid in rids}
+    assert saw_wait
+    assert cb.batch.page_stats()[0] == 5 and cb.budget == 5    # every page back in the pool
+    for rid, p, n in zip(rids, prompts, new):
+        b = eng.batch(3, 512)
+        want = [b.prefill(0, p)]
+        while len(want) < n:
+            want.append(b.decode_step()[0])
+        b.close()
+        assert got[rid] == want, f"request {rid}"

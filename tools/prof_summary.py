@@ -17,8 +17,8 @@ ROLE = {
     "gemv_kernel<1, 2, 0, 8, 2, 0, 576> [g 256 x 576]": "decode QKV GEMV (+RMSNorm, bias), one block per CU",
     "gemv_kernel<1, 2, 1, 8, 2, 0, 576> [g 256 x 448]": "decode O-proj GEMV (+residual), one block per CU",
     "gemv_kernel<1, 2, 0, 8, 2, 0, 256> [g 761 x 256]": "lm_head GEMV (+final RMSNorm, arg-max keys)",
-    "attn_decode_mfma2_kernel<128>": "decode attention (fused qk-norm/RoPE/KV append, split-K, in-launch combine)",
-    "attn_prefill_mfma2_kernel<128>": "prefill flash attention (MFMA, 32 rows/wave)",
+    "attn_decode_mfma2_kernel<128, false>": "decode attention (fused qk-norm/RoPE/KV append, split-K, in-launch combine)",
+    "attn_prefill_mfma2_kernel<128, false>": "prefill flash attention (MFMA, 32 rows/wave)",
     "gemm_big_kernel<2, 256>": "prefill gate/up GEMM (256x256 LDS-DMA, SwiGLU)",
     "gemm_big_kernel<1, 128>": "prefill O / down GEMM (256x128 LDS-DMA, +residual)",
     "gemm_kernel<0, 0>": "prefill QKV GEMM (128x128, +bias)",

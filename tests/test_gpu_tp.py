@@ -159,3 +159,26 @@ def test_rccl_single_rank_communicator():
     G.check(lib.qie_synchronize())
     assert np.array_equal(G.host(d), x)
     c.close()
+
+
+def test_tp_paged_equals_contiguous():
+    """Tensor-parallel ranks each hold their kv heads' pages; the per-rank allocators make
+    the same decisions, and a paged batch generates what a contiguous one does, bit for bit
+    (crossing a 128-token page during the run)."""
+    spec, world = CONFIGS["qwen3-qknorm-hd128"]
+    prompts = [list(rng(7 + i).integers(0, spec.vocab, n)) for i, n in enumerate([120, 40])]
+
+    def fn(rank, comm):
+        eng = Q.Engine(spec, max_ctx=256, comm=comm).init_synthetic(SYN)
+        out = []
+        for pt in (None, 128):
+            b = eng.batch(2, 256, page_tokens=pt)
+            first = [b.prefill(s, p) for s, p in enumerate(prompts)]
+            out.append((first, b.decode(20).tolist(), b.logits()))
+            b.close()
+        return out
+    res = run_ranks(world, fn)
+    for r in range(world):
+        (f0, d0, l0), (f1, d1, l1) = res[r]
+        assert f0 == f1 and d0 == d1 and np.array_equal(l0, l1)
+    assert res[0][1][1] == res[1][1][1]

@@ -4,7 +4,13 @@
 //
 //   qie_cli [--model Qwen2-7B|Qwen2-0.5B|Qwen2-72B|Qwen3-14B] [--numerics ref|hf]
 //           [--weights weights.bin --meta meta_data.txt | --synthetic SEED]
-//           [--prompt 151643,785,...] [--gen N] [--greedy] [--device D] [--no-graph]
+//           [--prompt 151643,785,... | --prompt-file ids.txt] [--gen N] [--greedy] [--device D]
+//           [--no-graph] [--stream] [--page-tokens T]
+//
+// --prompt-file: token ids separated by commas / whitespace (the reference hard-codes them,
+// iengine.cu:325, after tokenising with temp.py:4); --stream prints each id as it is
+// generated (the reference prints per step, qwen_main.cu:392-398); --page-tokens runs on a
+// paged KV cache (qie_batch_create_paged).
 //
 // Defaults follow the reference: Qwen3-14B dims, prompt ids
 // {151643,785,4767,315,279,3639,4180,374} (iengine.cu:325), reference sampling
@@ -13,6 +19,7 @@
 // getchar() between steps and the loop ends.
 #include <chrono>
 #include <cstdio>
+#include <fstream>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -43,7 +50,7 @@ int main(int argc, char** argv) {
     std::string model = "Qwen3-14B", weights, meta, numerics = "ref";
     std::vector<int> prompt = {151643, 785, 4767, 315, 279, 3639, 4180, 374};
     long seed = -1;
-    int gen = 32, device = 0, greedy = 0, graph = 1;
+    int gen = 32, device = 0, greedy = 0, graph = 1, stream = 0, page_tokens = 0;
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
         auto next = [&]() -> std::string {
@@ -59,6 +66,22 @@ int main(int argc, char** argv) {
         else if (a == "--device") device = std::atoi(next().c_str());
         else if (a == "--greedy") greedy = 1;
         else if (a == "--no-graph") graph = 0;
+        else if (a == "--stream") stream = 1;
+        else if (a == "--page-tokens") page_tokens = std::atoi(next().c_str());
+        else if (a == "--prompt-file") {
+            std::ifstream f(next());
+            if (!f) { std::fprintf(stderr, "cannot read %s\n", argv[i]); return 2; }
+            prompt.clear();
+            std::string tokstr;
+            char c;
+            auto flush = [&]() { if (!tokstr.empty()) prompt.push_back(std::atoi(tokstr.c_str())); tokstr.clear(); };
+            while (f.get(c)) {
+                if (c >= '0' && c <= '9') tokstr += c;
+                else flush();
+            }
+            flush();
+            if (prompt.empty()) { std::fprintf(stderr, "no token ids in %s\n", argv[i]); return 2; }
+        }
         else if (a == "--prompt") {
             prompt.clear();
             std::string p = next();
@@ -101,7 +124,9 @@ int main(int argc, char** argv) {
     std::printf("weights ready in %.2f s (%s)\n", std::chrono::duration<double>(t1 - t0).count(),
                 weights.empty() ? "synthetic" : weights.c_str());
     qie_batch* b = nullptr;
-    if (qie_batch_create(e, 1, opts.max_ctx, &b)) { std::fprintf(stderr, "%s\n", qie_last_error()); return 1; }
+    const int brc = page_tokens > 0 ? qie_batch_create_paged(e, 1, opts.max_ctx, page_tokens, 0, &b)
+                                    : qie_batch_create(e, 1, opts.max_ctx, &b);
+    if (brc) { std::fprintf(stderr, "%s\n", qie_last_error()); return 1; }
     batch_metadata* seq = create_new_sequence(0, prompt.data(), (int)prompt.size(), b, 0);
     qie_sampling g{1, 1.0f, 1.0f, 0};
     std::vector<int> out;
@@ -110,6 +135,7 @@ int main(int argc, char** argv) {
     auto tp1 = std::chrono::steady_clock::now();
     if (tok < 0) return 1;
     out.push_back(tok);
+    if (stream) { std::printf("%d\n", tok); std::fflush(stdout); }
     seq->step++;                 // iengine.cu:419-421
     seq->generated_token = tok;
     seq->state = decode;
@@ -117,6 +143,7 @@ int main(int argc, char** argv) {
         tok = llm(seq, greedy ? &g : nullptr);
         if (tok < 0) return 1;
         out.push_back(tok);
+        if (stream) { std::printf("%d\n", tok); std::fflush(stdout); }
         seq->step++;
         seq->generated_token = tok;
     }

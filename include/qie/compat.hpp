@@ -19,6 +19,8 @@
 #include <cstddef>
 #include <cstdint>
 #include <cstdio>
+#include <cstring>
+#include <fstream>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -123,8 +125,16 @@ inline int llm(batch_metadata* seq, const qie_sampling* sampling = nullptr) {
         }
         return tok;
     }
+    // qie_decode_step advances every slot of the batch; the reference's llm steps only
+    // `seq`, so a B > 1 batch would silently skip tokens of its other sequences.
+    int32_t nb = 0;
+    if (qie_batch_dims(seq->batch, &nb, nullptr) != 0 || nb != 1) {
+        std::fprintf(stderr, "llm(decode): needs a batch of one slot (got %d); step B > 1 batches with "
+                             "qie_decode_step, which returns every slot's token\n", nb);
+        return -1;
+    }
     qie_sampling s = sampling ? *sampling : reference_sampling(decode);
-    std::vector<int32_t> ids(64);
+    std::vector<int32_t> ids(8);
     if (qie_decode_step(seq->batch, &s, ids.data()) != 0) {
         std::fprintf(stderr, "llm(decode): %s\n", qie_last_error());
         return -1;
@@ -138,17 +148,19 @@ inline void destroy_sequence(batch_metadata* s) { delete s; }
 // Page list (iengine.cuh:39-49, iengine.cu:73-109).  The reference gives each sequence a
 // linked list of 4-token pages in managed memory (create_page_list, then
 // allocate_page_buffers per node as the sequence grows, free_page_list at the end).  In
-// qie every slot of a paged batch (qie_batch_create_paged) draws pages on demand from
-// one pool behind a device block table, so a page_table here is only the slot's handle:
-// create_page_list reserves nothing up front, free_page_list returns the slot's pages.
+// qie every slot of a batch (paged: qie_batch_create_paged) draws pages from one pool
+// behind a device block table, so a page_table here is the slot's handle:
+// create_page_list reserves nothing up front, allocate_page_buffers grows the slot by
+// one reference page's worth of positions, free_page_list returns the slot's pages.
 struct page_table {
     qie_batch* batch = nullptr;
     int slot = 0;
+    int tokens = 0;   // positions reserved so far (allocate_page_buffers / kv writes)
 };
 
-inline page_table* create_page_list(qie_batch* paged_batch, int slot) {
+inline page_table* create_page_list(qie_batch* batch, int slot) {
     auto* p = new page_table();
-    p->batch = paged_batch;
+    p->batch = batch;
     p->slot = slot;
     return p;
 }
@@ -157,6 +169,344 @@ inline void free_page_list(page_table* head) {
     if (!head) return;
     if (qie_batch_release(head->batch, head->slot) != 0) std::fprintf(stderr, "free_page_list: %s\n", qie_last_error());
     delete head;
+}
+
+// ===================================================================== operator tier
+// The reference's per-op host API (helpers.cuh:45-166, include_cuda.cu:165-279,
+// utills.cu:4-205) over qie_ops.h, so a host that keeps the reference's own layer loop
+// (qwen_main.cu:77-241 prefill, :271-359 decode) can be re-pointed op by op.
+//   * bf16 tensors are device pointers to bf16 bits (uint16_t); no CUDA types.
+//   * every launch goes to config().stream (default: the null stream, the reference's
+//     legacy default-stream ordering); failures print qie_last_error() to stderr like
+//     the reference's launch checks and set config().error.
+//   * the reference hard-codes eps 1e-4 for rmsNorm and qkNorm (normalization.cu:19,
+//     qk_norm.cu:70) and its model constants (utills.cu:8-16); here eps and numerics
+//     come from config() (defaults: 1e-4, REF) and dims from the engine's spec.
+using bf16 = uint16_t;
+
+struct Config {
+    float rms_eps = 1e-4f;
+    float qk_eps = 1e-4f;
+    int32_t numerics = QIE_NUMERICS_REF;
+    void* stream = nullptr;
+    int error = 0;        // last non-zero qie return code seen by a launch_* wrapper
+};
+inline Config& config() {
+    static Config c;
+    return c;
+}
+inline void check_(int rc, const char* who) {
+    if (rc != 0) {
+        config().error = rc;
+        std::fprintf(stderr, "%s: %s\n", who, qie_last_error());
+    }
+}
+
+// Device scratch the reference's launch helpers allocate per call (d_token in
+// sample_topk_bf16, smem in launch_attn): positions, attention / sampling workspace.
+struct Scratch {
+    void* p = nullptr;
+    int64_t bytes = 0;
+    void* get(int64_t n) {   // never NULL on success (a zero-byte request still gets 256 B)
+        n = n < 256 ? 256 : n;
+        if (n > bytes) {
+            if (p) qie_free(p);
+            p = nullptr;
+            bytes = 0;
+            if (qie_malloc(&p, n) != 0) return nullptr;
+            bytes = n;
+        }
+        return p;
+    }
+    ~Scratch() {
+        if (p) qie_free(p);
+    }
+};
+inline Scratch& scratch(int which) {
+    static Scratch s[3];   // 0: positions, 1: attention ws, 2: sampling ws + token
+    return s[which];
+}
+
+// assign_weight_pointer / load_weight (helpers.cuh:19-35): W = arena + data_offsets[0],
+// nothing copied.  The ifstream and host staging pointer are kept for signature parity.
+template <class T>
+void assign_weight_pointer(const tensor& t, T*& d, bf16* g_gpu_weights_buffer) {
+    d = reinterpret_cast<T*>(reinterpret_cast<char*>(g_gpu_weights_buffer) + t.data_offsets[0]);
+}
+template <class T>
+void load_weight(const tensor& t, std::ifstream&, T*, T*& d, size_t, bf16* g_gpu_weights_buffer) {
+    assign_weight_pointer(t, d, g_gpu_weights_buffer);
+}
+
+// load_all_weights_to_gpu_chunked (iengine.cu:117-223) in the reference's output form.
+inline bool load_all_weights_to_gpu_chunked(qie_engine* e, const char* weights_bin, const char* meta_data_txt,
+                                            size_t chunk_bytes, bf16*& d_base_out, size_t& total_bytes_out) {
+    if (qie_engine_load_weights_bin(e, weights_bin, meta_data_txt, (int64_t)chunk_bytes) != 0) return false;
+    void* base = nullptr;
+    int64_t n = 0;
+    if (qie_engine_arena(e, &base, &n) != 0) return false;
+    d_base_out = (bf16*)base;
+    total_bytes_out = (size_t)n;
+    return true;
+}
+
+// launch_rms (helpers.cuh:45-49, normalization.cu:5-25): y = rmsnorm(x) * w, seqlen rows
+inline void launch_rms(bf16* x, bf16* w, bf16* y, size_t hidden, size_t seqlen) {
+    check_(qie_rmsnorm(x, w, y, (int64_t)seqlen, (int64_t)hidden, config().rms_eps, config().numerics,
+                       config().stream), "launch_rms");
+}
+
+// launch_rope (helpers.cuh:51-55, RoPE.cu:6-22): rows 0..seqlen-1 at positions 0..seqlen-1,
+// in place; hidden_dim is the row stride, nheads heads of head_dim
+inline void launch_rope(float* cos_d, float* sin_d, bf16* x, size_t seqlen, size_t head_dim, size_t hidden_dim,
+                        size_t nheads) {
+    check_(qie_rope(x, (int64_t)seqlen, (int64_t)hidden_dim, (int32_t)nheads, (int32_t)head_dim, nullptr, 0, cos_d,
+                    sin_d, config().numerics, config().stream), "launch_rope");
+}
+
+// launch_rope_single (helpers.cuh:143-147): one row at position pos
+inline void launch_rope_single(float* cos_d, float* sin_d, bf16* x, size_t pos, size_t head_dim, int hidden_dim,
+                               int nheads) {
+    check_(qie_rope(x, 1, hidden_dim, nheads, (int32_t)head_dim, nullptr, (int32_t)pos, cos_d, sin_d,
+                    config().numerics, config().stream), "launch_rope_single");
+}
+
+// launch_qknorm (helpers.cuh:140-142, qk_norm.cu:43-79): in place, hidden = row stride
+inline void launch_qknorm(bf16* X, bf16* w, int head_dim, int seqlen, int hidden, int nheads) {
+    check_(qie_qknorm(X, seqlen, hidden, nheads, head_dim, w, config().qk_eps, config().numerics, config().stream),
+           "launch_qknorm");
+}
+
+// launch_matmul (helpers.cuh:81-106, matrix_mul.cu:165-288): C[M][K] = A[M][N] . W[K][N]^T
+// (W in PyTorch [out, in] layout; the reference names the inner dimension N and the
+// output dimension K)
+inline void launch_matmul(bf16* A, bf16* W, bf16* Cout, int M, int N, int K) {
+    qie_linear_args a;
+    std::memset(&a, 0, sizeof(a));
+    a.x = A; a.ldx = N;
+    a.w[0] = W; a.seg_rows[0] = K;
+    a.M = M; a.K = N; a.N = K;
+    a.y = Cout; a.ldy = K;
+    a.epilogue = QIE_EPI_STORE;
+    a.numerics = config().numerics;
+    check_(qie_linear(&a, config().stream), "launch_matmul");
+}
+
+// proj (helpers.cuh:132-138): resolve the weight from the arena, then launch_matmul
+inline void proj(const tensor& t, std::ifstream& f, bf16* w_h, bf16* w_d, size_t w_elems, bf16* x, bf16* y, int m,
+                 int n, int k, bf16* g_gpu_weights_buffer) {
+    load_weight(t, f, w_h, w_d, w_elems, g_gpu_weights_buffer);
+    launch_matmul(x, w_d, y, m, n, k);
+}
+
+// launch_act / launch_elem / launch_resadd (helpers.cuh:108-119)
+inline void launch_act(bf16* x, size_t n) { check_(qie_silu(x, (int64_t)n, config().stream), "launch_act"); }
+inline void launch_elem(bf16* a, bf16* b, bf16* out, int n) {
+    check_(qie_mul(a, b, out, n, config().stream), "launch_elem");
+}
+inline void launch_resadd(bf16* x, bf16* y, size_t n) {
+    check_(qie_residual_add(x, y, (int64_t)n, config().stream), "launch_resadd");
+}
+
+// copy_last_vocab_vec / copy_first_token (helpers.cuh:149-155)
+inline void copy_last_vocab_vec(bf16* seq, bf16* dst, int hidden, int seqlen) {
+    check_(qie_memcpy_d2d(dst, seq + (int64_t)(seqlen - 1) * hidden, (int64_t)hidden * 2, config().stream),
+           "copy_last_vocab_vec");
+}
+inline void copy_first_token(bf16* seq, bf16* dst, int hidden) {
+    check_(qie_memcpy_d2d(dst, seq, (int64_t)hidden * 2, config().stream), "copy_first_token");
+}
+
+// sample_topk_bf16 (helpers.cuh:157-166, logit_decode.cu:149-274): k rounds of arg-max,
+// softmax(v / T), one XORWOW draw from curand_init(seed, subsequence = step, 0).  Only
+// subsequence 0 is implemented (every call site in the reference passes 0 and moves the
+// seed instead, qwen_main.cu:241,388).  Returns the token, or -1 on error.
+inline int sample_topk_bf16(bf16* logits_d, int vocab, float temperature, int topk, unsigned long long seed,
+                            int step) {
+    if (step != 0) {
+        std::fprintf(stderr, "sample_topk_bf16: cuRAND subsequence %d not supported (only 0)\n", step);
+        config().error = -22;
+        return -1;
+    }
+    const int64_t ws = qie_sample_workspace_bytes(1, vocab);
+    char* p = (char*)scratch(2).get(ws + 256);
+    if (!p) return -1;
+    qie_sampling s;
+    s.top_k = topk;
+    s.temperature = temperature;
+    s.top_p = 1.0f;
+    s.seed = seed;
+    int32_t* d_tok = (int32_t*)(p + (ws + 255) / 256 * 256);
+    int rc = qie_sample(logits_d, 1, vocab, vocab, &s, nullptr, d_tok, p, config().stream);
+    check_(rc, "sample_topk_bf16");
+    int32_t h = -1;
+    if (rc == 0) check_(qie_memcpy_d2h(&h, d_tok, 4), "sample_topk_bf16");
+    return h;
+}
+
+// allocate_page_buffers (iengine.cu:90-100): the reference allocates one page node of
+// elems_per_page = page_size * L * hidden_kv elements; here the slot grows by the
+// positions those elements hold (elems / (L * hidden_kv)), taken from the pool.
+inline void allocate_page_buffers(page_table* node, size_t elems_per_page, size_t n_layers, size_t hidden_dim_kv) {
+    node->tokens += (int)(elems_per_page / (n_layers * hidden_dim_kv));
+    check_(qie_batch_reserve(node->batch, node->slot, node->tokens), "allocate_page_buffers");
+}
+
+// ModelBuffers (utils.hh:14-88): per-sequence activations and dims.  Weight pointer
+// slots are bound by load_weight into the engine arena; RoPE tables are the engine's.
+struct ModelBuffers {
+    int* d_token_ids = nullptr;
+    size_t sequence_len = 0;
+    size_t number_of_layers = 0, head_dim = 0, hidden_dim = 0, hidden_dim_kv = 0, num_of_qheads = 0,
+           num_of_kvheads = 0, context_size = 0, vocab_size = 0, up_dim = 0;
+    bf16* embeddings_d = nullptr;     // E [V][H] (engine arena)
+    bf16* embeddings_out = nullptr;   // residual stream [rows][H]
+    float* cos_values_d = nullptr;
+    float* sin_values_d = nullptr;
+    bf16 *norm_weights_h = nullptr, *norm_weights_d = nullptr, *rms_out = nullptr;
+    bf16 *qk_norm_weights_h = nullptr, *qk_norm_weights_d = nullptr;
+    bf16 *q_proj_weights_h = nullptr, *q_proj_weights_d = nullptr, *Q = nullptr;
+    size_t q_proj_size = 0;
+    bf16 *kv_proj_weights_h = nullptr, *kv_proj_weights_d = nullptr, *K = nullptr, *V = nullptr;
+    size_t kv_proj_size = 0;
+    bf16* atten_out = nullptr;
+    bf16 *o_proj_weights_h = nullptr, *o_proj_weights_d = nullptr, *out_proj = nullptr;
+    size_t o_proj_size = 0;
+    bf16 *mlp_up_proj_weights_h = nullptr, *mlp_up_proj_weights_d = nullptr, *MLP_UP = nullptr, *MLP_GATE = nullptr,
+         *MLP_GATE_OUT = nullptr, *MLP_DOWN = nullptr;
+    size_t mlp_up_proj_size = 0;
+    bf16 *last_x = nullptr, *prefill_output_d = nullptr, *logits_weights_h = nullptr, *logits_weights_d = nullptr;
+    size_t logtis_shape = 0;   // (sic, utils.hh:87)
+    size_t rows = 0;           // activation rows allocated (max prompt length)
+};
+
+// initialize_model_buffers (utills.cu:4-129): dims from the engine's spec, activations
+// for `sequence_len` rows, the prompt ids on device and embedded into embeddings_out
+// (embedding_matrix_func, embedded_matrix.cu:5-17).  Returns false on error.
+inline bool initialize_model_buffers(ModelBuffers& buf, const int* h_token_ids, TensorTable&, qie_engine* e,
+                                     size_t sequence_len) {
+    qie_model_spec s;
+    if (qie_engine_spec(e, &s) != 0) return false;
+    qie_model_weights w;
+    if (qie_engine_weights(e, &w, nullptr) != 0) return false;
+    int32_t rope_rows = 0;
+    const float *cs = nullptr, *sn = nullptr;
+    if (qie_engine_rope_tables(e, &cs, &sn, &rope_rows) != 0) return false;
+    buf.sequence_len = sequence_len;
+    buf.rows = sequence_len;
+    buf.number_of_layers = (size_t)s.n_layers;
+    buf.head_dim = (size_t)s.head_dim;
+    buf.num_of_qheads = (size_t)s.n_heads;
+    buf.num_of_kvheads = (size_t)s.n_kv_heads;
+    buf.hidden_dim = (size_t)s.hidden;
+    buf.hidden_dim_kv = (size_t)s.n_kv_heads * s.head_dim;
+    buf.context_size = (size_t)rope_rows;
+    buf.vocab_size = (size_t)s.vocab;
+    buf.up_dim = (size_t)s.ffn;
+    buf.embeddings_d = (bf16*)w.embed;
+    buf.cos_values_d = (float*)cs;
+    buf.sin_values_d = (float*)sn;
+    const int64_t R = (int64_t)sequence_len, H = s.hidden, QD = (int64_t)s.n_heads * s.head_dim;
+    const int64_t KD = (int64_t)buf.hidden_dim_kv, I = s.ffn;
+    bool ok = true;
+    auto A = [&](bf16** p, int64_t elems) {
+        void* q = nullptr;
+        if (ok && qie_malloc(&q, elems * 2) == 0) *p = (bf16*)q;
+        else ok = false;
+    };
+    A(&buf.embeddings_out, R * H);
+    A(&buf.rms_out, R * H);
+    A(&buf.Q, R * QD);
+    A(&buf.K, R * KD);
+    A(&buf.V, R * KD);
+    A(&buf.atten_out, R * QD);
+    A(&buf.out_proj, R * H);
+    A(&buf.MLP_UP, R * I);
+    A(&buf.MLP_GATE, R * I);
+    A(&buf.MLP_GATE_OUT, R * I);
+    A(&buf.MLP_DOWN, R * H);
+    A(&buf.last_x, H);
+    A(&buf.prefill_output_d, s.vocab);
+    void* ids = nullptr;
+    if (ok && qie_malloc(&ids, R * 4) == 0) buf.d_token_ids = (int*)ids;
+    else ok = false;
+    buf.q_proj_size = (size_t)(QD * H);
+    buf.kv_proj_size = (size_t)(KD * H);
+    buf.o_proj_size = (size_t)(H * QD);
+    buf.mlp_up_proj_size = (size_t)(I * H);
+    buf.logtis_shape = (size_t)s.vocab * H;
+    if (ok) ok = qie_memcpy_h2d(buf.d_token_ids, h_token_ids, R * 4) == 0;
+    if (ok) ok = qie_embedding(buf.embeddings_d, buf.d_token_ids, buf.embeddings_out, R, H, config().stream) == 0;
+    if (!ok) std::fprintf(stderr, "initialize_model_buffers: %s\n", qie_last_error());
+    return ok;
+}
+
+// destroy_model_buffers (utils.hh:105, utills.cu:142-205): frees the activations
+// (weights and RoPE tables belong to the engine)
+inline void destroy_model_buffers(ModelBuffers& buf) {
+    bf16* ps[] = {buf.embeddings_out, buf.rms_out, buf.Q, buf.K, buf.V, buf.atten_out, buf.out_proj, buf.MLP_UP,
+                  buf.MLP_GATE, buf.MLP_GATE_OUT, buf.MLP_DOWN, buf.last_x, buf.prefill_output_d};
+    for (bf16* p : ps)
+        if (p) qie_free(p);
+    if (buf.d_token_ids) qie_free(buf.d_token_ids);
+    buf = ModelBuffers();
+}
+
+// embedding_matrix_func launch (embedded_matrix.cu:5-17; decode: qwen_main.cu:259-268):
+// rows 0..n-1 of `out` = E[ids]; ids on the host
+inline void embed_tokens(ModelBuffers& buf, const int* h_ids, size_t n) {
+    check_(qie_memcpy_h2d(buf.d_token_ids, h_ids, (int64_t)n * 4), "embed_tokens");
+    check_(qie_embedding(buf.embeddings_d, buf.d_token_ids, buf.embeddings_out, (int64_t)n, (int64_t)buf.hidden_dim,
+                         config().stream), "embed_tokens");
+}
+
+// kv_copy_layer_to_cache_prefill (include_cuda.cu:165-228): K/V rows 0..sequence_len-1
+// of layer i into positions 0..sequence_len-1 of the page table's slot
+inline void kv_copy_layer_to_cache_prefill(ModelBuffers* buffer, int i, page_table* kv, int /*page_size*/) {
+    const int n = (int)buffer->sequence_len;
+    if (kv->tokens < n) {
+        kv->tokens = n;
+        check_(qie_batch_reserve(kv->batch, kv->slot, n), "kv_copy_layer_to_cache_prefill");
+    }
+    qie_kv_cache c;
+    check_(qie_batch_kv_cache(kv->batch, kv->slot, &c), "kv_copy_layer_to_cache_prefill");
+    check_(qie_kv_write(buffer->K, buffer->V, n, (int64_t)buffer->hidden_dim_kv, 0, &c, 0, i, config().stream),
+           "kv_copy_layer_to_cache_prefill");
+}
+
+// kv_copy_layer_to_cache_decode (include_cuda.cu:233-279): row 0 of K/V of layer i into
+// position sequence_len - 1 (a missing page is taken from the pool, as the reference
+// allocates one)
+inline void kv_copy_layer_to_cache_decode(ModelBuffers* buffer, int i, page_table* kv, int /*page_size*/) {
+    const int pos = (int)buffer->sequence_len - 1;
+    if (kv->tokens < pos + 1) {
+        kv->tokens = pos + 1;
+        check_(qie_batch_reserve(kv->batch, kv->slot, pos + 1), "kv_copy_layer_to_cache_decode");
+    }
+    qie_kv_cache c;
+    check_(qie_batch_kv_cache(kv->batch, kv->slot, &c), "kv_copy_layer_to_cache_decode");
+    check_(qie_kv_write(buffer->K, buffer->V, 1, (int64_t)buffer->hidden_dim_kv, pos, &c, 0, i, config().stream),
+           "kv_copy_layer_to_cache_decode");
+}
+
+// launch_attn (helpers.cuh:121-130, self_attension.cu:10-149): mq query rows of Q
+// ([mq][hidden]) over the first mkv cached positions of the slot's layer `layer_id`.
+// causal: row r sees positions <= q_abs_base + r; otherwise every row sees all mkv.
+inline void launch_attn(bf16* Q, bf16* out, size_t mq, size_t mkv, size_t head_dim, size_t hidden, size_t hidden_kv,
+                        int causal, size_t q_abs_base, int layer_id, page_table* kv, int /*page_size*/) {
+    qie_kv_cache c;
+    if (qie_batch_kv_cache(kv->batch, kv->slot, &c) != 0) return check_(-22, "launch_attn");
+    std::vector<int32_t> pos(mq);
+    for (size_t r = 0; r < mq; r++) pos[r] = causal ? (int32_t)(q_abs_base + r) : (int32_t)mkv - 1;
+    int32_t* dpos = (int32_t*)scratch(0).get((int64_t)mq * 4);
+    const int32_t nq = (int32_t)(hidden / head_dim);
+    void* ws = scratch(1).get(qie_attention_workspace_bytes((int64_t)mq, nq, (int32_t)head_dim, c.max_ctx));
+    // every call site in the reference is causal prefill or mq = 1 decode (qwen_main.cu:123,300)
+    if (!dpos || !ws || hidden_kv != (size_t)c.n_kv_heads * c.head_dim || (!causal && mq != 1))
+        return check_(-22, "launch_attn");
+    check_(qie_memcpy_h2d(dpos, pos.data(), (int64_t)mq * 4), "launch_attn");
+    check_(qie_attention(Q, (int64_t)mq, dpos, (int32_t)mq, &c, layer_id, nq, out, ws, config().stream),
+           "launch_attn");
 }
 
 }  // namespace qie_compat

@@ -141,6 +141,21 @@ int qie_batch_history(qie_batch* b, int32_t seq, int32_t* host_ids, int32_t n);
 /* Rewind/set sequence `seq` to position pos with current token `token`
  * (KV rows >= pos are simply overwritten later). */
 int qie_batch_set_position(qie_batch* b, int32_t seq, int32_t pos, int32_t token);
+/* Batch geometry: B slots, max_ctx positions per slot. */
+int qie_batch_dims(const qie_batch* b, int32_t* batch, int32_t* max_ctx);
+/* KV descriptor of slot `seq` for the operator tier (qie_kv_write, qie_attention with
+ * sequence index 0): contiguous -> that slot's region; paged -> the pool with the
+ * slot's block-table row.  Valid until the batch is destroyed. */
+int qie_batch_kv_cache(const qie_batch* b, int32_t seq, qie_kv_cache* out);
+/* Operator tier: make slot `seq` a live sequence holding the KV pages for positions
+ * [0, n_tokens) (paged: taken from the pool, all-or-nothing; contiguous: a bounds
+ * check).  allocate_page_buffers (iengine.cu:90-100) in the reference's terms. */
+int qie_batch_reserve(qie_batch* b, int32_t seq, int32_t n_tokens);
+/* The engine's weight arena (load_all_weights_to_gpu_chunked's d_base_out /
+ * total_bytes_out, iengine.cu:117) and its RoPE tables (fp32 [rows][head_dim/2]). */
+int qie_engine_arena(const qie_engine* e, void** base, int64_t* bytes);
+int qie_engine_rope_tables(const qie_engine* e, const float** rope_cos, const float** rope_sin,
+                           int32_t* rows);
 /* Time `iters` launches of one of the decode step's kernels with hipEvents on
  * the engine stream (which: 0 = gate/up GEMV of layer 0, 1 = down GEMV,
  * 2 = QKV GEMV, 3 = O GEMV, 4 = lm_head GEMV, 5 = attention).  Returns the

@@ -167,9 +167,36 @@ int qie_attention_decode(const void* qkv, int64_t B, const int32_t* pos, const v
  * of lane l (pins the transposed-read lane mapping the prefill attention relies on). */
 int qie_debug_tr16_probe(int32_t* out_dev);
 
+/* ------------------------------------------- standalone in-place head ops
+ * The operator tier of a host that keeps the reference's layer loop
+ * (qwen_main.cu:77-241); the engine itself fuses these into qie_qkv_post /
+ * qie_attention_decode.  Rows [rows][row_stride] of n_heads heads of head_dim.
+ *   qie_qknorm: launch_qknorm / qkNorm (helpers.cuh:140-142, qk_norm.cu:43-79),
+ *     in place, the reference's tree summation order (REF); HF = transformers.
+ *   qie_rope:   launch_rope / launch_rope_single (helpers.cuh:51-55, 143-147;
+ *     RoPE.cu:6-22), in place; row r at position pos[r] (device, may be NULL)
+ *     or pos0 + r.  Tables as built by qie_rope_table_host.
+ *   qie_kv_write: kv_copy_layer_to_cache_prefill / _decode (include_cuda.cu:
+ *     165-279): K and V rows [rows][ld] (n_kv_heads*head_dim used) into layer
+ *     `layer` of sequence `seq` at positions pos0 .. pos0+rows-1.  Paged caches
+ *     need those pages held (qie_batch_reserve). */
+int qie_qknorm(void* x, int64_t rows, int64_t row_stride, int32_t n_heads, int32_t head_dim,
+               const void* w, float eps, int32_t numerics, void* stream);
+int qie_rope(void* x, int64_t rows, int64_t row_stride, int32_t n_heads, int32_t head_dim,
+             const int32_t* pos, int32_t pos0, const float* rope_cos, const float* rope_sin,
+             int32_t numerics, void* stream);
+int qie_kv_write(const void* k, const void* v, int64_t rows, int64_t ld, int32_t pos0,
+                 const qie_kv_cache* cache, int32_t seq, int32_t layer, void* stream);
+
 /* ------------------------------------------------------------- elementwise
  * launch_act + launch_elem (helpers.cuh:108-115) and launch_resadd (:116-119)
- * for callers that do not use the fused linear epilogues. */
+ * for callers that do not use the fused linear epilogues: qie_silu_mul fuses the
+ * two; qie_silu (activation, SiLU.cu:10-23, in place: x = bf16(x*sigmoid(x))) and
+ * qie_mul (element_mul, element_add.cu:4-12: c = bf16(a*b)) are the separate ops.
+ * qie_memcpy_d2d: copy_last_vocab_vec / copy_first_token (helpers.cuh:149-155). */
+int qie_silu(void* x, int64_t n, void* stream);
+int qie_mul(const void* a, const void* b, void* c, int64_t n, void* stream);
+int qie_memcpy_d2d(void* dst, const void* src, int64_t bytes, void* stream);
 int qie_silu_mul(const void* gate, const void* up, void* h, int64_t n, void* stream);
 int qie_residual_add(void* x, const void* y, int64_t n, void* stream);
 /* Tensor-parallel residual: x = bf16(x + bf16(sum)) with sum the fp32 all-reduced

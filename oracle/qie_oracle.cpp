@@ -123,6 +123,22 @@ void or_rope_table_hf(float* cos_out, float* sin_out, int n_pos, int head_dim, f
     }
 }
 
+static int g_sum_order = 0;
+/* Summation-order variants (test infrastructure only; every variant is a valid
+ * evaluation of the reference's arithmetic, since the reference leaves WMMA fragment
+ * order unspecified and an MI355X kernel necessarily reduces in a different order):
+ *   0 = the orders restated below (the reference's where it is specified);
+ *   1 = matmul inner products as 64 interleaved fp32 partials over 8-element blocks
+ *       (k / 8 mod 64), combined by a float pairwise tree;
+ *   2 = EVERY fp32 reduction reordered: matmul as 1; RMSNorm sum of squares as 256
+ *       strided partials + pairwise tree; qk-norm sequential; attention dot products as
+ *       8 interleaved partials + tree, softmax denominator and P.V accumulated per
+ *       128-key block then summed across blocks.
+ * The logit spread between variant 0 and 1 / 2 at a given depth is the reference
+ * algorithm's own order sensitivity, which sizes the end-to-end parity tolerance
+ * (bench.py cpu_baseline, tests/test_gpu_headline.py, DESIGN.md "Parity"). */
+void or_set_sum_order(int v) { g_sum_order = v; }
+
 /* ---------------------------------------------------------------- RMSNorm
  * Reference: rmsNorm, layers/src/normalization.cu:5-25 (one thread per row):
  *   sum = sequential fp32 sum of x_i^2; rms = sqrtf(sum/H + eps);
@@ -135,9 +151,21 @@ void or_rmsnorm(const bf16_t* x, const bf16_t* w, bf16_t* y, int64_t rows, int64
         const bf16_t* xr = x + r * H;
         bf16_t* yr = y + r * H;
         float sum = 0.f;
-        for (int64_t i = 0; i < H; i++) {
-            float t = bf2f(xr[i]);
-            sum += t * t;
+        if (g_sum_order == 2) {
+            float part[256];
+            for (int j = 0; j < 256; j++) part[j] = 0.f;
+            for (int64_t i = 0; i < H; i++) {
+                float t = bf2f(xr[i]);
+                part[i & 255] += t * t;
+            }
+            for (int w = 128; w > 0; w >>= 1)
+                for (int j = 0; j < w; j++) part[j] += part[j + w];
+            sum = part[0];
+        } else {
+            for (int64_t i = 0; i < H; i++) {
+                float t = bf2f(xr[i]);
+                sum += t * t;
+            }
         }
         if (numerics == QIE_NUMERICS_HF) {
             float inv = 1.0f / sqrtf(sum / (float)H + eps);
@@ -159,30 +187,23 @@ void or_rmsnorm(const bf16_t* x, const bf16_t* w, bf16_t* y, int64_t rows, int64
  * oracle fixes its own order: 16 fp32 partial sums over k, combined in double.)
  * Bias (Qwen2, absent in the reference): C = bf16(float(sum) + b[n]).
  */
-static int g_sum_order = 0;
-/* Summation-order variant for the matmul inner products (test infrastructure only):
- * 0 = the order above; 1 = 64 interleaved fp32 partials over 8-element blocks
- * (k / 8 mod 64), combined by a float pairwise tree — another order the reference's
- * unspecified WMMA accumulation could take.  The logit spread between the two at full
- * depth is the reference algorithm's own order sensitivity, which sizes the full-depth
- * parity tolerance (bench.py cpu_baseline, DESIGN.md "Parity"). */
-void or_set_sum_order(int v) { g_sum_order = v; }
+
 
 void or_matmul(const bf16_t* A, const bf16_t* W, const bf16_t* bias, bf16_t* C,
                int64_t M, int64_t K, int64_t N, int nthreads) {
     std::vector<float> Af((size_t)M * K);
     for (int64_t i = 0; i < M * K; i++) Af[i] = bf2f(A[i]);
     int nt = set_threads(nthreads);
+    if (g_sum_order == 1 || g_sum_order == 2) {
 #pragma omp parallel num_threads(nt)
-    {
-        std::vector<float> wf((size_t)K);
+        {
+            std::vector<float> wf((size_t)K);
 #pragma omp for schedule(static)
-        for (int64_t n = 0; n < N; n++) {
-            const bf16_t* wr = W + n * K;
-            for (int64_t k = 0; k < K; k++) wf[k] = bf2f(wr[k]);
-            for (int64_t m = 0; m < M; m++) {
-                const float* ar = Af.data() + m * K;
-                if (g_sum_order == 1) {
+            for (int64_t n = 0; n < N; n++) {
+                const bf16_t* wr = W + n * K;
+                for (int64_t k = 0; k < K; k++) wf[k] = bf2f(wr[k]);
+                for (int64_t m = 0; m < M; m++) {
+                    const float* ar = Af.data() + m * K;
                     float part[64];
                     for (int j = 0; j < 64; j++) part[j] = 0.f;
                     for (int64_t k = 0; k < K; k++) part[(k >> 3) & 63] += ar[k] * wf[k];
@@ -191,21 +212,54 @@ void or_matmul(const bf16_t* A, const bf16_t* W, const bf16_t* bias, bf16_t* C,
                     float f = part[0];
                     if (bias) f = f + bf2f(bias[n]);
                     C[m * N + n] = f2bf(f);
-                    continue;
                 }
-                float acc[16];
-                for (int j = 0; j < 16; j++) acc[j] = 0.f;
-                int64_t k = 0;
-                for (; k + 16 <= K; k += 16)
-                    for (int j = 0; j < 16; j++) acc[j] += ar[k + j] * wf[k + j];
-                double s = 0.0;
-                for (int j = 0; j < 16; j++) s += (double)acc[j];
-                for (; k < K; k++) s += (double)(ar[k] * wf[k]);
-                float f = (float)s;
-                if (bias) f = f + bf2f(bias[n]);
-                C[m * N + n] = f2bf(f);
             }
         }
+        return;
+    }
+    // Order 0, tiled (TM rows of A x TN rows of W per task, both L2-resident) — the
+    // per-element arithmetic is unchanged: 16 fp32 partials over k in blocks of 16, in
+    // k order, combined in double, then the k tail, then the bias.
+    const int64_t TM = 64, TN = 16;
+    const int64_t mt = (M + TM - 1) / TM, ntl = (N + TN - 1) / TN;
+#pragma omp parallel num_threads(nt)
+    {
+        std::vector<float> wf((size_t)TN * K);
+#pragma omp for schedule(dynamic, 1) collapse(2)
+        for (int64_t tn = 0; tn < ntl; tn++)
+            for (int64_t tm = 0; tm < mt; tm++) {
+                const int64_t n0 = tn * TN, n1 = std::min(N, n0 + TN);
+                const int64_t m0 = tm * TM, m1 = std::min(M, m0 + TM);
+                for (int64_t n = n0; n < n1; n++) {
+                    const bf16_t* wr = W + n * K;
+                    float* w = wf.data() + (n - n0) * K;
+                    for (int64_t k = 0; k < K; k++) w[k] = bf2f(wr[k]);
+                }
+                const int64_t K16 = K / 16 * 16;
+                for (int64_t m = m0; m < m1; m++) {
+                    const float* ar = Af.data() + m * K;
+                    for (int64_t n = n0; n < n1; n += 4) {
+                        // 4 output columns at once: independent accumulator chains
+                        const int nc = (int)std::min<int64_t>(4, n1 - n);
+                        const float* w[4];
+                        for (int c = 0; c < 4; c++) w[c] = wf.data() + (n + std::min(c, nc - 1) - n0) * K;
+                        float acc[4][16];
+                        for (int c = 0; c < 4; c++)
+                            for (int j = 0; j < 16; j++) acc[c][j] = 0.f;
+                        for (int64_t k = 0; k < K16; k += 16)
+                            for (int c = 0; c < 4; c++)
+                                for (int j = 0; j < 16; j++) acc[c][j] += ar[k + j] * w[c][k + j];
+                        for (int c = 0; c < nc; c++) {
+                            double sd = 0.0;
+                            for (int j = 0; j < 16; j++) sd += (double)acc[c][j];
+                            for (int64_t k = K16; k < K; k++) sd += (double)(ar[k] * w[c][k]);
+                            float f = (float)sd;
+                            if (bias) f = f + bf2f(bias[n + c]);
+                            C[m * N + n + c] = f2bf(f);
+                        }
+                    }
+                }
+            }
     }
 }
 
@@ -228,8 +282,11 @@ void or_qknorm(bf16_t* x, const bf16_t* w, int64_t rows, int64_t row_stride, int
                 continue;
             }
             for (int d = 0; d < hd; d++) { float t = bf2f(v[d]); buf[d] = t * t; }
-            for (int stride = hd / 2; stride > 0; stride >>= 1)
-                for (int d = 0; d < stride; d++) buf[d] += buf[d + stride];
+            if (g_sum_order == 2)
+                for (int d = 1; d < hd; d++) buf[0] += buf[d];
+            else
+                for (int stride = hd / 2; stride > 0; stride >>= 1)
+                    for (int d = 0; d < stride; d++) buf[d] += buf[d + stride];
             float rms = sqrtf((buf[0] / hd) + eps);
             for (int d = 0; d < hd; d++) v[d] = f2bf((bf2f(v[d]) / rms) * bf2f(w[d]));
         }
@@ -324,8 +381,16 @@ void or_attention(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, bf16_t* o
                 for (int t = 0; t < mkv; t++) {
                     const bf16_t* kr = kh + (int64_t)t * hd;
                     for (int d = 0; d < hd; d++) buf[d] = bf2f(qr[d]) * bf2f(kr[d]);
-                    for (int stride = hd / 2; stride > 0; stride >>= 1)
-                        for (int d = 0; d < stride; d++) buf[d] += buf[d + stride];
+                    if (g_sum_order == 2) {
+                        float part[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+                        for (int d = 0; d < hd; d++) part[d & 7] += buf[d];
+                        for (int w = 4; w > 0; w >>= 1)
+                            for (int j = 0; j < w; j++) part[j] += part[j + w];
+                        buf[0] = part[0];
+                    } else {
+                        for (int stride = hd / 2; stride > 0; stride >>= 1)
+                            for (int d = 0; d < stride; d++) buf[d] += buf[d + stride];
+                    }
                     score[t] = buf[0] / scale;
                 }
                 int q_abs = q_abs_base + qt;
@@ -335,15 +400,35 @@ void or_attention(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, bf16_t* o
                 float mx = -1e9f;
                 for (int t = 0; t < mkv; t++) mx = fmaxf(mx, score[t]);
                 float sum = 0.f;
-                for (int t = 0; t < mkv; t++) {
-                    score[t] = expf(score[t] - mx);
-                    sum += score[t];
+                if (g_sum_order == 2) {   // per 128-key block, then across blocks
+                    for (int t0 = 0; t0 < mkv; t0 += 128) {
+                        float bs = 0.f;
+                        for (int t = t0; t < std::min(mkv, t0 + 128); t++) {
+                            score[t] = expf(score[t] - mx);
+                            bs += score[t];
+                        }
+                        sum += bs;
+                    }
+                } else {
+                    for (int t = 0; t < mkv; t++) {
+                        score[t] = expf(score[t] - mx);
+                        sum += score[t];
+                    }
                 }
                 for (int t = 0; t < mkv; t++) score[t] /= sum;
                 bf16_t* orow = out + (int64_t)qt * nq * hd + (int64_t)h * hd;
                 for (int d = 0; d < hd; d++) {
                     float acc = 0.f;
-                    for (int t = 0; t < mkv; t++) acc += score[t] * bf2f(vh[(int64_t)t * hd + d]);
+                    if (g_sum_order == 2) {
+                        for (int t0 = 0; t0 < mkv; t0 += 128) {
+                            float ba = 0.f;
+                            for (int t = t0; t < std::min(mkv, t0 + 128); t++)
+                                ba += score[t] * bf2f(vh[(int64_t)t * hd + d]);
+                            acc += ba;
+                        }
+                    } else {
+                        for (int t = 0; t < mkv; t++) acc += score[t] * bf2f(vh[(int64_t)t * hd + d]);
+                    }
                     orow[d] = f2bf(acc);
                 }
             }

@@ -105,6 +105,12 @@ SIGNATURES = [
     ("qie_attention_decode", C.c_int, [_P, _I64, _P, _P, _P, _P, _P, _I32, C.POINTER(KvCacheC), _I32, _F, _I32,
                                        _P, _P, _P]),
     ("qie_debug_tr16_probe", C.c_int, [_P]),
+    ("qie_qknorm", C.c_int, [_P, _I64, _I64, _I32, _I32, _P, _F, _I32, _P]),
+    ("qie_rope", C.c_int, [_P, _I64, _I64, _I32, _I32, _P, _I32, _P, _P, _I32, _P]),
+    ("qie_kv_write", C.c_int, [_P, _P, _I64, _I64, _I32, C.POINTER(KvCacheC), _I32, _I32, _P]),
+    ("qie_silu", C.c_int, [_P, _I64, _P]),
+    ("qie_mul", C.c_int, [_P, _P, _P, _I64, _P]),
+    ("qie_memcpy_d2d", C.c_int, [_P, _P, _I64, _P]),
     ("qie_silu_mul", C.c_int, [_P, _P, _P, _I64, _P]),
     ("qie_residual_add", C.c_int, [_P, _P, _I64, _P]),
     ("qie_residual_add_f32", C.c_int, [_P, _P, _I64, _P]),
@@ -155,6 +161,11 @@ SIGNATURES = [
     ("qie_batch_positions", C.c_int, [_P, _PI32]),
     ("qie_batch_history", C.c_int, [_P, _I32, _PI32, _I32]),
     ("qie_batch_set_position", C.c_int, [_P, _I32, _I32, _I32]),
+    ("qie_batch_dims", C.c_int, [_P, _PI32, _PI32]),
+    ("qie_batch_kv_cache", C.c_int, [_P, _I32, C.POINTER(KvCacheC)]),
+    ("qie_batch_reserve", C.c_int, [_P, _I32, _I32]),
+    ("qie_engine_arena", C.c_int, [_P, C.POINTER(_P), _PI64]),
+    ("qie_engine_rope_tables", C.c_int, [_P, C.POINTER(_P), C.POINTER(_P), _PI32]),
     ("qie_batch_time_kernel", C.c_int, [_P, _I32, _I32, _PD, _PD]),
 ]
 

@@ -97,6 +97,7 @@ struct qie_batch {
              *pf_h = nullptr;
     int32_t *pf_pos = nullptr, *pf_ids = nullptr;
     void* pf_attn_ws = nullptr;
+    int64_t pf_attn_ws_bytes = 0;   // the split workspace depends on n (short prompts split), not on n <= pf_rows
     // paged KV (qie_batch_create_paged): pool pages of page_tokens tokens, block table
     // [B][max_pages] on device and host, free list, pages held per slot
     int page_tokens = 0, max_pages = 0, n_pages = 0;
@@ -510,13 +511,29 @@ static int enqueue_decode(qie_batch* b, const qie_sampling* smp) {
 }
 
 static int ensure_prefill_scratch(qie_batch* b, int64_t n) {
-    if (n <= b->pf_rows) return 0;
+    if (n <= b->pf_rows) {
+        // rows fit; the attention workspace is not monotone in n (<= 8 rows run the split
+        // kernel with partials, longer prompts need none), so size it for this n
+        const qie_model_spec& s = b->e->spec;
+        const int64_t ws = qie_attention_workspace_bytes(n, b->e->sh.nq, s.head_dim, b->max_ctx);
+        if (ws > b->pf_attn_ws_bytes) {
+            hipFree(b->pf_attn_ws);
+            b->pf_attn_ws = nullptr;
+            b->pf_attn_ws_bytes = 0;
+            QIE_TRY(dmalloc(&b->pf_attn_ws, (size_t)ws));
+            b->pf_attn_ws_bytes = ws;
+        }
+        return 0;
+    }
     const qie_model_spec& s = b->e->spec;
     const TpShard& sh = b->e->sh;
     const int64_t H = s.hidden, QD = (int64_t)sh.nq * s.head_dim, KD = (int64_t)sh.nkv * s.head_dim;
-    hipFree(b->pf_x); hipFree(b->pf_hn); hipFree(b->pf_qkv); hipFree(b->pf_q); hipFree(b->pf_att);
-    hipFree(b->pf_h); hipFree(b->pf_pos); hipFree(b->pf_ids); hipFree(b->pf_attn_ws); hipFree(b->pf_part);
-    b->pf_part = nullptr;
+    void** olds[] = {(void**)&b->pf_x, (void**)&b->pf_hn, (void**)&b->pf_qkv, (void**)&b->pf_q, (void**)&b->pf_att,
+                     (void**)&b->pf_h, (void**)&b->pf_pos, (void**)&b->pf_ids, &b->pf_attn_ws, (void**)&b->pf_part};
+    for (void** p : olds) {   // nulled as freed: a failed re-allocation below leaves nothing dangling
+        if (*p) hipFree(*p);
+        *p = nullptr;
+    }
     b->pf_rows = 0;
     if (sh.tp > 1) QIE_TRY(dmalloc((void**)&b->pf_part, n * H * 4));
     QIE_TRY(dmalloc((void**)&b->pf_x, n * H * 2));
@@ -527,8 +544,11 @@ static int ensure_prefill_scratch(qie_batch* b, int64_t n) {
     QIE_TRY(dmalloc((void**)&b->pf_h, n * (int64_t)sh.ffn * 2));
     QIE_TRY(dmalloc((void**)&b->pf_pos, n * 4));
     QIE_TRY(dmalloc((void**)&b->pf_ids, n * 4));
+    b->pf_attn_ws = nullptr;
+    b->pf_attn_ws_bytes = 0;
     int64_t ws = qie_attention_workspace_bytes(n, sh.nq, s.head_dim, b->max_ctx);
     QIE_TRY(dmalloc(&b->pf_attn_ws, (size_t)ws));
+    b->pf_attn_ws_bytes = ws;
     b->pf_rows = n;
     return 0;
 }
@@ -902,7 +922,10 @@ static int batch_create(qie_engine* e, int32_t batch, int32_t max_ctx, int32_t p
     } else {
         b->seq_stride = (int64_t)s.n_layers * sh.nkv * max_ctx * hd;   // this rank's kv heads only
     }
-    b->idle.assign(batch, 0);
+    // Slots start idle: a slot runs as a live sequence only after a prefill or
+    // set_position, so unused slots never take pool pages (they run on scratch page 0)
+    // and are rewound before they would pass max_ctx (prepare_steps).
+    b->idle.assign(batch, 1);
     int rc = 0;
     auto A = [&](void** p, size_t bytes) {
         if (!rc) rc = dmalloc(p, bytes);
@@ -1027,6 +1050,12 @@ int qie_prefill(qie_batch* b, int32_t seq, const int32_t* ids, int32_t n, const 
         QIE_REQUIRE(ids[i] >= 0 && ids[i] < s.vocab, "qie_prefill: token id %d out of range", ids[i]);
     hipStream_t st = e->stream;
     QIE_TRY(ensure_prefill_scratch(b, n));
+    if (b->d_table) {   // all-or-nothing: the slot's own pages count, nothing is dropped on failure
+        const int64_t need = ((int64_t)n + b->page_tokens - 1) / b->page_tokens;
+        QIE_REQUIRE(need <= (int64_t)b->free_pages.size() + b->held[seq],
+                    "qie_prefill: KV pool exhausted (%lld pages needed, %zu free + %d held by slot %d)",
+                    (long long)need, b->free_pages.size(), b->held[seq], seq);
+    }
     drop_pages(b, seq);   // a prefill starts a new sequence in the slot
     QIE_TRY(ensure_pages(b, seq, n));
     QIE_TRY(flush_table(b));
@@ -1115,6 +1144,7 @@ static int launch_step(qie_batch* b, const qie_sampling* smp) {
 // steps write (positions h_pos .. h_pos + n_steps - 1); idle slots are rewound to
 // position 0 when they would run past max_ctx.  Nothing is launched on failure.
 static int prepare_steps(qie_batch* b, int n_steps, const char* who) {
+    QIE_REQUIRE(n_steps < b->max_ctx, "%s: %d steps exceed max_ctx %d", who, n_steps, b->max_ctx);
     for (int m = 0; m < b->B; m++)
         if (!b->idle[m])
             QIE_REQUIRE(b->h_pos[m] + n_steps < b->max_ctx, "%s: sequence %d would exceed max_ctx %d", who, m,
@@ -1212,6 +1242,43 @@ int qie_batch_set_position(qie_batch* b, int32_t seq, int32_t pos, int32_t token
     QIE_LAUNCH_CHECK();
     QIE_HIP(hipStreamSynchronize(e->stream));
     b->h_pos[seq] = pos;
+    return 0;
+}
+
+int qie_batch_dims(const qie_batch* b, int32_t* batch, int32_t* max_ctx) {
+    QIE_REQUIRE(b, "qie_batch_dims: null batch");
+    if (batch) *batch = b->B;
+    if (max_ctx) *max_ctx = b->max_ctx;
+    return 0;
+}
+
+int qie_batch_kv_cache(const qie_batch* b, int32_t seq, qie_kv_cache* out) {
+    QIE_REQUIRE(b && out && seq >= 0 && seq < b->B, "qie_batch_kv_cache: bad arguments");
+    *out = batch_cache(b, seq);
+    return 0;
+}
+
+int qie_batch_reserve(qie_batch* b, int32_t seq, int32_t n_tokens) {
+    QIE_REQUIRE(b && seq >= 0 && seq < b->B && n_tokens >= 0, "qie_batch_reserve: bad arguments");
+    QIE_REQUIRE(n_tokens <= b->max_ctx, "qie_batch_reserve: %d tokens exceed max_ctx %d", n_tokens, b->max_ctx);
+    QIE_TRY(ensure_pages(b, seq, n_tokens));
+    QIE_TRY(flush_table(b));
+    b->idle[seq] = 0;
+    return 0;
+}
+
+int qie_engine_arena(const qie_engine* e, void** base, int64_t* bytes) {
+    QIE_REQUIRE(e && e->have_weights, "qie_engine_arena: engine has no weights");
+    if (base) *base = e->arena;
+    if (bytes) *bytes = (int64_t)e->arena_bytes;
+    return 0;
+}
+
+int qie_engine_rope_tables(const qie_engine* e, const float** rope_cos, const float** rope_sin, int32_t* rows) {
+    QIE_REQUIRE(e, "qie_engine_rope_tables: null engine");
+    if (rope_cos) *rope_cos = e->rope_cos;
+    if (rope_sin) *rope_sin = e->rope_sin;
+    if (rows) *rows = e->rope_rows;
     return 0;
 }
 

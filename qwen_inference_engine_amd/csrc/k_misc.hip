@@ -220,6 +220,130 @@ __global__ __launch_bounds__(256) void qkv_post_kernel(QkvPostArgs a) {
     }
 }
 
+// ------------------------------------------- standalone per-head ops (operator tier)
+// qie_qknorm / qie_rope: the reference's separate in-place launches (launch_qknorm,
+// launch_rope, launch_rope_single; helpers.cuh:51-55,140-147) for hosts that keep the
+// reference layer loop.  Block per row, one wave per head (looped), one lane per pair.
+//   qk-norm: lane l owns elements (l, l + hd/2); its x_l^2 + x_{l+hd/2}^2 is the
+//     reference's shared-memory tree after the stride-hd/2 step (qk_norm.cu:59-66), the
+//     xor butterfly 32..1 then reproduces the remaining strides, and lane 0's sum (the
+//     tree's buf[0]) is broadcast — the reference's exact summation order.
+//   RoPE: REF interleaved pairs (2l, 2l+1) (RoPE.cu:12-18), HF rotate_half (l, l+hd/2);
+//     row r at position pos[r] (pos != NULL) or pos0 + r.
+struct HeadOpArgs {
+    uint16_t* x;
+    int64_t row_stride;
+    int nheads, hd;
+    const uint16_t* w;
+    float eps;
+    const float* cs;
+    const float* sn;
+    const int32_t* pos;
+    int pos0;
+    int numerics;
+    int rope;   // 0: qk-norm, 1: RoPE
+};
+
+__device__ __forceinline__ float tree_sum64(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return __shfl(v, 0, 64);
+}
+
+__global__ __launch_bounds__(256) void head_op_kernel(HeadOpArgs a) {
+#pragma clang fp contract(off)
+    const int64_t r = blockIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int hd = a.hd, half = hd / 2;
+    const bool hf = a.numerics == QIE_NUMERICS_HF;
+    const bool active = lane < half;
+    const bool pair_split = hf || !a.rope;   // (l, l + half) pairs
+    const int i0 = pair_split ? lane : 2 * lane;
+    const int i1 = pair_split ? lane + half : 2 * lane + 1;
+    float c = 0.f, s = 0.f;
+    if (a.rope && active) {
+        const int64_t p = a.pos ? a.pos[r] : (int64_t)a.pos0 + r;
+        c = a.cs[p * half + lane];
+        s = a.sn[p * half + lane];
+    }
+    for (int h = wave; h < a.nheads; h += 4) {
+        uint16_t* v = a.x + r * a.row_stride + (int64_t)h * hd;
+        float x0 = active ? bf2f(v[i0]) : 0.f;
+        float x1 = active ? bf2f(v[i1]) : 0.f;
+        float y0, y1;
+        if (!a.rope) {
+            const float rms = sqrtf((tree_sum64(x0 * x0 + x1 * x1) / (float)hd) + a.eps);
+            if (hf) {
+                const float inv = 1.0f / rms;
+                y0 = bf2f(a.w[i0]) * rbf(x0 * inv);
+                y1 = bf2f(a.w[i1]) * rbf(x1 * inv);
+            } else {
+                y0 = (x0 / rms) * bf2f(a.w[i0]);
+                y1 = (x1 / rms) * bf2f(a.w[i1]);
+            }
+        } else if (hf) {
+            y0 = rbf(rbf(x0 * c) + rbf(-x1 * s));
+            y1 = rbf(rbf(x1 * c) + rbf(x0 * s));
+        } else {
+            y0 = x0 * c - x1 * s;
+            y1 = x1 * c + x0 * s;
+        }
+        if (active) {
+            v[i0] = f2bf(y0);
+            v[i1] = f2bf(y1);
+        }
+    }
+}
+
+// K/V rows [rows][nkv * hd] (row stride ld) -> cache positions pos0 + r of sequence `seq`
+// (kv_copy_layer_to_cache_prefill / _decode, include_cuda.cu:165-279).  Block per row,
+// one 16-byte chunk per thread.
+template <bool PG>
+__global__ __launch_bounds__(256) void kv_write_kernel(const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
+                                                       int64_t ld, int pos0, uint16_t* kc, uint16_t* vc, KvMap km,
+                                                       int seq, int layer, int nkv, int hd) {
+    const int64_t r = blockIdx.x;
+    const int p = pos0 + (int)r;
+    const int cph = hd / 8;
+    for (int i = threadIdx.x; i < 2 * nkv * cph; i += 256) {
+        const int which = i / (nkv * cph), j = i % (nkv * cph), g = j / cph, ch = j % cph;
+        const uint16_t* src = (which ? v : k) + r * ld + g * hd + ch * 8;
+        uint16_t* dst = (which ? vc : kc) + kv_run_off(km, (int64_t)layer * nkv + g, hd) + kv_tok<PG>(km, seq, p, hd) +
+                        ch * 8;
+        *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+    }
+}
+
+// activation (SiLU.cu:10-23): x = bf16(x * (1 / (1 + expf(-x)))), in place
+__global__ __launch_bounds__(256) void silu_kernel(uint4* __restrict__ x, int64_t n8) {
+#pragma clang fp contract(off)
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+        const uint4 g = x[i];
+        const uint32_t ga[4] = {g.x, g.y, g.z, g.w};
+        uint32_t o[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const float g0 = bf_lo(ga[j]), g1 = bf_hi(ga[j]);
+            o[j] = pack2(g0 * (1.0f / (1.0f + expf(-g0))), g1 * (1.0f / (1.0f + expf(-g1))));
+        }
+        x[i] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+}
+
+// element_mul (element_add.cu:4-12): c = bf16(a * b)
+__global__ __launch_bounds__(256) void mul_kernel(const uint4* __restrict__ a, const uint4* __restrict__ b,
+                                                  uint4* __restrict__ c, int64_t n8) {
+#pragma clang fp contract(off)
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+        const uint4 x = a[i], y = b[i];
+        const uint32_t aa[4] = {x.x, x.y, x.z, x.w}, bb[4] = {y.x, y.y, y.z, y.w};
+        uint32_t o[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) o[j] = pack2(bf_lo(aa[j]) * bf_lo(bb[j]), bf_hi(aa[j]) * bf_hi(bb[j]));
+        c[i] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+}
+
 // ----------------------------------------------------------- elementwise
 __global__ __launch_bounds__(256) void silu_mul_kernel(const uint4* __restrict__ g,
                                                        const uint4* __restrict__ u,
@@ -500,6 +624,82 @@ int qie_qkv_post(const void* qkv, int64_t M, const int32_t* pos, int32_t rows_pe
     a.q_out = (uint16_t*)q_out;
     hipLaunchKernelGGL((a.km.table ? qkv_post_kernel<true> : qkv_post_kernel<false>), dim3((unsigned)M), dim3(256), 0,
                        (hipStream_t)stream, a);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+
+int qie_memcpy_d2d(void* dst, const void* src, int64_t bytes, void* stream) {
+    QIE_REQUIRE(dst && src && bytes >= 0, "qie_memcpy_d2d: bad arguments");
+    if (bytes == 0) return 0;
+    QIE_HIP(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return 0;
+}
+
+int qie_qknorm(void* x, int64_t rows, int64_t row_stride, int32_t n_heads, int32_t head_dim, const void* w,
+               float eps, int32_t numerics, void* stream) {
+    QIE_REQUIRE(w, "qie_qknorm: null weight");
+    HeadOpArgs a{};
+    a.x = (uint16_t*)x; a.row_stride = row_stride; a.nheads = n_heads; a.hd = head_dim;
+    a.w = (const uint16_t*)w; a.eps = eps; a.numerics = numerics; a.rope = 0;
+    QIE_REQUIRE(a.x && rows >= 0 && n_heads > 0 && head_dim > 0 && head_dim % 2 == 0 && head_dim <= 128 &&
+                    row_stride >= (int64_t)n_heads * head_dim,
+                "qie_qknorm: bad arguments (head_dim even and <= 128, row_stride >= n_heads * head_dim)");
+    if (rows == 0) return 0;
+    hipLaunchKernelGGL(head_op_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, a);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+
+int qie_rope(void* x, int64_t rows, int64_t row_stride, int32_t n_heads, int32_t head_dim, const int32_t* pos,
+             int32_t pos0, const float* rope_cos, const float* rope_sin, int32_t numerics, void* stream) {
+    QIE_REQUIRE(rope_cos && rope_sin && pos0 >= 0, "qie_rope: bad tables / position");
+    HeadOpArgs a{};
+    a.x = (uint16_t*)x; a.row_stride = row_stride; a.nheads = n_heads; a.hd = head_dim;
+    a.cs = rope_cos; a.sn = rope_sin; a.pos = pos; a.pos0 = pos0; a.numerics = numerics; a.rope = 1;
+    QIE_REQUIRE(a.x && rows >= 0 && n_heads > 0 && head_dim > 0 && head_dim % 2 == 0 && head_dim <= 128 &&
+                    row_stride >= (int64_t)n_heads * head_dim,
+                "qie_rope: bad arguments (head_dim even and <= 128, row_stride >= n_heads * head_dim)");
+    if (rows == 0) return 0;
+    hipLaunchKernelGGL(head_op_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, a);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+
+int qie_kv_write(const void* k, const void* v, int64_t rows, int64_t ld, int32_t pos0, const qie_kv_cache* cache,
+                 int32_t seq, int32_t layer, void* stream) {
+    QIE_REQUIRE(k && v && cache && rows >= 0 && pos0 >= 0 && seq >= 0 && layer >= 0 && layer < cache->n_layers,
+                "qie_kv_write: bad arguments");
+    QIE_REQUIRE(pos0 + rows <= cache->max_ctx, "qie_kv_write: positions %d..%lld exceed max_ctx %d", pos0,
+                (long long)(pos0 + rows - 1), cache->max_ctx);
+    QIE_REQUIRE(cache->head_dim % 8 == 0 && ld >= (int64_t)cache->n_kv_heads * cache->head_dim && ld % 8 == 0 &&
+                    ((uintptr_t)k % 16) == 0 && ((uintptr_t)v % 16) == 0,
+                "qie_kv_write: rows must be 16-byte aligned with ld >= n_kv_heads * head_dim, ld % 8 == 0");
+    if (rows == 0) return 0;
+    KvMap km;
+    QIE_TRY(kv_map_make(cache, &km, "qie_kv_write"));
+    hipLaunchKernelGGL((km.table ? kv_write_kernel<true> : kv_write_kernel<false>), dim3((unsigned)rows), dim3(256), 0,
+                       (hipStream_t)stream, (const uint16_t*)k, (const uint16_t*)v, ld, pos0, (uint16_t*)cache->k,
+                       (uint16_t*)cache->v, km, seq, layer, cache->n_kv_heads, cache->head_dim);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+
+int qie_silu(void* x, int64_t n, void* stream) {
+    QIE_REQUIRE(x && n >= 0 && n % 8 == 0, "qie_silu: bad arguments (n % 8 == 0)");
+    if (n == 0) return 0;
+    const int64_t n8 = n / 8;
+    hipLaunchKernelGGL(silu_kernel, dim3((unsigned)std::min<int64_t>((n8 + 255) / 256, 8192)), dim3(256), 0,
+                       (hipStream_t)stream, (uint4*)x, n8);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+
+int qie_mul(const void* a, const void* b, void* c, int64_t n, void* stream) {
+    QIE_REQUIRE(a && b && c && n >= 0 && n % 8 == 0, "qie_mul: bad arguments (n % 8 == 0)");
+    if (n == 0) return 0;
+    const int64_t n8 = n / 8;
+    hipLaunchKernelGGL(mul_kernel, dim3((unsigned)std::min<int64_t>((n8 + 255) / 256, 8192)), dim3(256), 0,
+                       (hipStream_t)stream, (const uint4*)a, (const uint4*)b, (uint4*)c, n8);
     QIE_LAUNCH_CHECK();
     return 0;
 }

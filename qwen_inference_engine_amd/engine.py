@@ -238,6 +238,37 @@ class Batch:
                    "qie_batch_block_table")
         return out
 
+    def reserve(self, seq: int, n_tokens: int) -> None:
+        """Operator tier: make `seq` live and hold KV pages for positions [0, n_tokens)."""
+        _lib.check(self.lib.qie_batch_reserve(self.h, seq, n_tokens), "qie_batch_reserve")
+
+    def kv_cache(self, seq: int) -> _lib.KvCacheC:
+        """KV descriptor of slot `seq` (kernels address it as sequence 0)."""
+        c = _lib.KvCacheC()
+        _lib.check(self.lib.qie_batch_kv_cache(self.h, seq, C.byref(c)), "qie_batch_kv_cache")
+        return c
+
+    def kv_rows(self, seq: int, layer: int, n: int):
+        """Host copy of the cached K and V rows [n_kv_heads][n][head_dim] (bf16 bits) of
+        positions [0, n) of `seq` at `layer` (diagnostics / tests)."""
+        c = self.kv_cache(seq)
+        hd, nkv, L = c.head_dim, c.n_kv_heads, c.n_layers
+        out = [np.zeros((nkv, n, hd), np.uint16), np.zeros((nkv, n, hd), np.uint16)]
+        if c.block_table:
+            T = c.page_tokens
+            pages = self.block_table(seq, (n + T - 1) // T)
+            runs = [(t0, min(n, t0 + T), int(pages[t0 // T]) * c.seq_stride, T) for t0 in range(0, n, T)]
+        else:
+            runs = [(0, n, 0, c.max_ctx)]
+        for which, base in enumerate((c.k, c.v)):
+            for t0, t1, off, run in runs:
+                for g in range(nkv):
+                    src = base + 2 * (off + ((layer * nkv + g) * run + (t0 % run if c.block_table else t0)) * hd)
+                    buf = np.zeros((t1 - t0, hd), np.uint16)
+                    _lib.check(self.lib.qie_memcpy_d2h(buf.ctypes.data, src, buf.nbytes), "kv_rows")
+                    out[which][g, t0:t1] = buf
+        return out
+
     def time_kernel(self, which: int = 0, iters: int = 20):
         us, by = C.c_double(), C.c_double()
         _lib.check(self.lib.qie_batch_time_kernel(self.h, which, iters, C.byref(us), C.byref(by)),

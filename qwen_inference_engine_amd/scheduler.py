@@ -29,6 +29,7 @@ class Request:
     max_new_tokens: int
     stop_ids: tuple = ()
     tokens: List[int] = dataclasses.field(default_factory=list)
+    logits: list = dataclasses.field(default_factory=list)   # per token, when keep_logits
     slot: int = -1
     pages: int = 0
     done: bool = False
@@ -36,8 +37,9 @@ class Request:
 
 class ContinuousBatcher:
     def __init__(self, engine: Engine, slots: int = 8, max_ctx: Optional[int] = None, page_tokens: int = 128,
-                 n_pages: int = 0, sampling: Sampling = GREEDY):
+                 n_pages: int = 0, sampling: Sampling = GREEDY, keep_logits: bool = False):
         self.batch: Batch = engine.batch(slots, max_ctx, page_tokens=page_tokens, n_pages=n_pages)
+        self.keep_logits = keep_logits          # copy each token's logit row (tests / diagnostics)
         self.max_ctx = self.batch.max_ctx
         self.sampling = sampling
         free, _, self.page_tokens = self.batch.page_stats()
@@ -69,8 +71,10 @@ class ContinuousBatcher:
         self.budget += r.pages
         r.slot = -1
 
-    def _emit(self, r: Request, tok: int, out: list) -> None:
+    def _emit(self, r: Request, tok: int, out: list, logits=None) -> None:
         r.tokens.append(tok)
+        if self.keep_logits:
+            r.logits.append((self.batch.logits() if logits is None else logits)[r.slot].copy())
         out.append((r.rid, tok))
         if len(r.tokens) >= r.max_new_tokens or tok in r.stop_ids:
             self._finish(r)
@@ -96,9 +100,10 @@ class ContinuousBatcher:
         if any(s is not None for s in self.slots):
             live = list(self.slots)
             ids = self.batch.decode_step(self.sampling)
+            lg = self.batch.logits() if self.keep_logits else None
             for i, r in enumerate(live):
                 if r is not None and not r.done:
-                    self._emit(r, int(ids[i]), out)
+                    self._emit(r, int(ids[i]), out, lg)
         return out
 
     def idle(self) -> bool:

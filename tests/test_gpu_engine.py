@@ -3,7 +3,10 @@ oracle's full forward on identical synthetic weights and prompts.
 
 Bar (written per check):
 * logits: every step's bf16 logits within 4 bf16 ulps of the largest |logit| of the
-  oracle's (fp32 summation order differs inside every dot product, 2-80 layers deep);
+  oracle's (fp32 summation order differs inside every dot product, 2-80 layers deep),
+  and norm-relative within tests/parity.py's bar: max(1e-3, 2 x the oracle's own
+  order-0 vs order-2 spread on the same step) — 1e-3 alone is below the reference
+  algorithm's own order sensitivity (3e-3 .. 9e-3 on these models, DESIGN.md §5);
 * greedy ids: TEACHER-FORCED — at every step the engine's arg-max must equal the
   oracle's unless the oracle's own logits put the two tokens within that same tolerance
   (a near-tie, where any fp32 reordering may flip a bf16 arg-max); the oracle's token is
@@ -17,6 +20,7 @@ import pytest
 
 import gpu_util as G
 from conftest import rng
+from parity import OrderPair, check_step
 
 import qwen_inference_engine_amd as Q
 from qwen_inference_engine_amd import spec as S, weights as W
@@ -51,23 +55,25 @@ def logits_close(got, want, what=""):
 
 
 def forced_compare(oracle, b, om, prompt, n_new, seq=0):
-    """Teacher-forced greedy comparison; returns (oracle ids, near-tie flips)."""
-    lg_o = om.forward(prompt, 0)
+    """Teacher-forced greedy comparison under tests/parity.py's bar (`om` is an oracle
+    Model or a parity.OrderPair); returns (oracle ids, near-tie flips)."""
+    pair = om if isinstance(om, OrderPair) else None
+    fwd = (lambda ids, start=None: pair.forward(ids, start)) if pair else \
+        (lambda ids, start=None: (om.forward(ids, start), None))
+    lg0, lg2 = fwd(prompt, 0)
     t_e = b.prefill(seq, prompt)
     ids, flips = [], 0
     for i in range(n_new):
         lg_e = b.logits()[seq]
-        logits_close(lg_e, lg_o, f"step {i}")
-        t_o = oracle.argmax(lg_o)
+        logits_close(lg_e, lg0, f"step {i}")
+        t_o = oracle.argmax(lg0)
+        flips += check_step(lg_e, lg0, lg2, t_e, t_o, f"step {i}")
         if t_e != t_o:
-            gap = abs(float(G.bf(lg_o[t_o])) - float(G.bf(lg_o[t_e])))
-            assert gap <= logit_tol(lg_o), f"step {i}: engine {t_e} vs oracle {t_o}, oracle gap {gap}"
-            flips += 1
             b.set_position(seq, len(prompt) + i, t_o)
         ids.append(t_o)
         if i + 1 < n_new:
             t_e = b.decode_step()[seq]
-            lg_o = om.forward([t_o])
+            lg0, lg2 = fwd([t_o])
     return ids, flips
 
 
@@ -79,7 +85,7 @@ def test_greedy_generation_matches_oracle(oracle, name, num, P):
     eng, hw, om = make_pair(spec, oracle)
     prompt = list(rng(P).integers(0, spec.vocab, P))
     n_new = 16
-    ids, flips = forced_compare(oracle, eng.batch(1, 128), om, prompt, n_new)
+    ids, flips = forced_compare(oracle, eng.batch(1, 128), OrderPair(oracle, hw, 128), prompt, n_new)
     assert flips <= 2, f"{flips} near-tie flips in {n_new} steps"
 
 
@@ -226,3 +232,23 @@ def test_qwen2_7b_widths_two_layers_match_oracle(oracle):
     prompt = list(rng(2).integers(0, spec.vocab, 24))
     ids, flips = forced_compare(oracle, eng.batch(1, 64), om, prompt, 6)
     assert flips <= 2
+
+
+@pytest.mark.parametrize("paged", [False, True])
+def test_short_prefill_after_long_prefill(oracle, paged):
+    """Prompts of <= 8 tokens run the split prefill attention, which needs a workspace
+    that longer prompts do not; a short prefill after a long one in the same batch must
+    size it (it once wrote its split partials past a 16-byte buffer).  Ids and logits equal
+    the same short prompt in a fresh batch, bit for bit."""
+    spec = CONFIGS["qwen2-bias-hd64"]
+    eng = Q.Engine(spec, max_ctx=256).init_synthetic(SYN)
+    pt = 128 if paged else None
+    b = eng.batch(2, 256, page_tokens=pt)
+    b.prefill(0, list(rng(1).integers(0, spec.vocab, 40)))
+    short = list(rng(2).integers(0, spec.vocab, 3))
+    got = [b.prefill(1, short)] + [int(t) for t in b.decode(6)[:, 1]]
+    lg = b.logits()[1]
+    f = eng.batch(2, 256, page_tokens=pt)
+    want = [f.prefill(1, short)] + [int(t) for t in f.decode(6)[:, 1]]
+    assert got == want
+    assert np.array_equal(lg, f.logits()[1])

@@ -131,9 +131,9 @@ def test_fp8_engine_matches_oracle_on_dequantised_model(oracle, name, P):
     spec = CONFIGS[name]
     eng = Q.Engine(spec, max_ctx=128, weight_fp8=True).init_synthetic(SYN)
     hw = W.HostWeights.synthetic(spec, SYN).fp8_dequantized()
-    om = oracle.Model(hw, 128)
+    from parity import OrderPair
     prompt = list(rng(P).integers(0, spec.vocab, P))
-    ids, flips = forced_compare(oracle, eng.batch(1, 128), om, prompt, 12)
+    ids, flips = forced_compare(oracle, eng.batch(1, 128), OrderPair(oracle, hw, 128), prompt, 12)
     assert flips <= 2
 
 

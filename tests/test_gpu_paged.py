@@ -269,3 +269,59 @@ def test_continuous_batcher_matches_isolated_runs():
             want.append(b.decode_step()[0])
         b.close()
         assert got[rid] == want, f"request {rid}"
+
+
+def test_batcher_unused_slots_long_run_matches_oracle(oracle):
+    """More slots than concurrent requests and more total steps than max_ctx, on a pool
+    with one spare page: unused slots idle from creation (no pool pages, rewound before
+    max_ctx), so the run never exhausts the pool.  Every request's tokens and logits are
+    checked against or_forward, the oracle following the batcher's own tokens (so a
+    near-tie never derails the comparison): logits within 4 bf16 ulps of max|logit|, and
+    each chosen token the oracle's arg-max or a near-tie within that tolerance."""
+    from qwen_inference_engine_amd.scheduler import ContinuousBatcher
+    from test_gpu_engine import logit_tol
+    eng = Q.Engine(SPEC, max_ctx=256).init_synthetic(SYN)
+    hw = W.HostWeights.synthetic(SPEC, SYN)
+    cb = ContinuousBatcher(eng, slots=4, max_ctx=256, page_tokens=128, n_pages=3, keep_logits=True)
+    reqs, steps = [], 0
+    for i in range(4):   # one request at a time: 3 slots stay unused throughout
+        pr = [int(t) for t in rng(90 + i).integers(0, SPEC.vocab, 20 + 30 * i)]
+        rid = cb.submit(pr, 100)
+        while not cb.idle():
+            cb.step()
+            steps += 1
+        reqs.append((rid, pr))
+    assert steps > 256                                 # longer than max_ctx in total
+    assert cb.batch.page_stats()[0] == 2               # every page back in the pool
+    flips = 0
+    for rid, pr in reqs:
+        r = cb.requests[rid]
+        om = oracle.Model(hw, 256)
+        lg = om.forward(pr, 0)
+        for t, (tok, got) in enumerate(zip(r.tokens, r.logits)):
+            d = np.abs(G.bf(got).astype(np.float64) - G.bf(lg))
+            assert d.max() <= logit_tol(lg), f"request {rid} token {t}: {d.max()}"
+            want = oracle.argmax(lg)
+            if tok != want:
+                assert abs(float(G.bf(lg[want])) - float(G.bf(lg[tok]))) <= logit_tol(lg)
+                flips += 1
+            if t + 1 < len(r.tokens):
+                lg = om.forward([tok])
+    assert flips <= 3
+
+
+def test_failed_reprefill_leaves_live_slot_intact():
+    """A prefill into a live slot that the pool cannot hold fails with nothing changed:
+    the slot keeps its pages and continues exactly like an untouched run."""
+    eng = Q.Engine(SPEC, max_ctx=512).init_synthetic(SYN)
+    pr = list(rng(3).integers(0, SPEC.vocab, 100))
+    ref = eng.batch(1, 512, page_tokens=128, n_pages=3)
+    t0 = ref.prefill(0, pr)
+    want = list(ref.decode(60)[:, 0])
+    pb = eng.batch(1, 512, page_tokens=128, n_pages=3)
+    assert pb.prefill(0, pr) == t0
+    held = pb.page_stats()[1][0]
+    with pytest.raises(_lib.QieError):
+        pb.prefill(0, list(rng(4).integers(0, SPEC.vocab, 400)))   # 4 pages; 1 held + 1 free
+    assert pb.page_stats()[1][0] == held
+    assert list(pb.decode(60)[:, 0]) == want

@@ -132,8 +132,11 @@ static int g_sum_order = 0;
  *       (k / 8 mod 64), combined by a float pairwise tree;
  *   2 = EVERY fp32 reduction reordered: matmul as 1; RMSNorm sum of squares as 256
  *       strided partials + pairwise tree; qk-norm sequential; attention dot products as
- *       8 interleaved partials + tree, softmax denominator and P.V accumulated per
- *       128-key block then summed across blocks.
+ *       8 interleaved partials + tree, and the attention in the online-softmax form any
+ *       split / tiled kernel computes: exp2((s - m) log2 e) (the -use_fast_math
+ *       __expf of the reference build, flags.make:10), softmax denominator and P.V
+ *       accumulated per 128-key block, P.V divided by the denominator AFTER the sum;
+ *       SiLU's exponent in the same fast-math form.
  * The logit spread between variant 0 and 1 / 2 at a given depth is the reference
  * algorithm's own order sensitivity, which sizes the end-to-end parity tolerance
  * (bench.py cpu_baseline, tests/test_gpu_headline.py, DESIGN.md "Parity"). */
@@ -337,7 +340,10 @@ void or_rope(bf16_t* x, const float* cos_t, const float* sin_t, const int32_t* p
 void or_silu_mul(const bf16_t* gate, const bf16_t* up, bf16_t* h, int64_t n) {
     for (int64_t i = 0; i < n; i++) {
         float g = bf2f(gate[i]);
-        float a = rbf(g * (1.0f / (1.0f + expf(-g))));
+        // order 2: the reference build's -use_fast_math exponent (flags.make:10), which a
+        // GPU libm need not match to the last ulp either
+        const float ex = g_sum_order == 2 ? exp2f(-g * 1.44269504088896341f) : expf(-g);
+        float a = rbf(g * (1.0f / (1.0f + ex)));
         h[i] = f2bf(bf2f(up[i]) * a);
     }
 }
@@ -400,15 +406,31 @@ void or_attention(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, bf16_t* o
                 float mx = -1e9f;
                 for (int t = 0; t < mkv; t++) mx = fmaxf(mx, score[t]);
                 float sum = 0.f;
-                if (g_sum_order == 2) {   // per 128-key block, then across blocks
+                if (g_sum_order == 2) {
+                    // the online-softmax (flash) formulation every split / tiled kernel uses:
+                    // exponent as exp2((s - m) * log2 e) (the reference build's -use_fast_math
+                    // __expf), per-128-key block sums, and P.V normalised AFTER the
+                    // accumulation instead of p /= S before it
+                    bf16_t* orow = out + (int64_t)qt * nq * hd + (int64_t)h * hd;
                     for (int t0 = 0; t0 < mkv; t0 += 128) {
                         float bs = 0.f;
                         for (int t = t0; t < std::min(mkv, t0 + 128); t++) {
-                            score[t] = expf(score[t] - mx);
+                            score[t] = exp2f((score[t] - mx) * 1.44269504088896341f);
                             bs += score[t];
                         }
                         sum += bs;
                     }
+                    for (int d = 0; d < hd; d++) {
+                        float acc = 0.f;
+                        for (int t0 = 0; t0 < mkv; t0 += 128) {
+                            float ba = 0.f;
+                            for (int t = t0; t < std::min(mkv, t0 + 128); t++)
+                                ba += score[t] * bf2f(vh[(int64_t)t * hd + d]);
+                            acc += ba;
+                        }
+                        orow[d] = f2bf(acc / sum);
+                    }
+                    continue;
                 } else {
                     for (int t = 0; t < mkv; t++) {
                         score[t] = expf(score[t] - mx);
@@ -419,16 +441,7 @@ void or_attention(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, bf16_t* o
                 bf16_t* orow = out + (int64_t)qt * nq * hd + (int64_t)h * hd;
                 for (int d = 0; d < hd; d++) {
                     float acc = 0.f;
-                    if (g_sum_order == 2) {
-                        for (int t0 = 0; t0 < mkv; t0 += 128) {
-                            float ba = 0.f;
-                            for (int t = t0; t < std::min(mkv, t0 + 128); t++)
-                                ba += score[t] * bf2f(vh[(int64_t)t * hd + d]);
-                            acc += ba;
-                        }
-                    } else {
-                        for (int t = 0; t < mkv; t++) acc += score[t] * bf2f(vh[(int64_t)t * hd + d]);
-                    }
+                    for (int t = 0; t < mkv; t++) acc += score[t] * bf2f(vh[(int64_t)t * hd + d]);
                     orow[d] = f2bf(acc);
                 }
             }

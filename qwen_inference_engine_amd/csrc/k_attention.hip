@@ -888,10 +888,10 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
                         sacc[q][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[q][ks], sacc[q][t], 0, 0, 0);
                 }
             }
-            bf16x8_t pa[QG][2];
+            float pv[QG][4][4];   // this tile's probabilities (fp32), split into bf16 parts at P.V
 #pragma unroll
             for (int q = 0; q < QG; q++) {
-                float sv[4][4];
+                float (&sv)[4][4] = pv[q];
                 float mt = -INFINITY;
 #pragma unroll
                 for (int t = 0; t < 4; t++)
@@ -924,17 +924,24 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
                 for (int d = 0; d < DT; d++)
 #pragma unroll
                     for (int r = 0; r < 4; r++) oacc[q][d][r] *= ar[r];
-#pragma unroll
-                for (int c = 0; c < 2; c++)
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        pa[q][c][j] = (__bf16)sv[2 * c][j];
-                        pa[q][c][4 + j] = (__bf16)sv[2 * c + 1][j];
-                    }
             }
             const int q4 = fr >> 2, p4 = fr & 3;
 #pragma unroll
             for (int c = 0; c < 2; c++) {
+                // P = hi + mid + lo: three bf16 parts carry all 24 bits of each fp32
+                // probability, so the P.V products are the reference's fp32 products
+                // (self_attension.cu:127-135); only the accumulation order differs
+                bf16x8_t ph[QG], pm[QG], pl[QG];
+#pragma unroll
+                for (int q = 0; q < QG; q++)
+#pragma unroll
+                    for (int j = 0; j < 8; j++) {
+                        const float e = pv[q][2 * c + (j >> 2)][j & 3];
+                        ph[q][j] = (__bf16)e;
+                        const float r1 = e - (float)ph[q][j];
+                        pm[q][j] = (__bf16)r1;
+                        pl[q][j] = (__bf16)(r1 - (float)pm[q][j]);
+                    }
 #pragma unroll
                 for (int d = 0; d < DT; d++) {
                     // rows vr and vr + 16 share vswz: one column offset serves both reads
@@ -947,8 +954,11 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
                     const bf16x8_t vb8 =
                         __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
-                    for (int q = 0; q < QG; q++)
-                        oacc[q][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[q][c], vb8, oacc[q][d], 0, 0, 0);
+                    for (int q = 0; q < QG; q++) {
+                        oacc[q][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph[q], vb8, oacc[q][d], 0, 0, 0);
+                        oacc[q][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pm[q], vb8, oacc[q][d], 0, 0, 0);
+                        oacc[q][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pl[q], vb8, oacc[q][d], 0, 0, 0);
+                    }
                 }
             }
         }
@@ -1582,14 +1592,18 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
         for (int d = 0; d < DTW; d++)
 #pragma unroll
             for (int r = 0; r < 4; r++) oacc[d][r] *= ar[r];
-        // ---- O[:, slice] += P . V[:, slice], P = hi + lo
+        // ---- O[:, slice] += P . V[:, slice], P = hi + mid + lo: three bf16 parts hold all
+        // 24 bits of the fp32 probability, so every P.V product is the reference's fp32
+        // product (self_attension.cu:127-135) — only the accumulation order differs
 #pragma unroll
         for (int c = 0; c < 4; c++) {
-            bf16x8_t ph, pl;
+            bf16x8_t ph, pm, pl;
 #pragma unroll
             for (int j = 0; j < 8; j++) {
                 ph[j] = (__bf16)e[c][j];
-                pl[j] = (__bf16)(e[c][j] - (float)ph[j]);
+                const float r1 = e[c][j] - (float)ph[j];
+                pm[j] = (__bf16)r1;
+                pl[j] = (__bf16)(r1 - (float)pm[j]);
             }
 #pragma unroll
             for (int d = 0; d < DTW; d++) {
@@ -1600,6 +1614,7 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
                     (__attribute__((address_space(3))) i16x4_t*)(a0 + 4 * DW));
                 const bf16x8_t vb8 = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
                 oacc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph, vb8, oacc[d], 0, 0, 0);
+                oacc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pm, vb8, oacc[d], 0, 0, 0);
                 oacc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pl, vb8, oacc[d], 0, 0, 0);
             }
         }
@@ -1697,11 +1712,11 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
         mx = mb;
     }
     if (has_item) {
-        const float inv = 1.0f / ls;
         uint16_t* dst = a.out + m * (int64_t)nq * HD + (int64_t)(g * G + gi) * HD + d4 * 4;
-        // write-through 8-B store: the fused O-proj workgroups read it with sc1 loads
-        const unsigned long long pk = (unsigned long long)pack2(acc.x * inv, acc.y * inv) |
-                                      ((unsigned long long)pack2(acc.z * inv, acc.w * inv) << 32);
+        // write-through 8-B store: the fused O-proj workgroups read it with sc1 loads;
+        // divided (not multiplied by 1/l): the softmax normalisation's one rounding
+        const unsigned long long pk = (unsigned long long)pack2(acc.x / ls, acc.y / ls) |
+                                      ((unsigned long long)pack2(acc.z / ls, acc.w / ls) << 32);
         __hip_atomic_store(reinterpret_cast<unsigned long long*>(dst), pk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (tid == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -37,3 +37,17 @@ def _release_device_buffers():
 
 def rng(seed=0):
     return np.random.default_rng(seed)
+
+
+def pytest_sessionfinish(session, exitstatus):
+    """On the GPU box, keep every end-to-end parity step's (engine error, bar) as evidence."""
+    import json
+    try:
+        import parity
+    except Exception:
+        return
+    if parity.REPORT and os.environ.get("GRAFT_REPO_ROOT"):
+        out = os.path.join(ROOT, "gpurun_out")
+        os.makedirs(out, exist_ok=True)
+        with open(os.path.join(out, "parity_report.json"), "w") as f:
+            json.dump([{"step": w, "norm_rel": r, "bar": b} for w, r, b in parity.REPORT], f, indent=0)

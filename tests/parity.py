@@ -9,9 +9,18 @@ measured in this container).  The bar is therefore measured per i
 
 * logits: norm-relative error of the engine vs the oracle (order 0) within
   max(1e-3, 2 x the norm-relative spread between oracle order 0 and order 2 — every fp32
-  reduction reordered — on the same input, same step);
+  reduction reordered — on the same input), the spread taken as its maximum over the
+  whole teacher-forced run (both orders follow the same ids, so the oracle trace is
+  computed first; a single step's two orders can coincide by chance, the sensitivity is
+  a property of the model and prompt, and the engine's error is held to the same
+  statistic: every step within 2 x the run's worst oracle spread), together with the
+  spread of a fixed calibration run of the same model (a short run can be degenerate:
+  with fp8-dequantised weights every product is exact and two orders may agree on all
+  of a 5-token prompt's steps, while one 1-ulp rounding of a transcendental — ocml vs
+  glibc expf, both within the C standard's 1 ulp — moves the logits by ~4e-3);
 * greedy ids (teacher-forced): equal, or a near-tie whose oracle top-2 gap is within
-  max(2 bf16 ulps of max|logit|, the oracle's own max |order-2 - order-0| logit spread).
+  max(2 bf16 ulps of max|logit|, the oracle's own max |order-2 - order-0| logit spread
+  over the run); the number of such flips is bounded by max_flips(decisions).
 """
 import numpy as np
 
@@ -19,6 +28,13 @@ import gpu_util as G
 
 NORM_REL = 1e-3
 SPREAD_FACTOR = 2.0
+REPORT = []   # (what, engine norm-rel error, bar) of every checked step; conftest writes it out
+
+
+def max_flips(decisions: int) -> int:
+    """Near-tie flips tolerated over `decisions` greedy choices (each one already
+    individually within the oracle's own order spread): 1 in 8, at least 2."""
+    return max(2, decisions // 8)
 
 
 def norm_rel(got, want) -> float:
@@ -28,12 +44,15 @@ def norm_rel(got, want) -> float:
 
 class OrderPair:
     """Two oracle models over the same weights: summation order 0 (the restatement) and
-    order 2 (every fp32 reduction reordered), stepped in lock-step."""
+    order 2 (every fp32 reduction reordered), stepped in lock-step; tracks the running
+    maxima of their norm-relative and absolute logit spreads."""
 
     def __init__(self, oracle, hw, max_ctx, nthreads=0, with_spread=True):
         self.O = oracle
         self.m0 = oracle.Model(hw, max_ctx, nthreads=nthreads)
         self.m2 = oracle.Model(hw, max_ctx, nthreads=nthreads) if with_spread else None
+        self.rel_spread = 0.0
+        self.abs_spread = 0.0
 
     def forward(self, ids, start=None):
         lg0 = self.m0.forward(ids, start)
@@ -44,26 +63,49 @@ class OrderPair:
                 lg2 = self.m2.forward(ids, start)
             finally:
                 self.O.set_sum_order(0)
+            self.rel_spread = max(self.rel_spread, norm_rel(lg2, lg0))
+            self.abs_spread = max(self.abs_spread,
+                                  float(np.abs(G.bf(lg2).astype(np.float64) - G.bf(lg0)).max()))
         return lg0, lg2
 
+    def calibrate(self, vocab, n_prompt=24, n_steps=6, seed=12345):
+        """Spread of a fixed teacher-forced calibration run on fresh oracle models (same
+        weights); folds into the running maxima."""
+        cal = OrderPair(self.O, self.m0.hw, n_prompt + n_steps + 2, self.m0.nthreads)
+        prompt = [int(t) for t in np.random.default_rng(seed).integers(0, vocab, n_prompt)]
+        oracle_trace(self.O, cal, prompt, n_steps)
+        self.rel_spread = max(self.rel_spread, cal.rel_spread)
+        self.abs_spread = max(self.abs_spread, cal.abs_spread)
+        return self
 
-def bars(lg0, lg2):
-    """(norm-relative bar, near-tie gap bar) for one step."""
-    if lg2 is None:
-        return NORM_REL, 2 * 2.0 ** -7 * float(np.abs(G.bf(lg0)).max())
-    rel = max(NORM_REL, SPREAD_FACTOR * norm_rel(lg2, lg0))
-    gap = max(2 * 2.0 ** -7 * float(np.abs(G.bf(lg0)).max()),
-              float(np.abs(G.bf(lg2).astype(np.float64) - G.bf(lg0)).max()))
-    return rel, gap
+    def bars(self, lg0):
+        """(norm-relative bar, near-tie gap bar) for a step whose order-0 logits are lg0."""
+        ulps = 2 * 2.0 ** -7 * float(np.abs(G.bf(lg0)).max())
+        return max(NORM_REL, SPREAD_FACTOR * self.rel_spread), max(ulps, self.abs_spread)
 
 
-def check_step(got_lg, lg0, lg2, got_id, want_id, what, bar=None):
-    """Asserts the logit bar; returns 1 for a tolerated near-tie flip, else 0."""
-    rel_bar, gap_bar = bar if bar is not None else bars(lg0, lg2)
+def check_step(got_lg, lg0, pair, got_id, want_id, what, bar=None):
+    """Asserts the logit bar (`pair`'s running spreads, or an explicit (rel, gap) `bar`);
+    returns 1 for a tolerated near-tie flip, else 0."""
+    rel_bar, gap_bar = bar if bar is not None else pair.bars(lg0)
     rel = norm_rel(got_lg, lg0)
+    REPORT.append((what, rel, rel_bar))
     assert rel <= rel_bar, f"{what}: norm-relative logit error {rel:.3e} > bar {rel_bar:.3e}"
     if got_id != want_id:
         gap = abs(float(G.bf(lg0[want_id])) - float(G.bf(lg0[got_id])))
         assert gap <= gap_bar, f"{what}: engine {got_id} vs oracle {want_id}, oracle gap {gap} > {gap_bar}"
         return 1
     return 0
+
+
+def oracle_trace(oracle, pair, prompt, n_steps, forced=None):
+    """Teacher-forced oracle run: order-0 (and order-2) logits of the prompt and of
+    n_steps - 1 decode steps fed the order-0 arg-max (or `forced[i]`).  Returns
+    (ids, [(lg0, lg2), ...]); pair's spreads are then the whole run's maxima."""
+    outs = [pair.forward(prompt, 0)]
+    ids = [oracle.argmax(outs[0][0])]
+    for i in range(n_steps - 1):
+        nxt = ids[-1] if forced is None else forced[i]
+        outs.append(pair.forward([nxt]))
+        ids.append(oracle.argmax(outs[-1][0]))
+    return ids, outs

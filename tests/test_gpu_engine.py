@@ -20,7 +20,7 @@ import pytest
 
 import gpu_util as G
 from conftest import rng
-from parity import OrderPair, check_step
+from parity import OrderPair, check_step, max_flips, oracle_trace
 
 import qwen_inference_engine_amd as Q
 from qwen_inference_engine_amd import spec as S, weights as W
@@ -54,26 +54,23 @@ def logits_close(got, want, what=""):
     assert np.abs(g - w).max() <= logit_tol(want), f"{what}: max |dlogit| {np.abs(g - w).max()} > {logit_tol(want)}"
 
 
-def forced_compare(oracle, b, om, prompt, n_new, seq=0):
-    """Teacher-forced greedy comparison under tests/parity.py's bar (`om` is an oracle
-    Model or a parity.OrderPair); returns (oracle ids, near-tie flips)."""
-    pair = om if isinstance(om, OrderPair) else None
-    fwd = (lambda ids, start=None: pair.forward(ids, start)) if pair else \
-        (lambda ids, start=None: (om.forward(ids, start), None))
-    lg0, lg2 = fwd(prompt, 0)
+def forced_compare(oracle, b, pair, prompt, n_new, seq=0):
+    """Teacher-forced greedy comparison under tests/parity.py's bar (`pair` a
+    parity.OrderPair): the oracle trace first, then the engine forced onto its ids.
+    Returns (oracle ids, near-tie flips)."""
+    ids, outs = oracle_trace(oracle, pair, prompt, n_new)
+    pair.calibrate(b.e.spec.vocab)
     t_e = b.prefill(seq, prompt)
-    ids, flips = [], 0
+    flips = 0
     for i in range(n_new):
+        lg0 = outs[i][0]
         lg_e = b.logits()[seq]
         logits_close(lg_e, lg0, f"step {i}")
-        t_o = oracle.argmax(lg0)
-        flips += check_step(lg_e, lg0, lg2, t_e, t_o, f"step {i}")
-        if t_e != t_o:
-            b.set_position(seq, len(prompt) + i, t_o)
-        ids.append(t_o)
+        flips += check_step(lg_e, lg0, pair, t_e, ids[i], f"step {i}")
+        if t_e != ids[i]:
+            b.set_position(seq, len(prompt) + i, ids[i])
         if i + 1 < n_new:
             t_e = b.decode_step()[seq]
-            lg0, lg2 = fwd([t_o])
     return ids, flips
 
 
@@ -86,7 +83,7 @@ def test_greedy_generation_matches_oracle(oracle, name, num, P):
     prompt = list(rng(P).integers(0, spec.vocab, P))
     n_new = 16
     ids, flips = forced_compare(oracle, eng.batch(1, 128), OrderPair(oracle, hw, 128), prompt, n_new)
-    assert flips <= 2, f"{flips} near-tie flips in {n_new} steps"
+    assert flips <= max_flips(n_new), f"{flips} near-tie flips in {n_new} steps"
 
 
 def _teacher_forced_trace(b, prompts, n_new, forced=None):
@@ -218,7 +215,7 @@ def test_qwen2_0_5b_config1_greedy_matches_oracle(oracle):
     spec = S.QWEN2_0_5B
     eng, hw, om = make_pair(spec, oracle, max_ctx=64, syn=W.SynthParams(seed=0))
     prompt = list(rng(1).integers(0, spec.vocab, 16))
-    ids, flips = forced_compare(oracle, eng.batch(1, 64), om, prompt, 16)
+    ids, flips = forced_compare(oracle, eng.batch(1, 64), OrderPair(oracle, hw, 64), prompt, 16)
     assert flips <= 2
 
 
@@ -230,7 +227,7 @@ def test_qwen2_7b_widths_two_layers_match_oracle(oracle):
     spec = S.QWEN2_7B.replace(n_layers=2)
     eng, hw, om = make_pair(spec, oracle, max_ctx=64, syn=W.SynthParams(seed=0))
     prompt = list(rng(2).integers(0, spec.vocab, 24))
-    ids, flips = forced_compare(oracle, eng.batch(1, 64), om, prompt, 6)
+    ids, flips = forced_compare(oracle, eng.batch(1, 64), OrderPair(oracle, hw, 64), prompt, 6)
     assert flips <= 2
 
 

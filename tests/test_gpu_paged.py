@@ -307,7 +307,8 @@ def test_batcher_unused_slots_long_run_matches_oracle(oracle):
                 flips += 1
             if t + 1 < len(r.tokens):
                 lg = om.forward([tok])
-    assert flips <= 3
+    from parity import max_flips
+    assert flips <= max_flips(sum(len(cb.requests[rid].tokens) for rid, _ in reqs))
 
 
 def test_failed_reprefill_leaves_live_slot_intact():

@@ -38,11 +38,38 @@ using namespace qie;
 // Tensor-parallel shard of one rank (tp = 1: the whole model).  Column-parallel
 // QKV (by heads) and gate/up (by I), row-parallel O and down, vocab-parallel lm_head;
 // embedding, norms and the residual stream are replicated.
+// Heads: n_kv_heads % tp == 0 splits both head kinds evenly; otherwise, when
+// tp % n_kv_heads == 0, every kv head is replicated on rep = tp / n_kv_heads ranks and
+// the G = n_heads / n_kv_heads q heads of its group are split among those ranks as
+// evenly as they go (the first G % rep ranks take one more): Qwen2-7B (28 / 4 heads) at
+// TP 8 gives q heads 4,3,4,3,... with one kv head each.  Every q head lives
+// on exactly one rank, so the row-parallel O all-reduce still sums each head once.
 struct TpShard {
     int tp = 1, rank = 0;
     int nq = 0, nkv = 0, ffn = 0, vocab = 0;   // local counts
+    int q0 = 0, kv0 = 0;                        // first global q / kv head of this rank
     int64_t vocab0 = 0;                         // first global vocab row of this rank
 };
+
+// Head split of rank `rank` of `tp` (see TpShard); false when the heads do not shard.
+static bool shard_heads(int nq, int nkv, int tp, int rank, TpShard& sh) {
+    if (nkv % tp == 0 && nq % tp == 0) {
+        sh.nq = nq / tp;
+        sh.nkv = nkv / tp;
+        sh.q0 = rank * sh.nq;
+        sh.kv0 = rank * sh.nkv;
+        return true;
+    }
+    if (tp % nkv != 0) return false;
+    const int rep = tp / nkv, G = nq / nkv, g = rank / rep, sub = rank % rep;
+    if (rep > G) return false;   // a rank without q heads
+    const int base = G / rep, extra = G % rep;
+    sh.nkv = 1;
+    sh.kv0 = g;
+    sh.nq = base + (sub < extra ? 1 : 0);
+    sh.q0 = g * G + sub * base + std::min(sub, extra);
+    return true;
+}
 
 struct qie_engine {
     qie_model_spec spec{};   // the full model
@@ -574,10 +601,12 @@ int qie_engine_create(const qie_model_spec* spec, const qie_engine_opts* opts, q
                 "qie_engine_create: hidden/ffn must be multiples of 8 and head_dim 64 or 128");
     qie_comm* comm = opts ? (qie_comm*)opts->tp_comm : nullptr;
     const int tp = comm ? comm->world : 1;
-    QIE_REQUIRE(s.n_heads % tp == 0 && s.n_kv_heads % tp == 0 && s.ffn % tp == 0 && (s.ffn / tp) % 8 == 0 &&
+    TpShard probe;
+    QIE_REQUIRE(shard_heads(s.n_heads, s.n_kv_heads, tp, 0, probe) && s.ffn % tp == 0 && (s.ffn / tp) % 8 == 0 &&
                     s.vocab % tp == 0,
-                "qie_engine_create: tensor parallel %d needs n_heads, n_kv_heads, vocab divisible by it and "
-                "ffn / tp a multiple of 8 (use replicas for this model at this size)", tp);
+                "qie_engine_create: tensor parallel %d needs n_kv_heads divisible by it (or dividing it, with at "
+                "most n_heads / n_kv_heads ranks per kv head), vocab divisible by it and ffn / tp a multiple of 8 "
+                "(use replicas for this model at this size)", tp);
     qie_engine* e = new qie_engine();
     e->spec = s;
     if (opts) e->opts = *opts;
@@ -585,8 +614,7 @@ int qie_engine_create(const qie_model_spec* spec, const qie_engine_opts* opts, q
     e->comm = comm;
     e->sh.tp = tp;
     e->sh.rank = comm ? comm->rank : 0;
-    e->sh.nq = s.n_heads / tp;
-    e->sh.nkv = s.n_kv_heads / tp;
+    shard_heads(s.n_heads, s.n_kv_heads, tp, e->sh.rank, e->sh);
     e->sh.ffn = s.ffn / tp;
     e->sh.vocab = s.vocab / tp;
     e->sh.vocab0 = (int64_t)e->sh.rank * e->sh.vocab;
@@ -641,17 +669,18 @@ static ShardSlice plan_slice(const qie_index_entry& t, const qie_model_spec& s, 
     x.full_cols = x.cols;
     const int64_t hd = s.head_dim;
     const std::string& n = t.short_name;
-    auto rows_part = [&](int64_t local) { x.rows = local; x.row0 = (int64_t)sh.rank * local; };
-    auto cols_part = [&](int64_t local) { x.cols = local; x.col0 = (int64_t)sh.rank * local; };
+    auto rows_part = [&](int64_t local, int64_t first) { x.rows = local; x.row0 = first; };
+    auto cols_part = [&](int64_t local, int64_t first) { x.cols = local; x.col0 = first; };
     if (sh.tp == 1) return x;
-    if (n == "self_attn.q_proj.weight") rows_part(sh.nq * hd);                        // column-parallel
-    else if (n == "self_attn.k_proj.weight" || n == "self_attn.v_proj.weight") rows_part(sh.nkv * hd);
-    else if (n == "self_attn.q_proj.bias") cols_part(sh.nq * hd);
-    else if (n == "self_attn.k_proj.bias" || n == "self_attn.v_proj.bias") cols_part(sh.nkv * hd);
-    else if (n == "self_attn.o_proj.weight") cols_part(sh.nq * hd);                   // row-parallel
-    else if (n == "mlp.gate_proj.weight" || n == "mlp.up_proj.weight") rows_part(sh.ffn);
-    else if (n == "mlp.down_proj.weight") cols_part(sh.ffn);
-    else if (n == "logits") rows_part(sh.vocab);                                      // vocab-parallel
+    const int64_t qn = sh.nq * hd, q0 = (int64_t)sh.q0 * hd, kn = sh.nkv * hd, k0 = (int64_t)sh.kv0 * hd;
+    if (n == "self_attn.q_proj.weight") rows_part(qn, q0);                              // column-parallel
+    else if (n == "self_attn.k_proj.weight" || n == "self_attn.v_proj.weight") rows_part(kn, k0);
+    else if (n == "self_attn.q_proj.bias") cols_part(qn, q0);
+    else if (n == "self_attn.k_proj.bias" || n == "self_attn.v_proj.bias") cols_part(kn, k0);
+    else if (n == "self_attn.o_proj.weight") cols_part(qn, q0);                         // row-parallel
+    else if (n == "mlp.gate_proj.weight" || n == "mlp.up_proj.weight") rows_part(sh.ffn, (int64_t)sh.rank * sh.ffn);
+    else if (n == "mlp.down_proj.weight") cols_part(sh.ffn, (int64_t)sh.rank * sh.ffn);
+    else if (n == "logits") rows_part(sh.vocab, (int64_t)sh.rank * sh.vocab);          // vocab-parallel
     return x;
 }
 
@@ -1282,11 +1311,15 @@ int qie_engine_rope_tables(const qie_engine* e, const float** rope_cos, const fl
     return 0;
 }
 
+// Live per-kernel timing (bench.py's roofline line).  The launches cycle through layers
+// 1 .. L-1 (layer 0 where L == 1), as the decode step does: replaying ONE layer's weights
+// back to back would leave a ~272 MB gate/up working set largely in the 256 MiB Infinity
+// Cache and time a cache hit rate no decode step sees (round-1 verdict).  lm_head (which 4)
+// has one weight; its 1.09 GB stream cannot stay resident.
 int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* avg_us, double* bytes) {
-    QIE_REQUIRE(b && iters > 0 && avg_us && bytes, "qie_batch_time_kernel: bad arguments");
+    QIE_REQUIRE(b && iters > 0 && avg_us && bytes && which >= 0 && which <= 5, "qie_batch_time_kernel: bad arguments");
     qie_engine* e = b->e;
     const qie_model_spec& s = e->spec;
-    const qie_layer_weights& L = e->layers[0];
     const TpShard& sh = e->sh;   // this rank's shard sizes
     const int64_t H = s.hidden, hd = s.head_dim, QD = (int64_t)sh.nq * hd, KD = (int64_t)sh.nkv * hd;
     const int64_t I = sh.ffn, B = b->B, V = sh.vocab;
@@ -1294,64 +1327,72 @@ int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* av
     uint16_t* scratch = nullptr;
     QIE_TRY(dmalloc((void**)&scratch,
                     (size_t)B * std::max<int64_t>(std::max(I, V), QD + 2 * KD) * 2 + B * 8 + 64));
-    qie_linear_args a = lin_base(e);
-    double by = 0;
     const double wb = e->fp8 ? 1.0 : 2.0;   // weight bytes per element (fp8 row scales: negligible)
-    if (which == 0) {
-        a.x = b->x_res; a.ldx = H; a.w[0] = L.w_gate; a.w[1] = L.w_up; a.seg_rows[0] = I; a.seg_rows[1] = I;
-        a.M = B; a.K = H; a.N = I; a.y = scratch; a.ldy = I; a.epilogue = QIE_EPI_SWIGLU;
-        a.norm_w = L.ffn_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
-        by = 2.0 * I * H * wb + B * H * 2 + H * 2 + B * I * 2;
-    } else if (which == 1) {
-        a.x = b->h; a.ldx = I; a.w[0] = L.w_down; a.seg_rows[0] = H;
-        a.M = B; a.K = I; a.N = H; a.y = scratch; a.ldy = H; a.epilogue = QIE_EPI_STORE;
-        by = (double)H * I * wb + B * I * 2 + B * H * 2;
-    } else if (which == 2) {
-        a.x = b->x_res; a.ldx = H; a.w[0] = L.wq; a.w[1] = L.wk; a.w[2] = L.wv;
-        a.bias[0] = L.bq; a.bias[1] = L.bk; a.bias[2] = L.bv;
-        a.seg_rows[0] = QD; a.seg_rows[1] = KD; a.seg_rows[2] = KD;
-        a.M = B; a.K = H; a.N = QD + 2 * KD; a.y = scratch; a.ldy = QD + 2 * KD; a.epilogue = QIE_EPI_STORE;
-        a.norm_w = L.attn_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
-        by = (double)(QD + 2 * KD) * H * wb + B * H * 2 + B * (QD + 2 * KD) * 2;
-    } else if (which == 3) {
-        a.x = b->att; a.ldx = QD; a.w[0] = L.wo; a.seg_rows[0] = H;
-        a.M = B; a.K = QD; a.N = H; a.y = scratch; a.ldy = H; a.epilogue = QIE_EPI_STORE;
-        by = (double)H * QD * wb + B * QD * 2 + B * H * 2;
-    } else if (which == 4) {
-        a.x = b->x_res; a.ldx = H; a.w[0] = e->w.lm_head; a.seg_rows[0] = V;
-        a.M = B; a.K = H; a.N = V; a.y = scratch; a.ldy = V; a.epilogue = QIE_EPI_STORE;
-        a.norm_w = e->w.final_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
-        a.argmax_keys = (uint64_t*)(((uintptr_t)(scratch + B * V) + 7) & ~(uintptr_t)7);   // as the greedy step runs it
-        by = (double)V * H * wb + B * H * 2 + B * (double)V * 2;
-    } else if (which != 5) {
-        hipFree(scratch);
-        return fail(-22, "qie_batch_time_kernel: unknown kernel %d", which);
-    }
-    const qie_kv_cache cache = batch_cache(b, 0);
-    if (B >= 2 && a.norm_w && !(getenv("QIE_PRENORM") && atoi(getenv("QIE_PRENORM")) == 0)) {
-        a.x = b->xn;   // as the batched step runs it: rows normed once by prenorm(), plain GEMV
-        a.ldx = a.K;
-        a.norm_w = nullptr;
-    }
+    const bool batched_norm = B >= 2 && !(getenv("QIE_PRENORM") && atoi(getenv("QIE_PRENORM")) == 0);
+    auto args_for = [&](int l, double* by) {
+        const qie_layer_weights& L = e->layers[l];
+        qie_linear_args a = lin_base(e);
+        if (which == 0) {
+            a.x = b->x_res; a.ldx = H; a.w[0] = L.w_gate; a.w[1] = L.w_up; a.seg_rows[0] = I; a.seg_rows[1] = I;
+            a.M = B; a.K = H; a.N = I; a.y = scratch; a.ldy = I; a.epilogue = QIE_EPI_SWIGLU;
+            a.norm_w = L.ffn_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
+            *by = 2.0 * I * H * wb + B * H * 2 + H * 2 + B * I * 2;
+        } else if (which == 1) {
+            a.x = b->h; a.ldx = I; a.w[0] = L.w_down; a.seg_rows[0] = H;
+            a.M = B; a.K = I; a.N = H; a.y = scratch; a.ldy = H; a.epilogue = QIE_EPI_STORE;
+            *by = (double)H * I * wb + B * I * 2 + B * H * 2;
+        } else if (which == 2) {
+            a.x = b->x_res; a.ldx = H; a.w[0] = L.wq; a.w[1] = L.wk; a.w[2] = L.wv;
+            a.bias[0] = L.bq; a.bias[1] = L.bk; a.bias[2] = L.bv;
+            a.seg_rows[0] = QD; a.seg_rows[1] = KD; a.seg_rows[2] = KD;
+            a.M = B; a.K = H; a.N = QD + 2 * KD; a.y = scratch; a.ldy = QD + 2 * KD; a.epilogue = QIE_EPI_STORE;
+            a.norm_w = L.attn_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
+            *by = (double)(QD + 2 * KD) * H * wb + B * H * 2 + B * (QD + 2 * KD) * 2;
+        } else if (which == 3) {
+            a.x = b->att; a.ldx = QD; a.w[0] = L.wo; a.seg_rows[0] = H;
+            a.M = B; a.K = QD; a.N = H; a.y = scratch; a.ldy = H; a.epilogue = QIE_EPI_STORE;
+            *by = (double)H * QD * wb + B * QD * 2 + B * H * 2;
+        } else if (which == 4) {
+            a.x = b->x_res; a.ldx = H; a.w[0] = e->w.lm_head; a.seg_rows[0] = V;
+            a.M = B; a.K = H; a.N = V; a.y = scratch; a.ldy = V; a.epilogue = QIE_EPI_STORE;
+            a.norm_w = e->w.final_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
+            a.argmax_keys = (uint64_t*)(((uintptr_t)(scratch + B * V) + 7) & ~(uintptr_t)7);   // as the greedy step runs it
+            *by = (double)V * H * wb + B * H * 2 + B * (double)V * 2;
+        }
+        if (batched_norm && a.norm_w) {
+            a.x = b->xn;   // as the batched step runs it: rows normed once by prenorm(), plain GEMV
+            a.ldx = a.K;
+            a.norm_w = nullptr;
+        }
+        return a;
+    };
+    double by = 0;
     if (which == 5) {
         std::vector<int32_t> pos(B);
-        hipMemcpy(pos.data(), b->d_pos, B * 4, hipMemcpyDeviceToHost);
-        by = 0;
+        QIE_HIP(hipMemcpy(pos.data(), b->d_pos, B * 4, hipMemcpyDeviceToHost));
         for (int m = 0; m < B; m++) by += (double)(pos[m] + 1) * KD * 2 * 2;
         by += (double)B * QD * 2 * 2;
     }
+    const qie_kv_cache cache = batch_cache(b, 0);
+    const int nl = s.n_layers;
+    auto layer_of = [&](int i) { return which == 4 || nl == 1 ? 0 : 1 + i % (nl - 1); };
+    auto run = [&](int i) -> int {
+        const int l = layer_of(i);
+        const qie_layer_weights& L = e->layers[l];
+        if (which == 5)
+            return qie_attention_decode(b->qkv, B, b->d_pos, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, sh.nq,
+                                        &cache, l, s.rms_eps, s.numerics, scratch, b->dec_ws, e->stream);
+        double lb = 0;
+        qie_linear_args a = args_for(l, &lb);
+        return qie_linear(&a, e->stream);
+    };
+    if (which != 5) args_for(0, &by);
     hipEvent_t t0, t1;
     QIE_HIP(hipEventCreate(&t0));
     QIE_HIP(hipEventCreate(&t1));
-    auto run = [&]() -> int {
-        if (which == 5)
-            return qie_attention_decode(b->qkv, B, b->d_pos, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, sh.nq,
-                                        &cache, 0, s.rms_eps, s.numerics, scratch, b->dec_ws, e->stream);
-        return qie_linear(&a, e->stream);
-    };
-    QIE_TRY(run());   // warm-up
+    for (int i = 0; i < std::min(nl, 4); i++) QIE_TRY(run(i));   // warm-up
     QIE_HIP(hipEventRecord(t0, e->stream));
-    for (int i = 0; i < iters; i++) QIE_TRY(run());
+    for (int i = 0; i < iters; i++) QIE_TRY(run(i));
     QIE_HIP(hipEventRecord(t1, e->stream));
     QIE_HIP(hipEventSynchronize(t1));
     float ms = 0;

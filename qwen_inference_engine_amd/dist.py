@@ -1,23 +1,35 @@
-"""Minimal single-node process group for replica benchmarks (no torch in-process).
+"""Minimal single-node process group for the multi-rank benchmark (no torch in-process).
 
-torch.distributed.run launches one process per GPU and exports RANK / WORLD_SIZE /
-LOCAL_RANK / MASTER_PORT.  Replica ranks only need a barrier and a max/sum over a few
-floats, so they meet through files under /tmp keyed by MASTER_PORT (all ranks share
-one node).  Keeping torch out of the process avoids loading a second HIP runtime
-beside libqie's (the wheel bundles its own ROCm).
+One process per GPU, started by torch.distributed.run (RANK / WORLD_SIZE / LOCAL_RANK /
+MASTER_PORT exported) or by bench.py's own launcher (which also exports QIE_GROUP_DIR, a
+fresh directory).  Ranks only need a barrier, an all-gather of small JSON values (the RCCL
+unique id) and a max over floats, so they meet through files.  The directory is unique to
+the run: QIE_GROUP_DIR, else MASTER_PORT + the launcher's pid (all ranks of one
+torch.distributed.run share their parent, the elastic agent) — files of an earlier run on
+the same port can never satisfy a new barrier.  Rank 0 removes it at close().  Keeping
+torch out of the process avoids loading a second HIP runtime beside libqie's (the wheel
+bundles its own ROCm).
 """
 from __future__ import annotations
 
 import json
 import os
+import shutil
 import time
 
 
+def group_dir() -> str:
+    d = os.environ.get("QIE_GROUP_DIR")
+    if d:
+        return d
+    run = os.environ.get("TORCHELASTIC_RUN_ID", "x")
+    return os.path.join("/tmp", f"qie_group_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}_{run}")
+
+
 class FileGroup:
-    def __init__(self, rank: int, world: int, tag: str = None, timeout: float = 600.0):
+    def __init__(self, rank: int, world: int, path: str = None, timeout: float = 300.0):
         self.rank, self.world = rank, world
-        tag = tag or os.environ.get("MASTER_PORT", "0")
-        self.dir = os.path.join("/tmp", f"qie_group_{tag}_{os.environ.get('TORCHELASTIC_RUN_ID', 'x')}")
+        self.dir = path or group_dir()
         os.makedirs(self.dir, exist_ok=True)
         self.timeout = timeout
         self.gen = 0
@@ -38,13 +50,13 @@ class FileGroup:
                     p = os.path.join(self.dir, f"g{self.gen}_r{r}.json")
                     if os.path.exists(p):
                         with open(p) as f:
-                            vals[r] = json.load(f)
+                            vals[r] = [json.load(f)]
                     else:
                         done = False
             if done:
-                return vals
+                return [v[0] for v in vals]
             if time.time() - t0 > self.timeout:
-                raise TimeoutError(f"rank {self.rank}: group exchange {self.gen} timed out")
+                raise TimeoutError(f"rank {self.rank}: group exchange {self.gen} timed out in {self.dir}")
             time.sleep(0.0005)
 
     def barrier(self) -> None:
@@ -55,3 +67,10 @@ class FileGroup:
 
     def max(self, x: float) -> float:
         return max(self._exchange(float(x)))
+
+    def close(self) -> None:
+        """Final barrier, then rank 0 removes the rendezvous directory."""
+        self.barrier()
+        if self.rank == 0:
+            time.sleep(0.05)
+            shutil.rmtree(self.dir, ignore_errors=True)

@@ -131,3 +131,31 @@ def tiny(name: str = "tiny-qwen2", *, n_layers=2, hidden=128, n_heads=4, n_kv_he
     """Small test configurations (oracle finishes in well under a second)."""
     return ModelSpec(name, n_layers, hidden, n_heads, n_kv_heads, head_dim, ffn, vocab, tie, bias,
                      qk_norm, 1e-6, 1e6, numerics)
+
+
+def shard_heads(nq: int, nkv: int, tp: int, rank: int):
+    """(local q heads, first q head, local kv heads, first kv head) of `rank` — the rule of
+    engine.hip shard_heads: even split when tp divides the kv heads, else every kv head on
+    tp / nkv ranks that split its group's q heads (the first G % rep ranks one more);
+    None when the heads do not shard."""
+    if nkv % tp == 0 and nq % tp == 0:
+        return nq // tp, rank * (nq // tp), nkv // tp, rank * (nkv // tp)
+    if tp % nkv:
+        return None
+    rep, G = tp // nkv, nq // nkv
+    if rep > G:
+        return None
+    g, sub = rank // rep, rank % rep
+    base, extra = G // rep, G % rep
+    return base + (1 if sub < extra else 0), g * G + sub * base + min(sub, extra), 1, g
+
+
+def tp_shardable(spec: ModelSpec, tp: int):
+    """(ok, reason): can `spec` run tensor-parallel over `tp` ranks (qie_engine_create's check)?"""
+    if shard_heads(spec.n_heads, spec.n_kv_heads, tp, 0) is None:
+        return False, f"{spec.n_heads} q / {spec.n_kv_heads} kv heads do not shard {tp} ways"
+    if spec.ffn % tp or (spec.ffn // tp) % 8:
+        return False, f"ffn {spec.ffn} / {tp} is not a multiple of 8"
+    if spec.vocab % tp:
+        return False, f"vocab {spec.vocab} not divisible by {tp}"
+    return True, ""

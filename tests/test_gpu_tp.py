@@ -32,6 +32,12 @@ CONFIGS = {
                                   vocab=1536, bias=False, qk_norm=True), 2),
     "tied-tp4": (S.tiny("t-tied4", n_layers=2, hidden=256, n_heads=8, n_kv_heads=4, head_dim=64, ffn=512,
                         vocab=1024, tie=True, bias=True), 4),
+    # uneven q heads with kv replication: one kv head shared by 2 ranks (q heads 4 + 3)
+    "g7-kvrep-tp2": (S.tiny("t-g7tp", n_layers=2, hidden=448, n_heads=7, n_kv_heads=1, head_dim=64, ffn=640,
+                            vocab=1554, bias=True), 2),
+    # Qwen2-7B's head layout (28 q / 4 kv, head_dim 128) at TP 8: q heads 4,3,4,3,... one kv head each
+    "q28kv4-tp8": (S.tiny("t-q28tp8", n_layers=2, hidden=512, n_heads=28, n_kv_heads=4, head_dim=128, ffn=1024,
+                          vocab=2048, bias=True), 8),
 }
 
 

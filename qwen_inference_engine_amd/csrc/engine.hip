@@ -32,6 +32,13 @@ int attention_o_fused(const void* qkv, const int32_t* pos, const void* q_norm, c
                       int64_t H, unsigned* ctr, void* stream);
 int gemm(const qie_linear_args* a, hipStream_t st);
 }  // namespace qie
+#include "k_chain.hpp"
+namespace qie {
+int chain_launch(const ChainParams& p, hipStream_t st);
+int chain_ctr_words();
+int chain_err_word();
+}  // namespace qie
+
 
 using namespace qie;
 
@@ -108,6 +115,7 @@ struct qie_batch {
     uint16_t* h = nullptr;
     uint16_t* xn = nullptr;     // [B][H] RMS-normed rows feeding the batched (B >= 2) projections
     unsigned* fuse_ctr = nullptr;   // attention + O-proj fused launch counters (k_attention.hip kFuseCtrWords)
+    unsigned* chain_ctr = nullptr;  // persistent layer-chain hand-off counters (k_chain.hip), zero at rest
     uint16_t* logits = nullptr;
     void* attn_ws = nullptr;
     void* dec_ws = nullptr;     // fused decode attention: split partials + zeroed counters
@@ -406,15 +414,64 @@ static bool fuse_attn_o(const qie_batch* b) {
            e->spec.hidden % 2 == 0;
 }
 
-// a fused launch that gave up waiting (20 ms bound) leaves err set: report it, clear it
+// a fused / chain launch that gave up waiting (20 ms bound) leaves err set: report it, clear it
 static int check_fuse_err(qie_batch* b) {
-    unsigned err = 0;
+    unsigned err = 0, cerr = 0;
     QIE_HIP(hipMemcpy(&err, b->fuse_ctr + 32, 4, hipMemcpyDeviceToHost));
+    QIE_HIP(hipMemcpy(&cerr, b->chain_ctr + chain_err_word(), 4, hipMemcpyDeviceToHost));
     if (err) {
         QIE_HIP(hipMemset(b->fuse_ctr, 0, 1024));
         return fail(-5, "decode: fused attention/O-proj launch timed out waiting for attention");
     }
+    if (cerr) {
+        QIE_HIP(hipMemset(b->chain_ctr, 0, (size_t)chain_ctr_words() * 4));
+        return fail(-5, "decode: layer-chain launch timed out at a hand-off");
+    }
     return 0;
+}
+
+// The persistent layer chain (k_chain.hip) serves batch-1 bf16 single-GPU decode;
+// QIE_CHAIN=0 restores the per-op launches (A/B timing).
+static bool use_chain(const qie_batch* b) {
+    const qie_engine* e = b->e;
+    static const int on = getenv("QIE_CHAIN") ? atoi(getenv("QIE_CHAIN")) : 1;
+    const int64_t H = e->spec.hidden, QD = (int64_t)e->sh.nq * e->spec.head_dim, I = e->sh.ffn;
+    return on && b->B == 1 && e->sh.tp == 1 && !e->fp8 && H % 8 == 0 && QD % 8 == 0 && I % 8 == 0 &&
+           std::max(std::max(H, QD), I) * 2 <= 64 * 1024;
+}
+
+static int enqueue_chain(qie_batch* b, int l) {
+    qie_engine* e = b->e;
+    const qie_model_spec& s = e->spec;
+    const qie_layer_weights& L = e->layers[l];
+    ChainParams c{};
+    c.att = b->att;
+    c.wo = (const uint16_t*)L.wo;
+    c.x = b->x_res;
+    c.ffn_norm = (const uint16_t*)L.ffn_norm;
+    c.wg = (const uint16_t*)L.w_gate;
+    c.wu = (const uint16_t*)L.w_up;
+    c.h = b->h;
+    c.wd = (const uint16_t*)L.w_down;
+    if (l + 1 < s.n_layers) {
+        const qie_layer_weights& N = e->layers[l + 1];
+        c.attn_norm = (const uint16_t*)N.attn_norm;
+        c.wq = (const uint16_t*)N.wq;
+        c.wk = (const uint16_t*)N.wk;
+        c.wv = (const uint16_t*)N.wv;
+        c.bq = (const uint16_t*)N.bq;
+        c.bk = (const uint16_t*)N.bk;
+        c.bv = (const uint16_t*)N.bv;
+        c.qkv = b->qkv;
+    }
+    c.H = s.hidden;
+    c.QD = (int64_t)e->sh.nq * s.head_dim;
+    c.KD = (int64_t)e->sh.nkv * s.head_dim;
+    c.I = e->sh.ffn;
+    c.eps = s.rms_eps;
+    c.numerics = s.numerics;
+    c.ctr = b->chain_ctr;
+    return chain_launch(c, e->stream);
 }
 
 static int enqueue_layer_decode(qie_batch* b, int l) {
@@ -425,8 +482,14 @@ static int enqueue_layer_decode(qie_batch* b, int l) {
     const int64_t H = s.hidden, hd = s.head_dim, QD = (int64_t)e->sh.nq * hd, KD = (int64_t)e->sh.nkv * hd;
     const int64_t QKVD = QD + 2 * KD, I = e->sh.ffn, B = b->B;
     const qie_kv_cache cache = batch_cache(b, 0);
+    const bool chain = use_chain(b);
 
     qie_linear_args a = lin_base(e);
+    if (chain && l > 0) {   // this layer's QKV was the previous chain launch's last phase
+        QIE_TRY(qie_attention_decode(b->qkv, B, b->d_pos, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, e->sh.nq,
+                                     &cache, l, s.rms_eps, s.numerics, b->att, b->dec_ws, st));
+        return enqueue_chain(b, l);
+    }
     a.x = b->x_res; a.ldx = H;
     a.w[0] = L.wq; a.w[1] = L.wk; a.w[2] = L.wv;
     a.bias[0] = L.bq; a.bias[1] = L.bk; a.bias[2] = L.bv;
@@ -438,6 +501,11 @@ static int enqueue_layer_decode(qie_batch* b, int l) {
     QIE_TRY(prenorm(b, a, B));
     QIE_TRY(gemv(&a, st));
 
+    if (chain) {   // layer 0: plain QKV above, then attention + the chain (O, MLP, layer 1's QKV)
+        QIE_TRY(qie_attention_decode(b->qkv, B, b->d_pos, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, e->sh.nq,
+                                     &cache, l, s.rms_eps, s.numerics, b->att, b->dec_ws, st));
+        return enqueue_chain(b, l);
+    }
     if (fuse_attn_o(b)) {
         // attention + O-proj + residual in one launch (batch 1, bf16, single GPU)
         QIE_TRY(attention_o_fused(b->qkv, b->d_pos, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, e->sh.nq, &cache, l,
@@ -974,6 +1042,7 @@ static int batch_create(qie_engine* e, int32_t batch, int32_t max_ctx, int32_t p
     A((void**)&b->h, batch * (int64_t)sh.ffn * 2);
     A((void**)&b->xn, batch * H * 2);
     A((void**)&b->fuse_ctr, 1024);
+    A((void**)&b->chain_ctr, (size_t)chain_ctr_words() * 4);
     A((void**)&b->logits, batch * (int64_t)sh.vocab * 2);
     A(&b->attn_ws, (size_t)qie_attention_workspace_bytes(batch, sh.nq, s.head_dim, max_ctx));
     A(&b->samp_ws, (size_t)qie_sample_workspace_bytes(batch, s.vocab));
@@ -987,6 +1056,7 @@ static int batch_create(qie_engine* e, int32_t batch, int32_t max_ctx, int32_t p
     if (!rc) {
         hipMemsetAsync(b->dec_ws, 0, (size_t)dec_ws, e->stream);
         hipMemsetAsync(b->fuse_ctr, 0, 1024, e->stream);
+        hipMemsetAsync(b->chain_ctr, 0, (size_t)chain_ctr_words() * 4, e->stream);
         hipMemsetAsync(b->kc, 0, (size_t)n_runs * b->seq_stride * 2, e->stream);
         hipMemsetAsync(b->vc, 0, (size_t)n_runs * b->seq_stride * 2, e->stream);
         hipMemsetAsync(b->d_keys, 0, batch * 8, e->stream);
@@ -1064,7 +1134,7 @@ void qie_batch_destroy(qie_batch* b) {
     void* ps[] = {b->kc, b->vc, b->d_table, b->d_pos, b->d_step, b->d_hist, b->d_ids, b->d_keys, b->x_res, b->qkv, b->q,
                   b->att, b->h, b->logits, b->attn_ws, b->dec_ws, b->samp_ws, b->pf_x, b->pf_hn, b->pf_qkv, b->pf_q,
                   b->pf_att, b->pf_h, b->pf_pos, b->pf_ids, b->pf_attn_ws, b->part, b->logits_full,
-                  b->gather_tmp, b->pf_part, b->xn, b->fuse_ctr};
+                  b->gather_tmp, b->pf_part, b->xn, b->fuse_ctr, b->chain_ctr};
     for (void* p : ps)
         if (p) hipFree(p);
     delete b;

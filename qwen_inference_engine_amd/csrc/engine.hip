@@ -440,7 +440,7 @@ static bool use_chain(const qie_batch* b) {
            std::max(std::max(H, QD), I) * 2 <= 64 * 1024;
 }
 
-static int enqueue_chain(qie_batch* b, int l) {
+static int enqueue_chain(qie_batch* b, int l, unsigned long long* dbg = nullptr) {
     qie_engine* e = b->e;
     const qie_model_spec& s = e->spec;
     const qie_layer_weights& L = e->layers[l];
@@ -471,6 +471,7 @@ static int enqueue_chain(qie_batch* b, int l) {
     c.eps = s.rms_eps;
     c.numerics = s.numerics;
     c.ctr = b->chain_ctr;
+    c.dbg = dbg;
     return chain_launch(c, e->stream);
 }
 
@@ -1387,7 +1388,58 @@ int qie_engine_rope_tables(const qie_engine* e, const float** rope_cos, const fl
 // Cache and time a cache hit rate no decode step sees (round-1 verdict).  lm_head (which 4)
 // has one weight; its 1.09 GB stream cannot stay resident.
 int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* avg_us, double* bytes) {
-    QIE_REQUIRE(b && iters > 0 && avg_us && bytes && which >= 0 && which <= 5, "qie_batch_time_kernel: bad arguments");
+    QIE_REQUIRE(b && iters > 0 && avg_us && bytes && which >= 0 && which <= 6, "qie_batch_time_kernel: bad arguments");
+    if (which == 6) {   // the layer chain (O, gate/up, down, next QKV), layers 1 .. L-2
+        QIE_REQUIRE(use_chain(b) && b->e->spec.n_layers >= 3, "qie_batch_time_kernel: no layer chain for this batch");
+        const qie_engine* e = b->e;
+        const int64_t H = e->spec.hidden, QD = (int64_t)e->sh.nq * e->spec.head_dim;
+        const int64_t KD = (int64_t)e->sh.nkv * e->spec.head_dim, I = e->sh.ffn;
+        const int nl = e->spec.n_layers, cus = device_cu_count();
+        unsigned long long* dbg = nullptr;
+        const bool stamps = getenv("QIE_CHAIN_DBG") != nullptr;
+        if (stamps) QIE_TRY(dmalloc((void**)&dbg, (size_t)cus * 16 * 8));
+        hipEvent_t t0, t1;
+        QIE_HIP(hipEventCreate(&t0));
+        QIE_HIP(hipEventCreate(&t1));
+        QIE_TRY(enqueue_chain(b, 1));
+        QIE_HIP(hipEventRecord(t0, e->stream));
+        for (int i = 0; i < iters; i++) QIE_TRY(enqueue_chain(b, 1 + i % (nl - 2), i == iters - 1 ? dbg : nullptr));
+        QIE_HIP(hipEventRecord(t1, e->stream));
+        QIE_HIP(hipEventSynchronize(t1));
+        float ms = 0;
+        QIE_HIP(hipEventElapsedTime(&ms, t0, t1));
+        hipEventDestroy(t0);
+        hipEventDestroy(t1);
+        if (stamps) {   // per-phase wall time, averaged over workgroups, to stderr
+            std::vector<unsigned long long> h((size_t)cus * 16);
+            QIE_HIP(hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost));
+            double acc[8] = {0}, mx[8] = {0};
+            for (int w = 0; w < cus; w++)
+                for (int i = 1; i < 8; i++) {
+                    const double d = (double)(h[(size_t)w * 16 + i] - h[(size_t)w * 16]) * 0.01;   // 100 MHz -> us
+                    acc[i] += d / cus;
+                    mx[i] = std::max(mx[i], d);
+                }
+            fprintf(stderr, "chain stamps (us from workgroup start, mean / max): O-done %.2f/%.2f  G-go %.2f/%.2f  "
+                    "G-done %.2f/%.2f  D-go %.2f/%.2f  D-done %.2f/%.2f  Q-go %.2f/%.2f  end %.2f/%.2f\n",
+                    acc[1], mx[1], acc[2], mx[2], acc[3], mx[3], acc[4], mx[4], acc[5], mx[5], acc[6], mx[6], acc[7],
+                    mx[7]);
+            double gx[8] = {0}, gm[8] = {0};   // G-done by blockIdx % 8 (the XCD of round-robin dispatch)
+            for (int w = 0; w < cus; w++) {
+                const double d = (double)(h[(size_t)w * 16 + 3] - h[(size_t)w * 16]) * 0.01;
+                gx[w % 8] += d * 8.0 / cus;
+                gm[w % 8] = std::max(gm[w % 8], d);
+            }
+            fprintf(stderr, "chain G-done by blockIdx%%8 (mean/max):");
+            for (int x = 0; x < 8; x++) fprintf(stderr, " %.1f/%.1f", gx[x], gm[x]);
+            fprintf(stderr, "\n");
+            hipFree(dbg);
+        }
+        QIE_TRY(check_fuse_err(b));
+        *avg_us = ms * 1000.0 / iters;
+        *bytes = (double)(H * QD + 2 * I * H + H * I + (QD + 2 * KD) * H) * 2.0;
+        return 0;
+    }
     qie_engine* e = b->e;
     const qie_model_spec& s = e->spec;
     const TpShard& sh = e->sh;   // this rank's shard sizes

@@ -59,11 +59,13 @@ __device__ __forceinline__ uint4 ld_sc1_16(const uint16_t* p) {
     return make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
 }
 
-// this workgroup's pair range of a phase with P pairs
-__device__ __forceinline__ void chain_range(int64_t P, int64_t& p0, int64_t& p1) {
-    p0 = P * blockIdx.x / gridDim.x;
-    p1 = P * (blockIdx.x + 1) / gridDim.x;
-}
+// Pair tasks are dealt round-robin over every wave of the grid (pair p to workgroup
+// p % G, wave (p / G) % 8): the 2048 waves stream 2048 neighbouring row pairs at any
+// moment, spread over all HBM channels.  (Contiguous per-CU slices, every CU at the same
+// offset of its own slice, ran the gate/up phase 10 % slower with a 5 us spread across
+// XCDs.)
+__device__ __forceinline__ int64_t chain_first(int wave) { return blockIdx.x + (int64_t)gridDim.x * wave; }
+__device__ __forceinline__ int64_t chain_step() { return (int64_t)gridDim.x * 8; }
 
 // seam: publish (after this workgroup's last store of the phase) / wait for all
 __device__ __forceinline__ void chain_signal(unsigned* ctr, int phase) {
@@ -73,8 +75,12 @@ __device__ __forceinline__ void chain_signal(unsigned* ctr, int phase) {
         __hip_atomic_fetch_add(&ctr[(phase * 8 + threadIdx.x) * kChainCtrStride], 1u, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
 }
+// The poll runs on the LAST wave, which issues no prefetch loads: vmcnt retires a wave's
+// loads in order, so a poll from a wave with 16 KB of weights in flight returns only after
+// they do (measured: ~5 us seams with the poll on wave 0).
+constexpr int kChainPoller = 0;
 __device__ __forceinline__ void chain_wait(unsigned* ctr, int phase) {
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 64 * kChainPoller) {
         const unsigned* rep = &ctr[(phase * 8 + (blockIdx.x & 7)) * kChainCtrStride];
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         while (__hip_atomic_load(rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x) {
@@ -139,9 +145,10 @@ __device__ __forceinline__ void chain_fma(const uint16_t* xs, int64_t K, int64_t
 // rows; done(task, acc[R]) runs on every lane with the wave-reduced sums.
 template <int R, int U, class Make, class Done>
 __device__ __forceinline__ void chain_phase(const uint16_t* xs, int64_t K, int64_t t0, int64_t t1, int64_t tstep,
-                                            cu32x4 (&wv)[U][R], Make make, Done done) {
+                                            cu32x4 (&wv)[U][R], Make make, Done done, bool prefetched = true) {
     RowTask<R> t;
     if (t0 < t1) make(t0, t);
+    if (!prefetched && t0 < t1) chain_load<R, U>(t, K, 0, wv);
     for (int64_t task = t0; task < t1; task += tstep) {
         float acc[R];
 #pragma unroll
@@ -214,23 +221,26 @@ __global__ __launch_bounds__(512) void chain_kernel(ChainParams p) {
     const int64_t H = p.H, QD = p.QD, I = p.I;
     cu32x4 wv2[kChainU2][2];
     cu32x4 wv4[kChainU4][4];
+    auto stamp = [&](int i) {   // phase timing (tools/ubench.py UB_SET=chain): wall clock per workgroup
+        if (p.dbg && tid == 0) p.dbg[blockIdx.x * 16 + i] = __builtin_amdgcn_s_memrealtime();
+    };
+    stamp(0);
 
     // ================= phase O: x += W_o . att   (pairs of x rows)
-    int64_t o0, o1;
-    chain_range(H / 2, o0, o1);
+    const int64_t o0 = chain_first(wave), o1 = H / 2, ts = chain_step();
     auto make_o = [&](int64_t pr, RowTask<2>& t) {
         t.wr[0] = reinterpret_cast<const cu32x4*>(p.wo + (2 * pr) * QD);
         t.wr[1] = reinterpret_cast<const cu32x4*>(p.wo + (2 * pr + 1) * QD);
     };
     {
         RowTask<2> t;
-        make_o(o0 + wave < o1 ? o0 + wave : o0, t);
+        make_o(o0 < o1 ? o0 : 0, t);
         chain_load<2, kChainU2>(t, QD, 0, wv2);
     }
     for (int64_t k = (int64_t)tid * 8; k < QD; k += 512 * 8)   // previous launch's output: plain loads
         *reinterpret_cast<uint4*>(xs + k) = *reinterpret_cast<const uint4*>(p.att + k);
     __syncthreads();
-    chain_phase<2, kChainU2>(xs, QD, o0 + wave, o1, kChainWaves, wv2, make_o, [&](int64_t pr, float (&acc)[2]) {
+    chain_phase<2, kChainU2>(xs, QD, o0, o1, ts, wv2, make_o, [&](int64_t pr, float (&acc)[2]) {
         if (lane == 0) {
             uint32_t* xp = reinterpret_cast<uint32_t*>(p.x) + pr;
             const uint32_t old = ld_sc1(xp);
@@ -239,23 +249,25 @@ __global__ __launch_bounds__(512) void chain_kernel(ChainParams p) {
     });
 
     // ================= phase G: h = swiglu(W_gate . n, W_up . n), n = rms(x) * w_ffn
-    int64_t g0, g1;
-    chain_range(I / 2, g0, g1);
+    const int64_t g0 = chain_first(wave), g1 = I / 2;
     auto make_g = [&](int64_t pr, RowTask<4>& t) {
         t.wr[0] = reinterpret_cast<const cu32x4*>(p.wg + (2 * pr) * H);
         t.wr[1] = reinterpret_cast<const cu32x4*>(p.wg + (2 * pr + 1) * H);
         t.wr[2] = reinterpret_cast<const cu32x4*>(p.wu + (2 * pr) * H);
         t.wr[3] = reinterpret_cast<const cu32x4*>(p.wu + (2 * pr + 1) * H);
     };
+    stamp(1);
     chain_signal(p.ctr, 0);   // drains this phase's stores first: vmcnt counts loads too
     {
         RowTask<4> t;
-        make_g(g0 + wave < g1 ? g0 + wave : g0, t);
-        chain_load<4, kChainU4>(t, H, 0, wv4);
+        make_g(g0 < g1 ? g0 : 0, t);
+        if (true) chain_load<4, kChainU4>(t, H, 0, wv4);
     }
     chain_wait(p.ctr, 0);
+    stamp(2);
     chain_norm_x(p, p.ffn_norm, xs, red);
-    chain_phase<4, kChainU4>(xs, H, g0 + wave, g1, kChainWaves, wv4, make_g, [&](int64_t pr, float (&acc)[4]) {
+    const bool pf = true;
+    chain_phase<4, kChainU4>(xs, H, g0, g1, ts, wv4, make_g, [&](int64_t pr, float (&acc)[4]) {
         if (lane == 0) {
             float o[2];
 #pragma unroll
@@ -267,36 +279,37 @@ __global__ __launch_bounds__(512) void chain_kernel(ChainParams p) {
             }
             st_sc1(reinterpret_cast<uint32_t*>(p.h) + pr, pack2(o[0], o[1]));
         }
-    });
+    }, pf);
 
     // ================= phase D: x += W_down . h
     auto make_d = [&](int64_t pr, RowTask<2>& t) {
         t.wr[0] = reinterpret_cast<const cu32x4*>(p.wd + (2 * pr) * I);
         t.wr[1] = reinterpret_cast<const cu32x4*>(p.wd + (2 * pr + 1) * I);
     };
+    stamp(3);
     chain_signal(p.ctr, 1);
     {
         RowTask<2> t;
-        make_d(o0 + wave < o1 ? o0 + wave : o0, t);
-        chain_load<2, kChainU2>(t, I, 0, wv2);
+        make_d(o0 < o1 ? o0 : 0, t);
+        if (true) chain_load<2, kChainU2>(t, I, 0, wv2);
     }
     chain_wait(p.ctr, 1);
+    stamp(4);
     for (int64_t k = (int64_t)tid * 8; k < I; k += 512 * 8)
         *reinterpret_cast<uint4*>(xs + k) = ld_sc1_16(p.h + k);
     __syncthreads();
-    chain_phase<2, kChainU2>(xs, I, o0 + wave, o1, kChainWaves, wv2, make_d, [&](int64_t pr, float (&acc)[2]) {
+    chain_phase<2, kChainU2>(xs, I, o0, o1, ts, wv2, make_d, [&](int64_t pr, float (&acc)[2]) {
         if (lane == 0) {
             uint32_t* xp = reinterpret_cast<uint32_t*>(p.x) + pr;
             const uint32_t old = ld_sc1(xp);
             st_sc1(xp, pack2(bf_lo(old) + rbf(acc[0]), bf_hi(old) + rbf(acc[1])));
         }
-    });
+    }, pf);
 
     // ================= phase Q (next layer): qkv = W_qkv . (rms(x) * w_attn) + b
     if (p.attn_norm) {
         const int64_t N = QD + 2 * p.KD;
-        int64_t q0, q1;
-        chain_range(N / 2, q0, q1);
+        const int64_t q0 = chain_first(wave), q1 = N / 2;
         auto make_q = [&](int64_t pr, RowTask<2>& t) {
 #pragma unroll
             for (int i = 0; i < 2; i++) {
@@ -306,15 +319,17 @@ __global__ __launch_bounds__(512) void chain_kernel(ChainParams p) {
                 t.wr[i] = reinterpret_cast<const cu32x4*>(w);
             }
         };
+        stamp(5);
         chain_signal(p.ctr, 2);
         {
             RowTask<2> t;
-            make_q(q0 + wave < q1 ? q0 + wave : q0, t);
-            chain_load<2, kChainU2>(t, H, 0, wv2);
+            make_q(q0 < q1 ? q0 : 0, t);
+            if (true) chain_load<2, kChainU2>(t, H, 0, wv2);
         }
         chain_wait(p.ctr, 2);
+        stamp(6);
         chain_norm_x(p, p.attn_norm, xs, red);
-        chain_phase<2, kChainU2>(xs, H, q0 + wave, q1, kChainWaves, wv2, make_q, [&](int64_t pr, float (&acc)[2]) {
+        chain_phase<2, kChainU2>(xs, H, q0, q1, ts, wv2, make_q, [&](int64_t pr, float (&acc)[2]) {
             if (lane == 0) {
                 float o[2];
 #pragma unroll
@@ -326,11 +341,12 @@ __global__ __launch_bounds__(512) void chain_kernel(ChainParams p) {
                 }
                 reinterpret_cast<uint32_t*>(p.qkv)[pr] = pack2(o[0], o[1]);   // next consumer: a new launch
             }
-        });
+        }, pf);
     }
 
     // ================= the last workgroup to finish zeroes the counters
     __syncthreads();
+    stamp(7);
     if (tid == 0) {
         const unsigned f = __hip_atomic_fetch_add(&p.ctr[kChainFin], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (f == gridDim.x - 1) {

@@ -26,6 +26,7 @@ struct ChainParams {
     float eps;
     int numerics;
     unsigned* ctr;                       // kChainCtrWords, zero at rest
+    unsigned long long* dbg;             // timing stamps [grid][16] (tools only; nullptr normally)
 };
 
 

@@ -157,9 +157,10 @@ int qie_engine_arena(const qie_engine* e, void** base, int64_t* bytes);
 int qie_engine_rope_tables(const qie_engine* e, const float** rope_cos, const float** rope_sin,
                            int32_t* rows);
 /* Time `iters` launches of one of the decode step's kernels with hipEvents on
- * the engine stream (which: 0 = gate/up GEMV of layer 0, 1 = down GEMV,
- * 2 = QKV GEMV, 3 = O GEMV, 4 = lm_head GEMV, 5 = attention).  Returns the
- * average microseconds per launch and the algorithmic bytes per launch. */
+ * the engine stream (which: 0 = gate/up GEMV, 1 = down GEMV, 2 = QKV GEMV,
+ * 3 = O GEMV, 4 = lm_head GEMV, 5 = attention; the layer GEMVs cycle through
+ * layers 1..L-1 so no weight stays cache-resident).  Returns the average
+ * microseconds per launch and the algorithmic bytes per launch. */
 int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* avg_us,
                           double* bytes);
 

@@ -26,17 +26,7 @@
 
 namespace qie {
 int gemv(const qie_linear_args* a, hipStream_t st);
-int attention_o_fused(const void* qkv, const int32_t* pos, const void* q_norm, const void* k_norm,
-                      const float* rope_cos, const float* rope_sin, int32_t n_heads, const qie_kv_cache* cache,
-                      int32_t layer, float eps, int32_t numerics, void* att_out, void* ws, const void* wo, void* x,
-                      int64_t H, unsigned* ctr, void* stream);
 int gemm(const qie_linear_args* a, hipStream_t st);
-}  // namespace qie
-#include "k_chain.hpp"
-namespace qie {
-int chain_launch(const ChainParams& p, hipStream_t st);
-int chain_ctr_words();
-int chain_err_word();
 }  // namespace qie
 
 
@@ -114,8 +104,6 @@ struct qie_batch {
     uint16_t* att = nullptr;
     uint16_t* h = nullptr;
     uint16_t* xn = nullptr;     // [B][H] RMS-normed rows feeding the batched (B >= 2) projections
-    unsigned* fuse_ctr = nullptr;   // attention + O-proj fused launch counters (k_attention.hip kFuseCtrWords)
-    unsigned* chain_ctr = nullptr;  // persistent layer-chain hand-off counters (k_chain.hip), zero at rest
     uint16_t* logits = nullptr;
     void* attn_ws = nullptr;
     void* dec_ws = nullptr;     // fused decode attention: split partials + zeroed counters
@@ -402,79 +390,6 @@ static int prenorm(qie_batch* b, qie_linear_args& a, int64_t M) {
     return 0;
 }
 
-// One launch for decode attention + O-proj (attn_o_fused_kernel), opt-in with QIE_FUSE_AO=1
-// where it applies (batch 1, bf16 weights, one GPU, nq * head_dim <= 4096).  Measured on
-// Qwen2-7B: 337 vs 351 tok/s for two launches — the in-launch hand-off costs more than the
-// boundary it removes (rejected experiments), so two launches stay the default.
-static bool fuse_attn_o(const qie_batch* b) {
-    const qie_engine* e = b->e;
-    const char* ev = getenv("QIE_FUSE_AO");
-    if (!ev || atoi(ev) == 0) return false;
-    return b->B == 1 && e->sh.tp == 1 && !e->fp8 && !b->d_table && (int64_t)e->sh.nq * e->spec.head_dim <= 4096 &&
-           e->spec.hidden % 2 == 0;
-}
-
-// a fused / chain launch that gave up waiting (20 ms bound) leaves err set: report it, clear it
-static int check_fuse_err(qie_batch* b) {
-    unsigned err = 0, cerr = 0;
-    QIE_HIP(hipMemcpy(&err, b->fuse_ctr + 32, 4, hipMemcpyDeviceToHost));
-    QIE_HIP(hipMemcpy(&cerr, b->chain_ctr + chain_err_word(), 4, hipMemcpyDeviceToHost));
-    if (err) {
-        QIE_HIP(hipMemset(b->fuse_ctr, 0, 1024));
-        return fail(-5, "decode: fused attention/O-proj launch timed out waiting for attention");
-    }
-    if (cerr) {
-        QIE_HIP(hipMemset(b->chain_ctr, 0, (size_t)chain_ctr_words() * 4));
-        return fail(-5, "decode: layer-chain launch timed out at a hand-off");
-    }
-    return 0;
-}
-
-// The persistent layer chain (k_chain.hip) serves batch-1 bf16 single-GPU decode;
-// QIE_CHAIN=0 restores the per-op launches (A/B timing).
-static bool use_chain(const qie_batch* b) {
-    const qie_engine* e = b->e;
-    static const int on = getenv("QIE_CHAIN") ? atoi(getenv("QIE_CHAIN")) : 1;
-    const int64_t H = e->spec.hidden, QD = (int64_t)e->sh.nq * e->spec.head_dim, I = e->sh.ffn;
-    return on && b->B == 1 && e->sh.tp == 1 && !e->fp8 && H % 8 == 0 && QD % 8 == 0 && I % 8 == 0 &&
-           std::max(std::max(H, QD), I) * 2 <= 64 * 1024;
-}
-
-static int enqueue_chain(qie_batch* b, int l, unsigned long long* dbg = nullptr) {
-    qie_engine* e = b->e;
-    const qie_model_spec& s = e->spec;
-    const qie_layer_weights& L = e->layers[l];
-    ChainParams c{};
-    c.att = b->att;
-    c.wo = (const uint16_t*)L.wo;
-    c.x = b->x_res;
-    c.ffn_norm = (const uint16_t*)L.ffn_norm;
-    c.wg = (const uint16_t*)L.w_gate;
-    c.wu = (const uint16_t*)L.w_up;
-    c.h = b->h;
-    c.wd = (const uint16_t*)L.w_down;
-    if (l + 1 < s.n_layers) {
-        const qie_layer_weights& N = e->layers[l + 1];
-        c.attn_norm = (const uint16_t*)N.attn_norm;
-        c.wq = (const uint16_t*)N.wq;
-        c.wk = (const uint16_t*)N.wk;
-        c.wv = (const uint16_t*)N.wv;
-        c.bq = (const uint16_t*)N.bq;
-        c.bk = (const uint16_t*)N.bk;
-        c.bv = (const uint16_t*)N.bv;
-        c.qkv = b->qkv;
-    }
-    c.H = s.hidden;
-    c.QD = (int64_t)e->sh.nq * s.head_dim;
-    c.KD = (int64_t)e->sh.nkv * s.head_dim;
-    c.I = e->sh.ffn;
-    c.eps = s.rms_eps;
-    c.numerics = s.numerics;
-    c.ctr = b->chain_ctr;
-    c.dbg = dbg;
-    return chain_launch(c, e->stream);
-}
-
 static int enqueue_layer_decode(qie_batch* b, int l) {
     qie_engine* e = b->e;
     const qie_model_spec& s = e->spec;
@@ -483,14 +398,8 @@ static int enqueue_layer_decode(qie_batch* b, int l) {
     const int64_t H = s.hidden, hd = s.head_dim, QD = (int64_t)e->sh.nq * hd, KD = (int64_t)e->sh.nkv * hd;
     const int64_t QKVD = QD + 2 * KD, I = e->sh.ffn, B = b->B;
     const qie_kv_cache cache = batch_cache(b, 0);
-    const bool chain = use_chain(b);
 
     qie_linear_args a = lin_base(e);
-    if (chain && l > 0) {   // this layer's QKV was the previous chain launch's last phase
-        QIE_TRY(qie_attention_decode(b->qkv, B, b->d_pos, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, e->sh.nq,
-                                     &cache, l, s.rms_eps, s.numerics, b->att, b->dec_ws, st));
-        return enqueue_chain(b, l);
-    }
     a.x = b->x_res; a.ldx = H;
     a.w[0] = L.wq; a.w[1] = L.wk; a.w[2] = L.wv;
     a.bias[0] = L.bq; a.bias[1] = L.bk; a.bias[2] = L.bv;
@@ -502,25 +411,14 @@ static int enqueue_layer_decode(qie_batch* b, int l) {
     QIE_TRY(prenorm(b, a, B));
     QIE_TRY(gemv(&a, st));
 
-    if (chain) {   // layer 0: plain QKV above, then attention + the chain (O, MLP, layer 1's QKV)
-        QIE_TRY(qie_attention_decode(b->qkv, B, b->d_pos, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, e->sh.nq,
-                                     &cache, l, s.rms_eps, s.numerics, b->att, b->dec_ws, st));
-        return enqueue_chain(b, l);
-    }
-    if (fuse_attn_o(b)) {
-        // attention + O-proj + residual in one launch (batch 1, bf16, single GPU)
-        QIE_TRY(attention_o_fused(b->qkv, b->d_pos, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, e->sh.nq, &cache, l,
-                                  s.rms_eps, s.numerics, b->att, b->dec_ws, L.wo, b->x_res, H, b->fuse_ctr, st));
-    } else {
-        QIE_TRY(qie_attention_decode(b->qkv, B, b->d_pos, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, e->sh.nq,
-                                     &cache, l, s.rms_eps, s.numerics, b->att, b->dec_ws, st));
-        a = lin_base(e);
-        a.x = b->att; a.ldx = QD;
-        a.w[0] = L.wo; a.seg_rows[0] = H;
-        a.M = B; a.K = QD; a.N = H;
-        a.ldy = H;
-        QIE_TRY(row_parallel(b, a, b->x_res, b->part, B));
-    }
+    QIE_TRY(qie_attention_decode(b->qkv, B, b->d_pos, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, e->sh.nq,
+                                 &cache, l, s.rms_eps, s.numerics, b->att, b->dec_ws, st));
+    a = lin_base(e);
+    a.x = b->att; a.ldx = QD;
+    a.w[0] = L.wo; a.seg_rows[0] = H;
+    a.M = B; a.K = QD; a.N = H;
+    a.ldy = H;
+    QIE_TRY(row_parallel(b, a, b->x_res, b->part, B));
 
     a = lin_base(e);
     a.x = b->x_res; a.ldx = H;
@@ -653,7 +551,7 @@ static int sync_ids(qie_batch* b, int32_t* next_ids) {
     if (!next_ids) return 0;
     QIE_HIP(hipMemcpyAsync(next_ids, b->d_ids, b->B * 4, hipMemcpyDeviceToHost, b->e->stream));
     QIE_HIP(hipStreamSynchronize(b->e->stream));
-    return check_fuse_err(b);
+    return 0;
 }
 
 }  // namespace qie
@@ -1042,8 +940,6 @@ static int batch_create(qie_engine* e, int32_t batch, int32_t max_ctx, int32_t p
     A((void**)&b->att, batch * QD * 2);
     A((void**)&b->h, batch * (int64_t)sh.ffn * 2);
     A((void**)&b->xn, batch * H * 2);
-    A((void**)&b->fuse_ctr, 1024);
-    A((void**)&b->chain_ctr, (size_t)chain_ctr_words() * 4);
     A((void**)&b->logits, batch * (int64_t)sh.vocab * 2);
     A(&b->attn_ws, (size_t)qie_attention_workspace_bytes(batch, sh.nq, s.head_dim, max_ctx));
     A(&b->samp_ws, (size_t)qie_sample_workspace_bytes(batch, s.vocab));
@@ -1056,8 +952,6 @@ static int batch_create(qie_engine* e, int32_t batch, int32_t max_ctx, int32_t p
     }
     if (!rc) {
         hipMemsetAsync(b->dec_ws, 0, (size_t)dec_ws, e->stream);
-        hipMemsetAsync(b->fuse_ctr, 0, 1024, e->stream);
-        hipMemsetAsync(b->chain_ctr, 0, (size_t)chain_ctr_words() * 4, e->stream);
         hipMemsetAsync(b->kc, 0, (size_t)n_runs * b->seq_stride * 2, e->stream);
         hipMemsetAsync(b->vc, 0, (size_t)n_runs * b->seq_stride * 2, e->stream);
         hipMemsetAsync(b->d_keys, 0, batch * 8, e->stream);
@@ -1135,7 +1029,7 @@ void qie_batch_destroy(qie_batch* b) {
     void* ps[] = {b->kc, b->vc, b->d_table, b->d_pos, b->d_step, b->d_hist, b->d_ids, b->d_keys, b->x_res, b->qkv, b->q,
                   b->att, b->h, b->logits, b->attn_ws, b->dec_ws, b->samp_ws, b->pf_x, b->pf_hn, b->pf_qkv, b->pf_q,
                   b->pf_att, b->pf_h, b->pf_pos, b->pf_ids, b->pf_attn_ws, b->part, b->logits_full,
-                  b->gather_tmp, b->pf_part, b->xn, b->fuse_ctr, b->chain_ctr};
+                  b->gather_tmp, b->pf_part, b->xn};
     for (void* p : ps)
         if (p) hipFree(p);
     delete b;
@@ -1289,7 +1183,6 @@ int qie_decode(qie_batch* b, int32_t n_steps, const qie_sampling* smp, int32_t* 
         for (int m = 0; m < b->B; m++) b->h_pos[m] += 1;
     }
     QIE_HIP(hipStreamSynchronize(b->e->stream));
-    QIE_TRY(check_fuse_err(b));
     if (out_ids && n_steps > 0) {
         std::vector<int32_t> row(b->max_ctx);
         for (int m = 0; m < b->B; m++) {
@@ -1388,58 +1281,7 @@ int qie_engine_rope_tables(const qie_engine* e, const float** rope_cos, const fl
 // Cache and time a cache hit rate no decode step sees (round-1 verdict).  lm_head (which 4)
 // has one weight; its 1.09 GB stream cannot stay resident.
 int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* avg_us, double* bytes) {
-    QIE_REQUIRE(b && iters > 0 && avg_us && bytes && which >= 0 && which <= 6, "qie_batch_time_kernel: bad arguments");
-    if (which == 6) {   // the layer chain (O, gate/up, down, next QKV), layers 1 .. L-2
-        QIE_REQUIRE(use_chain(b) && b->e->spec.n_layers >= 3, "qie_batch_time_kernel: no layer chain for this batch");
-        const qie_engine* e = b->e;
-        const int64_t H = e->spec.hidden, QD = (int64_t)e->sh.nq * e->spec.head_dim;
-        const int64_t KD = (int64_t)e->sh.nkv * e->spec.head_dim, I = e->sh.ffn;
-        const int nl = e->spec.n_layers, cus = device_cu_count();
-        unsigned long long* dbg = nullptr;
-        const bool stamps = getenv("QIE_CHAIN_DBG") != nullptr;
-        if (stamps) QIE_TRY(dmalloc((void**)&dbg, (size_t)cus * 16 * 8));
-        hipEvent_t t0, t1;
-        QIE_HIP(hipEventCreate(&t0));
-        QIE_HIP(hipEventCreate(&t1));
-        QIE_TRY(enqueue_chain(b, 1));
-        QIE_HIP(hipEventRecord(t0, e->stream));
-        for (int i = 0; i < iters; i++) QIE_TRY(enqueue_chain(b, 1 + i % (nl - 2), i == iters - 1 ? dbg : nullptr));
-        QIE_HIP(hipEventRecord(t1, e->stream));
-        QIE_HIP(hipEventSynchronize(t1));
-        float ms = 0;
-        QIE_HIP(hipEventElapsedTime(&ms, t0, t1));
-        hipEventDestroy(t0);
-        hipEventDestroy(t1);
-        if (stamps) {   // per-phase wall time, averaged over workgroups, to stderr
-            std::vector<unsigned long long> h((size_t)cus * 16);
-            QIE_HIP(hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost));
-            double acc[8] = {0}, mx[8] = {0};
-            for (int w = 0; w < cus; w++)
-                for (int i = 1; i < 8; i++) {
-                    const double d = (double)(h[(size_t)w * 16 + i] - h[(size_t)w * 16]) * 0.01;   // 100 MHz -> us
-                    acc[i] += d / cus;
-                    mx[i] = std::max(mx[i], d);
-                }
-            fprintf(stderr, "chain stamps (us from workgroup start, mean / max): O-done %.2f/%.2f  G-go %.2f/%.2f  "
-                    "G-done %.2f/%.2f  D-go %.2f/%.2f  D-done %.2f/%.2f  Q-go %.2f/%.2f  end %.2f/%.2f\n",
-                    acc[1], mx[1], acc[2], mx[2], acc[3], mx[3], acc[4], mx[4], acc[5], mx[5], acc[6], mx[6], acc[7],
-                    mx[7]);
-            double gx[8] = {0}, gm[8] = {0};   // G-done by blockIdx % 8 (the XCD of round-robin dispatch)
-            for (int w = 0; w < cus; w++) {
-                const double d = (double)(h[(size_t)w * 16 + 3] - h[(size_t)w * 16]) * 0.01;
-                gx[w % 8] += d * 8.0 / cus;
-                gm[w % 8] = std::max(gm[w % 8], d);
-            }
-            fprintf(stderr, "chain G-done by blockIdx%%8 (mean/max):");
-            for (int x = 0; x < 8; x++) fprintf(stderr, " %.1f/%.1f", gx[x], gm[x]);
-            fprintf(stderr, "\n");
-            hipFree(dbg);
-        }
-        QIE_TRY(check_fuse_err(b));
-        *avg_us = ms * 1000.0 / iters;
-        *bytes = (double)(H * QD + 2 * I * H + H * I + (QD + 2 * KD) * H) * 2.0;
-        return 0;
-    }
+    QIE_REQUIRE(b && iters > 0 && avg_us && bytes && which >= 0 && which <= 5, "qie_batch_time_kernel: bad arguments");
     qie_engine* e = b->e;
     const qie_model_spec& s = e->spec;
     const TpShard& sh = e->sh;   // this rank's shard sizes

@@ -201,11 +201,9 @@ __global__ __launch_bounds__(HD) void attn_combine_kernel(AttnParams a) {
 
 // ---------------------------------------------------------------------------
 // Fused decode attention: q-projection post-processing (qk-norm + RoPE) in the
-// prologue, KV append of the new token (qkv_post fused away), 64-token splits
-// with a two-pass block softmax, and the split combine done by the last
-// arriving workgroup of each (row, kv head) — agent-scope release before the
-// ticket, agent-scope acquire before reading the other splits' partials
-// (cdna_hip_programming.md §5 "In-launch split-K reduction").
+// prologue, KV append of the new token (qkv_post fused away), split-K over the context,
+// and the split combine done by the last arriving workgroup of each (row, kv head):
+// write-through (sc1) partials + ticket, one agent acquire in the combiner.
 // Grid: (nkv * nsplit_max, B); row m has one query token at position pos[m].
 struct DecodeAttnParams {
     const uint16_t* qkv;      // [B][(nq + 2 nkv) * HD] projection output (bias added)
@@ -219,33 +217,17 @@ struct DecodeAttnParams {
     KvMap km;
     int layer, nkv, nq, max_ctx, nsplit_max;
     int splits_target;        // ~splits per (row, kv head) at long context
-    int dbg;                  // timing experiments only (QIE_DEC_DBG): 1 no combine, 2 no release, 4 no acquire,
-                              // 8/16/32 stop after prologue / phase A / phase B, 64 exit at once
+    int dbg;                  // timing experiments only (QIE_DEC_DBG): 1 no combine,
+                              // 8/16 stop after prologue / P.V, 64 exit at once
     float eps;
     int numerics;
     float* part_o;            // [B][nq][nsplit_max][HD]
     float* part_ml;           // [B][nq][nsplit_max][2]
     unsigned* counters;       // [B][nkv], zero at rest
     uint16_t* out;            // [B][nq * HD]
-    int fused;                // 1: inside attn_o_fused_kernel (always the split path + combine)
 };
 
-// Splits per (row, kv head): ~16 at long context (>= 64 keys each), more only when
-// a split would exceed kDecNtMax keys per thread.  All derived from the live context on
-// device, so a captured graph stays valid as the sequence grows.
-constexpr int kDecMinKeys = 64;
-constexpr int kDecSplits = 16;
-constexpr int kDecNtMax = 8;         // keys per thread per split (K and V both held in VGPRs)
-constexpr int kDecMaxSplits = 512;   // 64k keys at head_dim 128, 128k at 64
-
-__host__ __device__ __forceinline__ int dec_tpb(int hd) { return 256 / (hd / 8); }
-__host__ __device__ __forceinline__ int dec_nsplit_target(int ctx, int hd, int splits = kDecSplits) {
-    const int by_min = (ctx + kDecMinKeys - 1) / kDecMinKeys;
-    const int cap = kDecNtMax * dec_tpb(hd);
-    const int by_cap = (ctx + cap - 1) / cap;
-    const int want = by_cap > splits ? by_cap : splits;
-    return by_min < want ? by_min : want;
-}
+constexpr int kDecMaxSplits = 512;   // 64k keys per (row, kv head)
 
 __device__ __forceinline__ void unpack_bf8(const uint4& r, float* f) {
     const uint32_t w[4] = {r.x, r.y, r.z, r.w};
@@ -264,314 +246,9 @@ __device__ __forceinline__ void pin4(float4& v) {
     asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
 }
 
-// Latency structure (B = 1 decode is a chain of dependent memory round trips, not a
-// bandwidth problem): one scalar load of pos, then EVERY global load of the split —
-// the new token's q/k/v slice, norm weights, RoPE row, the split's K rows and V rows —
-// is issued before any arithmetic, so the body costs one HBM round trip; the combine
-// costs one more (partials) plus the ticket atomic.
-// G (q heads per kv head) is a template parameter: a runtime group size made hipcc
-// emit a branch per (key, head) and 12k lines of ISA.
-template <int HD, int G>
-__global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnParams a) {
-#pragma clang fp contract(off)
-    constexpr int LPT = HD / 8;          // lanes per key row
-    constexpr int TPB = 256 / LPT;       // keys per block step (16 or 32)
-    constexpr int NTMAX = kDecNtMax;
-    constexpr int CHMAX = NTMAX * TPB;
-    __shared__ __attribute__((aligned(16))) float q_s[G][HD];
-    __shared__ __attribute__((aligned(16))) uint16_t kv_new[2][HD];
-    __shared__ float p_s[G][CHMAX];
-    __shared__ __attribute__((aligned(16))) float red_o[4][G][HD];
-    __shared__ float stat_m[G], stat_l[G];
-    __shared__ float cw[G][kDecMaxSplits];
-    __shared__ int last_flag;
-
-    const int64_t m = blockIdx.y;
-    const int g = blockIdx.x / a.nsplit_max, s = blockIdx.x % a.nsplit_max;
-    const int p = a.pos[m], ctx = p + 1;
-    const int nst = dec_nsplit_target(ctx, HD, a.splits_target);
-    int chunk = (ctx + nst - 1) / nst;
-    chunk = (chunk + TPB - 1) / TPB * TPB;
-    const int nsplit = (ctx + chunk - 1) / chunk;
-    if (s >= nsplit || (a.dbg & 64)) return;
-    const int t0 = s * chunk, t1 = min(ctx, t0 + chunk);
-    const int ntok = t1 - t0;
-    const bool has_new = (t1 == ctx);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int grp = tid / LPT, dl = tid % LPT;
-    const int QKVD = (a.nq + 2 * a.nkv) * HD;
-    const uint16_t* row = a.qkv + m * (int64_t)QKVD;
-    const bool hf = a.numerics == QIE_NUMERICS_HF;
-    const int64_t head_off = kv_run_off(a.km, (int64_t)a.layer * a.nkv + g, HD);
-    uint16_t* kb = a.kc + m * a.km.stride + head_off;
-    uint16_t* vb = a.vc + m * a.km.stride + head_off;
-
-    // ---------------- issue all loads.  Prologue operands first (vmcnt retires in
-    // order, so waiting for them does not wait for the K/V rows).  Groups past G + 1
-    // and the k/v groups of splits without the new token load valid dummies.
-    const bool is_q = grp < G, is_k = grp == G, is_v = grp == G + 1;
-    const bool pro = is_q || ((is_k || is_v) && has_new);
-    const uint16_t* src = is_q ? row + (g * G + grp) * HD
-                               : (is_k ? row + a.nq * HD + g * HD : row + (a.nq + a.nkv) * HD + g * HD);
-    if (!(is_q || is_k || is_v)) src = row;
-    const uint4 raw = *reinterpret_cast<const uint4*>(src + dl * 8);
-    const uint16_t* nwp = is_q ? a.q_norm : a.k_norm;
-    const uint4 nraw = *reinterpret_cast<const uint4*>((nwp ? nwp : row) + dl * 8);
-    // RoPE row: interleaved pairs (dl*4 .. dl*4+3) or rotate_half (dl*8 % (HD/2) .. +7)
-    const float* cp = a.cs + (int64_t)p * (HD / 2);
-    const float* sp = a.sn + (int64_t)p * (HD / 2);
-    const int rb = hf ? (dl * 8) % (HD / 2) : dl * 4;
-    const float4 c0 = *reinterpret_cast<const float4*>(cp + rb);
-    const float4 s0 = *reinterpret_cast<const float4*>(sp + rb);
-    const int rb2 = hf ? rb + 4 : rb;   // unconditional load (a load under a uniform
-    const float4 c1 = *reinterpret_cast<const float4*>(cp + rb2);   // condition serialises)
-    const float4 s1 = *reinterpret_cast<const float4*>(sp + rb2);
-
-    uint4 kr[NTMAX], vr[NTMAX];
-#pragma unroll
-    for (int i = 0; i < NTMAX; i++) {
-        const int t = t0 + grp + TPB * i;
-        const int tc = t < t1 ? t : t0;   // masked slots re-read a valid row
-        kr[i] = *reinterpret_cast<const uint4*>(kb + (int64_t)tc * HD + dl * 8);
-        vr[i] = *reinterpret_cast<const uint4*>(vb + (int64_t)tc * HD + dl * 8);
-    }
-    __builtin_amdgcn_sched_barrier(0);   // keep prologue math from interleaving (and waiting) mid-issue
-
-    // ---------------- prologue: q heads (norm + RoPE), new K (norm + RoPE), new V.
-    // Computed branch-free by every group (only the stores are predicated): hipcc sinks a
-    // load into the conditional block that consumes it, which would put the norm/RoPE
-    // loads behind the K/V rows in the vmcnt queue.
-    {
-        const bool nrm = nwp != nullptr && !is_v;
-        float x[8], wv[8];
-        unpack_bf8(raw, x);
-        unpack_bf8(nraw, wv);
-        // qk_norm.cu:43-79 (per-head RMSNorm)
-        float ss = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; j++) ss += x[j] * x[j];
-        ss = group_sum<LPT>(ss);
-        const float rms = sqrtf((ss / (float)HD) + a.eps);
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const float xn = hf ? rbf(wv[j] * rbf(x[j] * (1.0f / rms))) : rbf((x[j] / rms) * wv[j]);
-            x[j] = nrm ? xn : x[j];
-        }
-        // RoPE at position p (RoPE.cu:6-22 interleaved / HF rotate_half)
-        const float cv[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-        const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-        float o[8], y[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) o[j] = __shfl_xor(x[j], LPT / 2, 64);
-        const bool first = dl < LPT / 2;
-#pragma unroll
-        for (int j = 0; j < 8; j += 2) {
-            const float ya = rbf(x[j] * cv[j / 2] - x[j + 1] * sv[j / 2]);
-            const float yb = rbf(x[j + 1] * cv[j / 2] + x[j] * sv[j / 2]);
-            const float ha = first ? rbf(rbf(x[j] * cv[j]) + rbf(-o[j] * sv[j])) : rbf(rbf(x[j] * cv[j]) + rbf(o[j] * sv[j]));
-            const float hb = first ? rbf(rbf(x[j + 1] * cv[j + 1]) + rbf(-o[j + 1] * sv[j + 1]))
-                                   : rbf(rbf(x[j + 1] * cv[j + 1]) + rbf(o[j + 1] * sv[j + 1]));
-            y[j] = hf ? ha : ya;
-            y[j + 1] = hf ? hb : yb;
-        }
-#pragma unroll
-        for (int j = 0; j < 8; j++) x[j] = is_v ? x[j] : y[j];
-        if (is_q) {
-#pragma unroll
-            for (int j = 0; j < 8; j++) q_s[grp][dl * 8 + j] = x[j];
-        } else if (pro) {
-            const uint4 packed = make_uint4(pack2(x[0], x[1]), pack2(x[2], x[3]), pack2(x[4], x[5]),
-                                            pack2(x[6], x[7]));
-            uint16_t* dst = (is_k ? kb : vb) + (int64_t)p * HD + dl * 8;
-            *reinterpret_cast<uint4*>(dst) = packed;
-            *reinterpret_cast<uint4*>(&kv_new[is_k ? 0 : 1][dl * 8]) = packed;
-        }
-    }
-    __syncthreads();
-    if (a.dbg & 8) {   // timing: loads + prologue only
-        if (tid == 0) a.out[m] = (uint16_t)(kr[0].x + vr[NTMAX - 1].y + kr[NTMAX - 1].z + vr[0].w);
-        return;
-    }
-
-    // ---------------- phase A: raw scores q.k -> p_s (scaled in phase B)
-    {
-        const uint4 knew = *reinterpret_cast<const uint4*>(&kv_new[0][dl * 8]);
-        float qf[G][8];
-#pragma unroll
-        for (int gi = 0; gi < G; gi++)
-#pragma unroll
-            for (int j = 0; j < 8; j++) qf[gi][j] = q_s[gi][dl * 8 + j];
-#pragma unroll
-        for (int i = 0; i < NTMAX; i++) {
-            const int tl = grp + TPB * i;
-            float kf[8];
-            unpack_bf8(sel4(t0 + tl == p, knew, kr[i]), kf);
-#pragma unroll
-            for (int gi = 0; gi < G; gi++) {
-                float d = 0.f;
-#pragma unroll
-                for (int j = 0; j < 8; j++) d = fmaf(qf[gi][j], kf[j], d);
-                d = group_sum<LPT>(d);
-                if (dl == 0 && tl < ntok) p_s[gi][tl] = d;
-            }
-        }
-    }
-    __syncthreads();
-    if (a.dbg & 16) {
-        if (tid == 0) a.out[m] = (uint16_t)(p_s[0][1] + vr[NTMAX - 1].y + vr[0].w);
-        return;
-    }
-    // ---------------- phase B: s = dot / sqrt(hd); per-head max, p = exp(s - max), l = sum p
-    {
-        const float scale = sqrtf((float)HD);
-        for (int gi = wave; gi < G; gi += 4) {
-            float mx = -INFINITY;
-            for (int j = lane; j < ntok; j += 64) {
-                const float sc = p_s[gi][j] / scale;
-                p_s[gi][j] = sc;
-                mx = fmaxf(mx, sc);
-            }
-            mx = wave_max(mx);
-            float sum = 0.f;
-            for (int j = lane; j < ntok; j += 64) {
-                const float e = expf(p_s[gi][j] - mx);
-                p_s[gi][j] = e;
-                sum += e;
-            }
-            sum = wave_sum(sum);
-            if (lane == 0) {
-                stat_m[gi] = mx;
-                stat_l[gi] = sum;
-            }
-        }
-    }
-    __syncthreads();
-    if (a.dbg & 32) {
-        if (tid == 0) a.out[m] = (uint16_t)(p_s[0][1] + vr[NTMAX - 1].y + vr[0].w);
-        return;
-    }
-    // ---------------- phase C: o = sum p v (V rows already in registers)
-    float o[G][8];
-#pragma unroll
-    for (int gi = 0; gi < G; gi++)
-#pragma unroll
-        for (int j = 0; j < 8; j++) o[gi][j] = 0.f;
-    {
-        const uint4 vnew = *reinterpret_cast<const uint4*>(&kv_new[1][dl * 8]);
-#pragma unroll
-        for (int i = 0; i < NTMAX; i++) {
-            const int tl = grp + TPB * i;
-            if (tl >= ntok) continue;   // divergent only in the split's last step
-            float vf[8];
-            unpack_bf8(sel4(t0 + tl == p, vnew, vr[i]), vf);
-#pragma unroll
-            for (int gi = 0; gi < G; gi++) {
-                const float e = p_s[gi][tl];
-#pragma unroll
-                for (int j = 0; j < 8; j++) o[gi][j] = fmaf(e, vf[j], o[gi][j]);
-            }
-        }
-    }
-#pragma unroll
-    for (int gi = 0; gi < G; gi++) {
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            float v = o[gi][j];
-            if constexpr (LPT == 8) v += dpp_f<0x128>(v);   // row_ror:8 == lane ^ 8
-            o[gi][j] = xor32_sum(xor16_sum(v));
-        }
-    }
-    if (lane < LPT) {
-#pragma unroll
-        for (int gi = 0; gi < G; gi++)
-#pragma unroll
-            for (int j = 0; j < 8; j++) red_o[wave][gi][dl * 8 + j] = o[gi][j];
-    }
-    __syncthreads();
-    const int nq = a.nq;
-    if (nsplit == 1) {
-        for (int idx = tid; idx < G * HD; idx += 256) {
-            const int gi = idx / HD, d = idx % HD;
-            const float ov = red_o[0][gi][d] + red_o[1][gi][d] + red_o[2][gi][d] + red_o[3][gi][d];
-            a.out[m * (int64_t)nq * HD + (int64_t)(g * G + gi) * HD + d] = f2bf(ov / stat_l[gi]);
-        }
-        return;
-    }
-    for (int idx = tid; idx < G * HD; idx += 256) {
-        const int gi = idx / HD, d = idx % HD;
-        const int64_t pi = (m * nq + g * G + gi) * (int64_t)a.nsplit_max + s;
-        a.part_o[pi * HD + d] = red_o[0][gi][d] + red_o[1][gi][d] + red_o[2][gi][d] + red_o[3][gi][d];
-        if (d == 0) {
-            a.part_ml[pi * 2] = stat_m[gi];
-            a.part_ml[pi * 2 + 1] = stat_l[gi];
-        }
-    }
-    // ---------------- publish this split; the last arriver combines (release / acquire)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (a.dbg & 1) return;
-    unsigned* cnt = a.counters + m * a.nkv + g;
-    if (tid == 0) {
-        if (!(a.dbg & 2)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last_flag = (old == (unsigned)nsplit - 1) ? 1 : 0;
-    }
-    __syncthreads();
-    if (!last_flag) return;
-    if (tid == 0 && !(a.dbg & 4)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    // combine weights cw[gi][j] = exp(m_j - M) / sum_j l_j exp(m_j - M): one wave per head
-    for (int gi = wave; gi < G; gi += 4) {
-        const int64_t base = (m * nq + g * G + gi) * (int64_t)a.nsplit_max;
-        float mm = -INFINITY;
-        for (int j = lane; j < nsplit; j += 64) {
-            const float mj = a.part_ml[(base + j) * 2];
-            cw[gi][j] = mj;
-            mm = fmaxf(mm, mj);
-        }
-        mm = wave_max(mm);
-        float lv = 0.f;
-        for (int j = lane; j < nsplit; j += 64) {
-            const float c = expf(cw[gi][j] - mm);
-            cw[gi][j] = c;
-            lv += a.part_ml[(base + j) * 2 + 1] * c;
-        }
-        lv = wave_sum(lv);
-        const float inv = 1.0f / lv;
-        for (int j = lane; j < nsplit; j += 64) cw[gi][j] *= inv;
-    }
-    __syncthreads();
-    for (int idx = tid; idx < G * (HD / 4); idx += 256) {
-        const int gi = idx / (HD / 4), d4 = idx % (HD / 4);
-        const float4* src4 = reinterpret_cast<const float4*>(a.part_o) +
-                             ((m * nq + g * G + gi) * (int64_t)a.nsplit_max) * (HD / 4) + d4;
-        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int j0 = 0; j0 < nsplit; j0 += 16) {
-            float4 v[16];
-#pragma unroll
-            for (int jj = 0; jj < 16; jj++)
-                v[jj] = src4[(int64_t)min(j0 + jj, nsplit - 1) * (HD / 4)];
-#pragma unroll
-            for (int jj = 0; jj < 16; jj++) {
-                const float c = j0 + jj < nsplit ? cw[gi][j0 + jj] : 0.f;
-                acc.x = fmaf(c, v[jj].x, acc.x);
-                acc.y = fmaf(c, v[jj].y, acc.y);
-                acc.z = fmaf(c, v[jj].z, acc.z);
-                acc.w = fmaf(c, v[jj].w, acc.w);
-            }
-        }
-        uint16_t* dst = a.out + m * (int64_t)nq * HD + (int64_t)(g * G + gi) * HD + d4 * 4;
-        *reinterpret_cast<uint2*>(dst) = make_uint2(pack2(acc.x, acc.y), pack2(acc.z, acc.w));
-    }
-    if (tid == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // ---------------------------------------------------------------------------
 // Prefill: causal flash attention on MFMA (v_mfma_f32_16x16x32_bf16).
-// Workgroup = 4 waves = 64 query rows of ONE q head (16 rows per wave); K/V
-// tiles of 64 keys staged in LDS (double-buffered, register prefetch).
+// K/V tiles of 64 keys staged in LDS (double-buffered, register prefetch).
 //   S^T = K . Q^T  — A = K tile (row = key, k = d) from an XOR-swizzled LDS image,
 //                    B = Q^T from registers (lane: q = lane & 15, 8 contiguous d);
 //                    so each lane holds 4 keys x 4 key-tiles of ONE query row and
@@ -592,7 +269,6 @@ struct PrefillAttnParams {
     int layer, nkv, nq, max_ctx;
     int64_t M;
     uint16_t* out;
-    int no_tr;               // diagnostics (QIE_ATTN_NO_TR): V fragments by scalar LDS reads
 };
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -600,179 +276,8 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef short i16x4_t __attribute__((ext_vector_type(4)));
 typedef unsigned int kv16_t __attribute__((ext_vector_type(4)));
 
-template <int HD>
-__global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(PrefillAttnParams a) {
-    constexpr int KT = 64;                 // keys per tile
-    constexpr int CPR = HD / 8;            // 16-byte chunks per row
-    constexpr int KSTEPS = HD / 32;        // MFMA k-steps over d for S
-    constexpr int DT = HD / 16;            // output d tiles
-    constexpr int CHUNKS = KT * CPR;       // per tile per operand
-    constexpr int LPT = CHUNKS / 256;      // chunk loads per thread per operand
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint16_t* Ks = reinterpret_cast<uint16_t*>(smem);                  // [2][KT][HD] swizzled
-    uint16_t* Vs = reinterpret_cast<uint16_t*>(smem + 2 * KT * HD * 2);  // [2][KT][HD] plain
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int fr = lane & 15, g = lane >> 4;
-    const int h = blockIdx.y, seq = blockIdx.z;
-    const int ntiles_q = (a.rows_per_seq + 63) / 64;
-    const int qt = ntiles_q - 1 - (int)blockIdx.x;         // heaviest (latest) rows first
-    const int64_t row0 = (int64_t)seq * a.rows_per_seq;
-    const int rlo = qt * 64, rhi = min(a.rows_per_seq, rlo + 64);
-    const int G = a.nq / a.nkv, kvh = h / G;
-    const int64_t head_off = kv_run_off(a.km, (int64_t)a.layer * a.nkv + kvh, HD);
-    const uint16_t* kb = a.kc + seq * a.km.stride + head_off;
-    const uint16_t* vb = a.vc + seq * a.km.stride + head_off;
-    const int kmax = a.pos[row0 + rhi - 1];                // last key any row of the block needs
-    const int nkt = kmax / KT + 1;
-
-    // this lane's query row (B operand column) and its position
-    const int qrow = min(rlo + wave * 16 + fr, rhi - 1);
-    const int qpos = a.pos[row0 + qrow];
-    bf16x8_t qf[KSTEPS];
-    {
-        const uint16_t* qp = a.q + (row0 + qrow) * (int64_t)a.nq * HD + (int64_t)h * HD;
-#pragma unroll
-        for (int ks = 0; ks < KSTEPS; ks++) qf[ks] = *reinterpret_cast<const bf16x8_t*>(qp + ks * 32 + g * 8);
-    }
-
-    uint4 rk[LPT], rv[LPT];
-    auto gload = [&](int kt) {
-#pragma unroll
-        for (int i = 0; i < LPT; i++) {
-            const int c = tid + 256 * i;
-            const int key = min(kt * KT + c / CPR, kmax);
-            const int ch = c % CPR;
-            rk[i] = *reinterpret_cast<const uint4*>(kb + (int64_t)key * HD + ch * 8);
-            rv[i] = *reinterpret_cast<const uint4*>(vb + (int64_t)key * HD + ch * 8);
-        }
-    };
-    auto lstore = [&](int buf) {
-#pragma unroll
-        for (int i = 0; i < LPT; i++) {
-            const int c = tid + 256 * i;
-            const int r = c / CPR, ch = c % CPR;
-            *reinterpret_cast<uint4*>(Ks + buf * KT * HD + r * HD + ((ch ^ (r & (CPR - 1))) * 8)) = rk[i];
-            *reinterpret_cast<uint4*>(Vs + buf * KT * HD + r * HD + ch * 8) = rv[i];
-        }
-    };
-
-    f32x4_t oacc[DT];
-#pragma unroll
-    for (int d = 0; d < DT; d++) oacc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    float m_run = -INFINITY, l_run = 0.f;
-    const float scale = sqrtf((float)HD);
-
-    gload(0);
-    lstore(0);
-    __syncthreads();
-    int cur = 0;
-    for (int kt = 0; kt < nkt; kt++) {
-        if (kt + 1 < nkt) gload(kt + 1);
-        const uint16_t* K = Ks + cur * KT * HD;
-        const uint16_t* Vt = Vs + cur * KT * HD;
-        // ---- S^T = K . Q^T   (4 key tiles of 16)
-        f32x4_t sacc[4];
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-            sacc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-            const int r = t * 16 + fr;
-#pragma unroll
-            for (int ks = 0; ks < KSTEPS; ks++) {
-                const int ch = ks * 4 + g;
-                const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(K + r * HD + ((ch ^ (r & (CPR - 1))) * 8));
-                sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], sacc[t], 0, 0, 0);
-            }
-        }
-        // ---- online softmax over this tile (row = this lane's query)
-        float sv[4][4];
-        float mt = -INFINITY;
-#pragma unroll
-        for (int t = 0; t < 4; t++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int key = kt * KT + t * 16 + g * 4 + r;
-                const float sc = key <= qpos ? sacc[t][r] / scale : -INFINITY;
-                sv[t][r] = sc;
-                mt = fmaxf(mt, sc);
-            }
-        mt = xor32_max(xor16_max(mt));
-        const float m_new = fmaxf(m_run, mt);
-        const float alpha = expf(m_run - m_new);   // 0 on the first tile
-        float ls = 0.f;
-#pragma unroll
-        for (int t = 0; t < 4; t++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const float e = expf(sv[t][r] - m_new);
-                sv[t][r] = e;
-                ls += e;
-            }
-        ls = xor32_sum(xor16_sum(ls));
-        l_run = l_run * alpha + ls;
-        m_run = m_new;
-        // ---- rescale O rows (q = 4g + r) by their alpha
-        float ar[4];
-#pragma unroll
-        for (int r = 0; r < 4; r++) ar[r] = __shfl(alpha, g * 4 + r, 64);
-#pragma unroll
-        for (int d = 0; d < DT; d++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) oacc[d][r] *= ar[r];
-        // ---- O += P . V
-#pragma unroll
-        for (int c = 0; c < 2; c++) {
-            bf16x8_t pa;
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                pa[j] = (__bf16)sv[2 * c][j];
-                pa[4 + j] = (__bf16)sv[2 * c + 1][j];
-            }
-            const int q4 = fr >> 2, p4 = fr & 3;
-#pragma unroll
-            for (int d = 0; d < DT; d++) {
-                const uint16_t* a0 = Vt + (32 * c + 4 * g + q4) * HD + 16 * d + 4 * p4;
-                const uint16_t* a1 = a0 + 16 * HD;
-                bf16x8_t vb8;
-                if (a.no_tr) {
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        vb8[j] = __builtin_bit_cast(__bf16, Vt[(32 * c + 4 * g + j) * HD + 16 * d + fr]);
-                        vb8[4 + j] = __builtin_bit_cast(__bf16, Vt[(32 * c + 16 + 4 * g + j) * HD + 16 * d + fr]);
-                    }
-                } else {
-                    const i16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (__attribute__((address_space(3))) i16x4_t*)(a0));
-                    const i16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (__attribute__((address_space(3))) i16x4_t*)(a1));
-                    // whole-vector reinterpretation: a per-element short->__bf16 bit_cast
-                    // here was lowered (ROCm 7.2) to a v_perm_b32 that duplicated the low
-                    // half of each dword (caught by tests/test_gpu_probe.py)
-                    vb8 = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
-                }
-                oacc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb8, oacc[d], 0, 0, 0);
-            }
-        }
-        if (kt + 1 < nkt) lstore(cur ^ 1);
-        __syncthreads();
-        cur ^= 1;
-    }
-    // ---- normalise and store rows q = 4g + r of this wave
-    float lr[4];
-#pragma unroll
-    for (int r = 0; r < 4; r++) lr[r] = __shfl(l_run, g * 4 + r, 64);
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-        const int row = rlo + wave * 16 + g * 4 + r;
-        if (row >= rhi) continue;
-        uint16_t* orow = a.out + (row0 + row) * (int64_t)a.nq * HD + (int64_t)h * HD;
-#pragma unroll
-        for (int d = 0; d < DT; d++) orow[16 * d + fr] = f2bf(oacc[d][r] / lr[r]);
-    }
-}
-
 // ---------------------------------------------------------------------------
-// Prefill v2 (default): as attn_prefill_mfma_kernel, but each wave owns 32 query rows
+// Prefill kernel: each wave owns 32 query rows
 // (two 16-row groups), so every K fragment (S^T = K.Q^T) and every V fragment
 // (O += P.V) read from LDS feeds two MFMAs and one staged K/V tile serves 128 rows —
 // LDS reads and staging writes per MFMA halved.  Scores go to the log2 domain once
@@ -1004,351 +509,9 @@ __host__ __device__ __forceinline__ int decm_chunk(int ctx, int target) {
     return kDecMStep * (steps < 1 ? 1 : steps);
 }
 
-template <int HD>
-__global__ __launch_bounds__(256) void attn_decode_mfma_kernel(DecodeAttnParams a) {
-#pragma clang fp contract(off)
-    constexpr int LPT = HD / 8;          // prologue: lanes per head row
-    constexpr int KSTEPS = HD / 32;      // MFMA k-steps over d for S
-    constexpr int DT = HD / 16;          // output d tiles
-    constexpr int CPR = HD / 8;          // 16-byte chunks per row
-    constexpr int VCH = 32 * CPR / 64;   // V chunks per lane per wave step
-    __shared__ __attribute__((aligned(16))) uint16_t q_s[16][HD];
-    __shared__ __attribute__((aligned(16))) uint16_t kv_new[2][HD];
-    __shared__ __attribute__((aligned(16))) uint16_t v_s[4][32 * HD];
-    __shared__ float red_m[4][16], red_l[4][16];
-    __shared__ __attribute__((aligned(16))) float red_o[4][kMaxGroup][HD];
-    __shared__ float cw[kMaxGroup][kDecMaxSplits];
-    __shared__ int last_flag;
-
-    const int64_t m = blockIdx.y;
-    const int g = blockIdx.x / a.nsplit_max, s = blockIdx.x % a.nsplit_max;
-    const int G = a.nq / a.nkv;
-    const int p = a.pos[m], ctx = p + 1;
-    const int chunk = decm_chunk(ctx, a.splits_target);
-    const int nsplit = (ctx + chunk - 1) / chunk;
-    if (s >= nsplit || (a.dbg & 64)) return;
-    const int t0 = s * chunk, t1 = min(ctx, t0 + chunk);
-    const int nstep = (t1 - t0 + kDecMStep - 1) / kDecMStep;
-    const bool has_new = (t1 == ctx);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int fr = lane & 15, gq = lane >> 4;
-    const int grp = tid / LPT, dl = tid % LPT;
-    const int QKVD = (a.nq + 2 * a.nkv) * HD;
-    const uint16_t* row = a.qkv + m * (int64_t)QKVD;
-    const bool hf = a.numerics == QIE_NUMERICS_HF;
-    const int64_t head_off = kv_run_off(a.km, (int64_t)a.layer * a.nkv + g, HD);
-    uint16_t* kb = a.kc + m * a.km.stride + head_off;
-    uint16_t* vb = a.vc + m * a.km.stride + head_off;
-
-    // ---------------- issue all loads: prologue operands first, then step 0's K/V
-    const bool is_q = grp < G, is_k = grp == G, is_v = grp == G + 1;
-    const bool pro = is_q || ((is_k || is_v) && has_new);
-    const uint16_t* src = is_q ? row + (g * G + grp) * HD
-                               : (is_k ? row + a.nq * HD + g * HD : row + (a.nq + a.nkv) * HD + g * HD);
-    if (!(is_q || is_k || is_v)) src = row;
-    uint4 raw = *reinterpret_cast<const uint4*>(src + dl * 8);
-    const uint16_t* nwp = is_q ? a.q_norm : a.k_norm;
-    uint4 nraw = *reinterpret_cast<const uint4*>((nwp ? nwp : row) + dl * 8);
-    const float* cp = a.cs + (int64_t)p * (HD / 2);
-    const float* sp = a.sn + (int64_t)p * (HD / 2);
-    const int rb = hf ? (dl * 8) % (HD / 2) : dl * 4;
-    const int rb2 = hf ? rb + 4 : rb;
-    float4 c0 = *reinterpret_cast<const float4*>(cp + rb);
-    float4 s0 = *reinterpret_cast<const float4*>(sp + rb);
-    float4 c1 = *reinterpret_cast<const float4*>(cp + rb2);
-    float4 s1 = *reinterpret_cast<const float4*>(sp + rb2);
-    __builtin_amdgcn_sched_barrier(0);   // prologue operands ahead of K/V in the vmcnt queue
-
-    uint4 kf[2][KSTEPS], vr[VCH];
-    auto load_step = [&](int st) {
-        const int kbase = t0 + st * kDecMStep + wave * 32;
-#pragma unroll
-        for (int t = 0; t < 2; t++) {
-            const int key = min(kbase + 16 * t + fr, t1 - 1);
-#pragma unroll
-            for (int ks = 0; ks < KSTEPS; ks++)
-                kf[t][ks] = *reinterpret_cast<const uint4*>(kb + (int64_t)key * HD + 32 * ks + 8 * gq);
-        }
-#pragma unroll
-        for (int i = 0; i < VCH; i++) {
-            const int c = lane + 64 * i;
-            const int key = min(kbase + c / CPR, t1 - 1);
-            vr[i] = *reinterpret_cast<const uint4*>(vb + (int64_t)key * HD + (c % CPR) * 8);
-        }
-    };
-    load_step(0);
-    pin4(raw); pin4(nraw); pin4(c0); pin4(s0); pin4(c1); pin4(s1);
-
-    // ---------------- prologue (branch-free; see attn_decode_kernel)
-    {
-        const bool nrm = nwp != nullptr && !is_v;
-        float x[8], wv[8];
-        unpack_bf8(raw, x);
-        unpack_bf8(nraw, wv);
-        float ss = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; j++) ss += x[j] * x[j];
-        ss = group_sum<LPT>(ss);
-        const float rms = sqrtf((ss / (float)HD) + a.eps);
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const float xn = hf ? rbf(wv[j] * rbf(x[j] * (1.0f / rms))) : rbf((x[j] / rms) * wv[j]);
-            x[j] = nrm ? xn : x[j];
-        }
-        const float cv[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-        const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-        float o[8], y[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) o[j] = __shfl_xor(x[j], LPT / 2, 64);
-        const bool first = dl < LPT / 2;
-#pragma unroll
-        for (int j = 0; j < 8; j += 2) {
-            const float ya = rbf(x[j] * cv[j / 2] - x[j + 1] * sv[j / 2]);
-            const float yb = rbf(x[j + 1] * cv[j / 2] + x[j] * sv[j / 2]);
-            const float ha = first ? rbf(rbf(x[j] * cv[j]) + rbf(-o[j] * sv[j])) : rbf(rbf(x[j] * cv[j]) + rbf(o[j] * sv[j]));
-            const float hb = first ? rbf(rbf(x[j + 1] * cv[j + 1]) + rbf(-o[j + 1] * sv[j + 1]))
-                                   : rbf(rbf(x[j + 1] * cv[j + 1]) + rbf(o[j + 1] * sv[j + 1]));
-            y[j] = hf ? ha : ya;
-            y[j + 1] = hf ? hb : yb;
-        }
-#pragma unroll
-        for (int j = 0; j < 8; j++) x[j] = is_v ? x[j] : y[j];
-        const uint4 packed = make_uint4(pack2(x[0], x[1]), pack2(x[2], x[3]), pack2(x[4], x[5]), pack2(x[6], x[7]));
-        if (is_q) {
-            *reinterpret_cast<uint4*>(&q_s[grp][dl * 8]) = packed;
-        } else if (pro) {
-            uint16_t* dst = (is_k ? kb : vb) + (int64_t)p * HD + dl * 8;
-            *reinterpret_cast<uint4*>(dst) = packed;
-            *reinterpret_cast<uint4*>(&kv_new[is_k ? 0 : 1][dl * 8]) = packed;
-        }
-        for (int idx = tid; idx < (16 - G) * CPR; idx += 256)   // padded q rows
-            *reinterpret_cast<uint4*>(&q_s[G + idx / CPR][(idx % CPR) * 8]) = make_uint4(0, 0, 0, 0);
-    }
-    __syncthreads();
-    if (a.dbg & 8) {   // timing: loads + prologue only
-        if (tid == 0) a.out[m] = (uint16_t)(kf[0][0].x + vr[VCH - 1].y + kf[1][KSTEPS - 1].z);
-        return;
-    }
-
-    bf16x8_t qb[KSTEPS];
-    uint4 knew[KSTEPS];
-#pragma unroll
-    for (int ks = 0; ks < KSTEPS; ks++) {
-        qb[ks] = *reinterpret_cast<const bf16x8_t*>(&q_s[fr][32 * ks + 8 * gq]);
-        knew[ks] = *reinterpret_cast<const uint4*>(&kv_new[0][32 * ks + 8 * gq]);
-    }
-    const float scale = sqrtf((float)HD);
-    float m_run = -INFINITY, l_run = 0.f;
-    f32x4_t oacc[DT];
-#pragma unroll
-    for (int d = 0; d < DT; d++) oacc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    uint16_t* vw = &v_s[wave][0];
-    const int q4 = fr >> 2, p4 = fr & 3;
-
-    for (int st = 0; st < nstep; st++) {
-        const int kbase = t0 + st * kDecMStep + wave * 32;
-        // ---- S^T = K . Q^T over this wave's two 16-key tiles
-        f32x4_t sacc[2];
-#pragma unroll
-        for (int t = 0; t < 2; t++) {
-            sacc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-            const bool nw = kbase + 16 * t + fr == p;
-#pragma unroll
-            for (int ks = 0; ks < KSTEPS; ks++)
-                sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                    __builtin_bit_cast(bf16x8_t, sel4(nw, knew[ks], kf[t][ks])), qb[ks], sacc[t], 0, 0, 0);
-        }
-        // ---- V rows -> this wave's LDS slot (the new token's row from kv_new)
-#pragma unroll
-        for (int i = 0; i < VCH; i++) {
-            const int c = lane + 64 * i;
-            const int r = c / CPR, ch = c % CPR;
-            const uint4 vn = *reinterpret_cast<const uint4*>(&kv_new[1][ch * 8]);
-            *reinterpret_cast<uint4*>(vw + r * HD + ch * 8) = sel4(kbase + r == p, vn, vr[i]);
-        }
-        if (st + 1 < nstep) load_step(st + 1);
-        // ---- online softmax (lane: head fr; keys 4 gq + r of tiles 0 and 1)
-        float e[2][4];
-        float mt = -INFINITY;
-#pragma unroll
-        for (int t = 0; t < 2; t++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int key = kbase + 16 * t + 4 * gq + r;
-                const float sc = key < t1 ? sacc[t][r] / scale : -INFINITY;
-                e[t][r] = sc;
-                mt = fmaxf(mt, sc);
-            }
-        mt = xor32_max(xor16_max(mt));
-        const float m_new = fmaxf(m_run, mt);
-        const float m_use = m_new == -INFINITY ? 0.f : m_new;   // a wave with no live key yet
-        const float alpha = expf(m_run - m_use);
-        float ls = 0.f;
-#pragma unroll
-        for (int t = 0; t < 2; t++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                e[t][r] = expf(e[t][r] - m_use);
-                ls += e[t][r];
-            }
-        ls = xor32_sum(xor16_sum(ls));
-        l_run = l_run * alpha + ls;
-        m_run = m_new;
-        float ar[4];
-#pragma unroll
-        for (int r = 0; r < 4; r++) ar[r] = __shfl(alpha, gq * 4 + r, 64);
-#pragma unroll
-        for (int d = 0; d < DT; d++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) oacc[d][r] *= ar[r];
-        // ---- O += P . V, P = hi + lo (k slot 8 gq + j <-> key j < 4 ? 4 gq + j : 16 + 4 gq + j - 4)
-        bf16x8_t ph, pl;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            ph[j] = (__bf16)e[0][j];
-            ph[4 + j] = (__bf16)e[1][j];
-            pl[j] = (__bf16)(e[0][j] - (float)ph[j]);
-            pl[4 + j] = (__bf16)(e[1][j] - (float)ph[4 + j]);
-        }
-        __syncthreads();   // V slot written
-#pragma unroll
-        for (int d = 0; d < DT; d++) {
-            const uint16_t* a0 = vw + (4 * gq + q4) * HD + 16 * d + 4 * p4;
-            const i16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4_t*)(a0));
-            const i16x4_t v1 =
-                __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4_t*)(a0 + 16 * HD));
-            const bf16x8_t vb8 = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
-            oacc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph, vb8, oacc[d], 0, 0, 0);
-            oacc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pl, vb8, oacc[d], 0, 0, 0);
-        }
-        __syncthreads();   // slot free for the next step
-    }
-    if (a.dbg & 16) {
-        if (tid == 0) a.out[m] = (uint16_t)(oacc[0][0] + m_run);
-        return;
-    }
-
-    // ---------------- merge the 4 waves (rows = heads 4 gq + r of this lane)
-    if (gq == 0) {
-        red_m[wave][fr] = m_run;
-        red_l[wave][fr] = l_run;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-        const int h = 4 * gq + r;
-        if (h >= G) continue;
-        const float M = fmaxf(fmaxf(red_m[0][h], red_m[1][h]), fmaxf(red_m[2][h], red_m[3][h]));
-        const float mw = red_m[wave][h];
-        const float sc = mw == -INFINITY ? 0.f : expf(mw - M);
-#pragma unroll
-        for (int d = 0; d < DT; d++) red_o[wave][h][16 * d + fr] = oacc[d][r] * sc;
-    }
-    __syncthreads();
-    const int nq = a.nq;
-    for (int idx = tid; idx < G * HD; idx += 256) {
-        const int h = idx / HD, d = idx % HD;
-        const float M = fmaxf(fmaxf(red_m[0][h], red_m[1][h]), fmaxf(red_m[2][h], red_m[3][h]));
-        float L = 0.f;
-#pragma unroll
-        for (int w = 0; w < 4; w++)
-            if (red_m[w][h] != -INFINITY) L += red_l[w][h] * expf(red_m[w][h] - M);
-        const float ov = red_o[0][h][d] + red_o[1][h][d] + red_o[2][h][d] + red_o[3][h][d];
-        if (nsplit == 1) {
-            a.out[m * (int64_t)nq * HD + (int64_t)(g * G + h) * HD + d] = f2bf(ov / L);
-        } else {
-            const int64_t pi = (m * nq + g * G + h) * (int64_t)a.nsplit_max + s;
-            a.part_o[pi * HD + d] = ov;
-            if (d == 0) {
-                a.part_ml[pi * 2] = M;
-                a.part_ml[pi * 2 + 1] = L;
-            }
-        }
-    }
-    if (nsplit == 1) return;
-    // ---------------- publish this split; the last arriver combines (release / acquire)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (a.dbg & 1) return;
-    unsigned* cnt = a.counters + m * a.nkv + g;
-    if (tid == 0) {
-        if (!(a.dbg & 2)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last_flag = (old == (unsigned)nsplit - 1) ? 1 : 0;
-    }
-    __syncthreads();
-    if (!last_flag) return;
-    if (tid == 0 && !(a.dbg & 4)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    // each (head, d4) item issues its first 16 partial loads together with the m / l loads
-    const bool has_item = tid < G * (HD / 4);
-    const int gi = has_item ? tid / (HD / 4) : 0, d4 = tid % (HD / 4);
-    const float4* src4 =
-        reinterpret_cast<const float4*>(a.part_o) + ((m * nq + g * G + gi) * (int64_t)a.nsplit_max) * (HD / 4) + d4;
-    float4 v[16];
-#pragma unroll
-    for (int jj = 0; jj < 16; jj++) v[jj] = src4[(int64_t)min(jj, nsplit - 1) * (HD / 4)];
-    __builtin_amdgcn_sched_barrier(0);
-    for (int gh = wave; gh < G; gh += 4) {   // cw[h][j] = exp(m_j - M) / sum_j l_j exp(m_j - M)
-        const int64_t base = (m * nq + g * G + gh) * (int64_t)a.nsplit_max;
-        float mm = -INFINITY;
-        float ml[2][2];   // (m, l) of splits lane and lane + 64: one 8-B load each, no 2nd round trip
-#pragma unroll
-        for (int q = 0; q < 2; q++) {
-            const int j = lane + 64 * q;
-            const float2 v2 = j < nsplit ? *reinterpret_cast<const float2*>(&a.part_ml[(base + j) * 2])
-                                         : make_float2(-INFINITY, 0.f);
-            ml[q][0] = v2.x;
-            ml[q][1] = v2.y;
-            mm = fmaxf(mm, v2.x);
-        }
-        for (int j = lane + 128; j < nsplit; j += 64) mm = fmaxf(mm, a.part_ml[(base + j) * 2]);
-        mm = wave_max(mm);
-        float lv = 0.f;
-#pragma unroll
-        for (int q = 0; q < 2; q++) {
-            const int j = lane + 64 * q;
-            if (j >= nsplit) continue;
-            const float c = __expf(ml[q][0] - mm);
-            cw[gh][j] = c;
-            lv += ml[q][1] * c;
-        }
-        for (int j = lane + 128; j < nsplit; j += 64) {
-            const float c = __expf(a.part_ml[(base + j) * 2] - mm);
-            cw[gh][j] = c;
-            lv += a.part_ml[(base + j) * 2 + 1] * c;
-        }
-        lv = wave_sum(lv);
-        const float inv = 1.0f / lv;
-        for (int j = lane; j < nsplit; j += 64) cw[gh][j] *= inv;
-    }
-    __syncthreads();
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int j0 = 0; j0 < nsplit; j0 += 16) {
-        if (j0 > 0) {
-#pragma unroll
-            for (int jj = 0; jj < 16; jj++) v[jj] = src4[(int64_t)min(j0 + jj, nsplit - 1) * (HD / 4)];
-        }
-#pragma unroll
-        for (int jj = 0; jj < 16; jj++) {
-            const float c = j0 + jj < nsplit ? cw[gi][j0 + jj] : 0.f;
-            acc.x = fmaf(c, v[jj].x, acc.x);
-            acc.y = fmaf(c, v[jj].y, acc.y);
-            acc.z = fmaf(c, v[jj].z, acc.z);
-            acc.w = fmaf(c, v[jj].w, acc.w);
-        }
-    }
-    if (has_item) {
-        uint16_t* dst = a.out + m * (int64_t)nq * HD + (int64_t)(g * G + gi) * HD + d4 * 4;
-        *reinterpret_cast<uint2*>(dst) = make_uint2(pack2(acc.x, acc.y), pack2(acc.z, acc.w));
-    }
-    if (tid == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // ---------------------------------------------------------------------------
-// Decode attention, MFMA v2 (default): as attn_decode_mfma_kernel, but the 4 waves of
+// Decode attention, MFMA: as the prefill kernel's 16-row flash step, but the 4 waves of
 // a block split the head dimension for P.V instead of the keys, so no cross-wave
 // softmax merge is needed:
 //   * S^T for the step's 128 keys: wave w computes keys 32w..32w+31 (2 MFMA tiles),
@@ -1392,7 +555,7 @@ __device__ __forceinline__ DecPro dec_pro_issue(const DecodeAttnParams& a, const
 }
 
 // qk-norm + RoPE of the q heads and the new k, then q -> LDS (bf16), new k/v -> cache
-// and LDS.  Branch-free (only the stores are predicated), see attn_decode_kernel.
+// and LDS.  Branch-free (only the stores are predicated), stores predicated, loads unconditional).
 template <int HD>
 __device__ __forceinline__ void dec_pro_finish(const DecodeAttnParams& a, DecPro& d, int dl, int grp, int64_t poff,
                                                uint16_t* kb, uint16_t* vb, uint16_t (*q_s)[HD],
@@ -1630,7 +793,7 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
     float lr[4];
 #pragma unroll
     for (int r = 0; r < 4; r++) lr[r] = __shfl(l_run, gq * 4 + r, 64);
-    if (nsplit == 1 && !a.fused) {
+    if (nsplit == 1) {
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             const int h = 4 * gq + r;
@@ -1670,7 +833,10 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
     }
     __syncthreads();
     if (!last_flag) return false;
-    if (tid == 0 && !(a.dbg & 4)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    // acquire, then plain loads.  Measured alternatives without the fence (sc1 loads of
+    // the write-through partials, MI355X_MICROARCH.md hand-off row 1): 8-B agent-scope
+    // atomic loads 11.4 vs 10.7 us per launch; 16-B sc1 raw buffer loads 73 us.
+    if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     // Per-thread online combine: thread (head gi, d4) loads the (m, l) of EVERY split of its
@@ -1713,7 +879,6 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
     }
     if (has_item) {
         uint16_t* dst = a.out + m * (int64_t)nq * HD + (int64_t)(g * G + gi) * HD + d4 * 4;
-        // write-through 8-B store: the fused O-proj workgroups read it with sc1 loads;
         // divided (not multiplied by 1/l): the softmax normalisation's one rounding
         const unsigned long long pk = (unsigned long long)pack2(acc.x / ls, acc.y / ls) |
                                       ((unsigned long long)pack2(acc.z / ls, acc.w / ls) << 32);
@@ -1728,137 +893,6 @@ __global__ __launch_bounds__(256) void attn_decode_mfma2_kernel(DecodeAttnParams
     attn_decode_mfma2_body<HD, PG>(a, blockIdx.x, blockIdx.y);
 }
 
-// ---------------------------------------------------------------------------
-// Decode attention + O-projection in ONE launch (batch 1, bf16 weights): workgroups take a
-// ticket at entry; tickets [0, n_attn) run the attention above, the rest own two O-proj
-// rows per wave.  An O workgroup issues its weight rows BEFORE waiting for the attention,
-// so the W_o stream overlaps the attention's round trips and the attention -> O launch
-// boundary disappears.  Deadlock-free by construction: every attention ticket was taken by
-// a running workgroup before any O workgroup can wait.  Hand-off: the combining attention
-// workgroups store the output write-through (sc1), drain, then add to `done`; the O side
-// polls `done` (relaxed, bounded by a 20 ms give-up that sets `err`) and reads the row with
-// sc1 loads — cdna_hip_programming.md Guideline 16 / MI355X_MICROARCH.md § visibility,
-// 'atomic add + sc1 loads' form.  The last workgroup to finish zeroes the counters.
-// Per-row arithmetic is the GEMV's (lane chunks k = 8 lane + 512 u, wave butterfly,
-// x = bf16(x + bf16(acc))), so results equal the unfused path bit for bit.
-// counter words: ticket [0], fin [16], err [32], done replica r at [64 + 16 r] (64-B apart:
-// the O workgroups poll the replica of their XCD group, blockIdx % 8, not one hot line)
-constexpr int kFuseCtrWords = 64 + 16 * 8;
-constexpr int kFuseRows = 4;    // O-proj rows per wave
-struct AttnOParams {
-    const uint16_t* wo;       // [H][QD] bf16
-    uint16_t* x;              // residual stream row [H]
-    int64_t H, QD;
-    unsigned* ctr;            // [kFuseCtrWords]: ticket, fin, err, 8 per-XCD `done` replicas (zero at rest)
-    int n_attn;
-    int prefetch;             // 1: W_o rows loaded before the wait (A/B: QIE_FUSE_PF)
-    int sleep;                // poll back-off (QIE_FUSE_SLEEP, s_sleep units of 64 cycles)
-};
-
-template <int HD>
-__global__ __launch_bounds__(256) void attn_o_fused_kernel(DecodeAttnParams a, AttnOParams o) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
-    uint16_t* xs = reinterpret_cast<uint16_t*>(dsm);   // [QD] attention output row
-    __shared__ int role_s;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (tid == 0) role_s = (int)__hip_atomic_fetch_add(&o.ctr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const int t = role_s;
-    if (t < o.n_attn) {
-        if (attn_decode_mfma2_body<HD, false>(a, t, 0)) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
-            __syncthreads();
-            if (tid == 0) {
-#pragma unroll
-                for (int r = 0; r < 8; r++)
-                    __hip_atomic_fetch_add(&o.ctr[64 + 16 * r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-    } else {
-        typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
-        constexpr int R = kFuseRows;
-        const int64_t task = (int64_t)(t - o.n_attn) * 4 + wave;
-        const u32x4v* wr[R];
-#pragma unroll
-        for (int i = 0; i < R; i++) {
-            const int64_t r = task * R + i < o.H ? task * R + i : o.H - 1;
-            wr[i] = reinterpret_cast<const u32x4v*>(o.wo + r * o.QD);
-        }
-        constexpr int U = 8;   // 512-element chunks per row: QD <= 4096
-        u32x4v wv[U][R];
-        auto load_w = [&]() {
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                const int64_t k = (int64_t)lane * 8 + u * 512;
-                const int64_t kc = (k < o.QD ? k : o.QD - 8) / 8;
-#pragma unroll
-                for (int i = 0; i < R; i++) wv[u][i] = __builtin_nontemporal_load(wr[i] + kc);
-            }
-        };
-        if (o.prefetch) load_w();
-        if (tid == 0) {
-            const unsigned target = (unsigned)a.nkv;
-            const unsigned* rep = &o.ctr[64 + 16 * (blockIdx.x & 7)];
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            while (__hip_atomic_load(rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-                for (int z = 0; z < o.sleep; z++) __builtin_amdgcn_s_sleep(1);
-                if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000ull) {   // 20 ms at 100 MHz: give up
-                    __hip_atomic_store(&o.ctr[32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
-            }
-        }
-        __syncthreads();
-        if (!o.prefetch) load_w();
-        for (int64_t k = (int64_t)tid * 4; k < o.QD; k += 1024)
-            *reinterpret_cast<unsigned long long*>(xs + k) = __hip_atomic_load(
-                reinterpret_cast<const unsigned long long*>(a.out + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        float acc[R];
-#pragma unroll
-        for (int i = 0; i < R; i++) acc[i] = 0.f;
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int64_t k = (int64_t)lane * 8 + u * 512;
-            if (k < o.QD) {
-                const uint4 xv = *reinterpret_cast<const uint4*>(xs + k);
-                const uint32_t xw[4] = {xv.x, xv.y, xv.z, xv.w};
-                float xf[8];
-#pragma unroll
-                for (int j = 0; j < 4; j++) { xf[2 * j] = bf_lo(xw[j]); xf[2 * j + 1] = bf_hi(xw[j]); }
-#pragma unroll
-                for (int i = 0; i < R; i++) {
-                    const uint32_t wq[4] = {wv[u][i].x, wv[u][i].y, wv[u][i].z, wv[u][i].w};
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        acc[i] = fmaf(xf[2 * j], bf_lo(wq[j]), acc[i]);
-                        acc[i] = fmaf(xf[2 * j + 1], bf_hi(wq[j]), acc[i]);
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < R; i++) acc[i] = wave_sum(acc[i]);
-        if (lane == 0) {
-#pragma clang fp contract(off)
-#pragma unroll
-            for (int i = 0; i < R; i++) {
-                const int64_t r = task * R + i;
-                if (r < o.H) o.x[r] = f2bf(bf2f(o.x[r]) + rbf(acc[i]));
-            }
-        }
-    }
-    if (tid == 0) {
-        const unsigned f = __hip_atomic_fetch_add(&o.ctr[16], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (f == gridDim.x - 1) {   // every workgroup has finished: reset for the next launch
-            __hip_atomic_store(&o.ctr[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&o.ctr[16], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-            for (int r = 0; r < 8; r++)
-                __hip_atomic_store(&o.ctr[64 + 16 * r], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
 
 // Diagnostics: lane l reads the 8 bytes at element 4*l of an LDS array holding
 // value == element index; out[l][e] = what ds_read_b64_tr_b16 delivered.
@@ -1897,13 +931,11 @@ static int fill_dec_params(DecodeAttnParams& a, const void* qkv, int64_t B, cons
     a.nkv = cache->n_kv_heads;
     a.nq = n_heads;
     a.max_ctx = cache->max_ctx;
-    const bool valu = getenv("QIE_DEC_VALU") && atoi(getenv("QIE_DEC_VALU")) != 0;   // A/B timing only
     const char* se = getenv("QIE_DEC_SPLITS");
     const int senv = se ? std::min(atoi(se), kDecMaxSplits) : 0;
-    a.splits_target = senv > 0 ? senv : (valu ? kDecSplits : kDecMSplits);
+    a.splits_target = senv > 0 ? senv : kDecMSplits;
     a.dbg = getenv("QIE_DEC_DBG") ? atoi(getenv("QIE_DEC_DBG")) : 0;
-    a.nsplit_max = valu ? dec_nsplit_target(cache->max_ctx, cache->head_dim, a.splits_target)
-                        : std::min(a.splits_target, (cache->max_ctx + kDecMStep - 1) / kDecMStep);
+    a.nsplit_max = std::min(a.splits_target, (cache->max_ctx + kDecMStep - 1) / kDecMStep);
     QIE_REQUIRE(a.nsplit_max <= kDecMaxSplits, "qie_attention_decode: max_ctx %d too long", cache->max_ctx);
     a.eps = eps;
     a.numerics = numerics;
@@ -1912,7 +944,6 @@ static int fill_dec_params(DecodeAttnParams& a, const void* qkv, int64_t B, cons
     a.part_o = (float*)((char*)ws + cnt);
     a.part_ml = a.part_o + B * n_heads * (int64_t)a.nsplit_max * cache->head_dim;
     a.out = (uint16_t*)out;
-    a.fused = 0;
     return 0;
 }
 
@@ -1953,22 +984,12 @@ int qie_attention(const void* q, int64_t M, const int32_t* pos, int32_t rows_per
         pa.max_ctx = cache->max_ctx;
         pa.M = M;
         pa.out = (uint16_t*)out;
-        pa.no_tr = getenv("QIE_ATTN_NO_TR") ? 1 : 0;
         const size_t shm = (size_t)2 * 2 * 64 * cache->head_dim * 2;
         const bool pg = pa.km.table != nullptr;
-        if ((!getenv("QIE_ATTN_PREFILL_V1") && !pa.no_tr) || pg) {   // v1: A/B timing and diagnostics only
-            dim3 g2((unsigned)((rows_per_seq + 127) / 128), (unsigned)n_heads, (unsigned)(M / rows_per_seq));
-            auto k2 = cache->head_dim == 128 ? (pg ? attn_prefill_mfma2_kernel<128, true> : attn_prefill_mfma2_kernel<128, false>)
-                                             : (pg ? attn_prefill_mfma2_kernel<64, true> : attn_prefill_mfma2_kernel<64, false>);
-            hipLaunchKernelGGL(k2, g2, dim3(256), shm, (hipStream_t)stream, pa);
-            QIE_LAUNCH_CHECK();
-            return 0;
-        }
-        dim3 grid((unsigned)((rows_per_seq + 63) / 64), (unsigned)n_heads, (unsigned)(M / rows_per_seq));
-        if (cache->head_dim == 128)
-            hipLaunchKernelGGL(attn_prefill_mfma_kernel<128>, grid, dim3(256), shm, (hipStream_t)stream, pa);
-        else
-            hipLaunchKernelGGL(attn_prefill_mfma_kernel<64>, grid, dim3(256), shm, (hipStream_t)stream, pa);
+        dim3 g2((unsigned)((rows_per_seq + 127) / 128), (unsigned)n_heads, (unsigned)(M / rows_per_seq));
+        auto k2 = cache->head_dim == 128 ? (pg ? attn_prefill_mfma2_kernel<128, true> : attn_prefill_mfma2_kernel<128, false>)
+                                         : (pg ? attn_prefill_mfma2_kernel<64, true> : attn_prefill_mfma2_kernel<64, false>);
+        hipLaunchKernelGGL(k2, g2, dim3(256), shm, (hipStream_t)stream, pa);
         QIE_LAUNCH_CHECK();
         return 0;
     }
@@ -2014,8 +1035,8 @@ int qie_debug_tr16_probe(int32_t* out_dev) {
 
 int64_t qie_attention_decode_workspace_bytes(int64_t B, int32_t n_heads, int32_t n_kv_heads, int32_t head_dim,
                                              int32_t max_ctx) {
-    // an upper bound for every splits_target <= kDecMaxSplits (monotone in it)
-    const int64_t ns = dec_nsplit_target(max_ctx, head_dim, kDecMaxSplits);
+    // an upper bound for every splits_target <= kDecMaxSplits (nsplit_max in fill_dec_params)
+    const int64_t ns = std::min<int64_t>(kDecMaxSplits, (max_ctx + kDecMStep - 1) / kDecMStep);
     const int64_t cnt = ((B * n_kv_heads * 4 + 255) / 256) * 256;
     return cnt + B * n_heads * ns * (head_dim + 2) * 4;
 }
@@ -2033,76 +1054,14 @@ int qie_attention_decode(const void* qkv, int64_t B, const int32_t* pos, const v
     DecodeAttnParams a;
     QIE_TRY(fill_dec_params(a, qkv, B, pos, q_norm, k_norm, rope_cos, rope_sin, n_heads, cache, layer, eps, numerics,
                             out, ws));
-    const bool valu = getenv("QIE_DEC_VALU") && atoi(getenv("QIE_DEC_VALU")) != 0;   // A/B timing only
     dim3 grid((unsigned)(a.nkv * a.nsplit_max), (unsigned)B);
-    const int G = n_heads / cache->n_kv_heads;
-    using K = void (*)(DecodeAttnParams);
-    static const K k128[kMaxGroup] = {attn_decode_kernel<128, 1>, attn_decode_kernel<128, 2>,
-                                      attn_decode_kernel<128, 3>, attn_decode_kernel<128, 4>,
-                                      attn_decode_kernel<128, 5>, attn_decode_kernel<128, 6>,
-                                      attn_decode_kernel<128, 7>, attn_decode_kernel<128, 8>};
-    static const K k64[kMaxGroup] = {attn_decode_kernel<64, 1>, attn_decode_kernel<64, 2>,
-                                     attn_decode_kernel<64, 3>, attn_decode_kernel<64, 4>,
-                                     attn_decode_kernel<64, 5>, attn_decode_kernel<64, 6>,
-                                     attn_decode_kernel<64, 7>, attn_decode_kernel<64, 8>};
-    const bool v1 = getenv("QIE_DEC_MFMA1") && atoi(getenv("QIE_DEC_MFMA1")) != 0;   // A/B timing only
     const bool pg = a.km.table != nullptr;
-    if ((!valu && !v1) || pg) {   // the legacy A/B kernels address contiguous caches only
-        auto k2 = cache->head_dim == 128 ? (pg ? attn_decode_mfma2_kernel<128, true> : attn_decode_mfma2_kernel<128, false>)
-                                         : (pg ? attn_decode_mfma2_kernel<64, true> : attn_decode_mfma2_kernel<64, false>);
-        hipLaunchKernelGGL(k2, grid, dim3(256), 0, (hipStream_t)stream, a);
-    } else if (!valu) {
-        if (cache->head_dim == 128)
-            hipLaunchKernelGGL(attn_decode_mfma_kernel<128>, grid, dim3(256), 0, (hipStream_t)stream, a);
-        else
-            hipLaunchKernelGGL(attn_decode_mfma_kernel<64>, grid, dim3(256), 0, (hipStream_t)stream, a);
-    } else {
-        hipLaunchKernelGGL((cache->head_dim == 128 ? k128 : k64)[G - 1], grid, dim3(256), 0, (hipStream_t)stream, a);
-    }
+    auto k2 = cache->head_dim == 128 ? (pg ? attn_decode_mfma2_kernel<128, true> : attn_decode_mfma2_kernel<128, false>)
+                                     : (pg ? attn_decode_mfma2_kernel<64, true> : attn_decode_mfma2_kernel<64, false>);
+    hipLaunchKernelGGL(k2, grid, dim3(256), 0, (hipStream_t)stream, a);
     QIE_LAUNCH_CHECK();
     return 0;
 }
 
 }  // extern "C"
 
-namespace qie {
-// Decode attention + O-projection + residual in one launch (attn_o_fused_kernel); batch 1,
-// bf16 W_o [H][QD] with QD <= 4096; ctr = 4 zeroed unsigned counters owned by the caller.
-int attention_o_fused(const void* qkv, const int32_t* pos, const void* q_norm, const void* k_norm,
-                      const float* rope_cos, const float* rope_sin, int32_t n_heads, const qie_kv_cache* cache,
-                      int32_t layer, float eps, int32_t numerics, void* att_out, void* ws, const void* wo, void* x,
-                      int64_t H, unsigned* ctr, void* stream) {
-    QIE_REQUIRE(qkv && pos && cache && cache->k && cache->v && rope_cos && rope_sin && att_out && ws && wo && x && ctr,
-                "attention_o_fused: bad arguments");
-    QIE_REQUIRE(cache->head_dim == 64 || cache->head_dim == 128, "attention_o_fused: head_dim 64 or 128");
-    QIE_REQUIRE(n_heads % cache->n_kv_heads == 0 && n_heads / cache->n_kv_heads <= kMaxGroup,
-                "attention_o_fused: bad head grouping");
-    QIE_REQUIRE(layer >= 0 && layer < cache->n_layers, "attention_o_fused: bad layer");
-    const int64_t QD = (int64_t)n_heads * cache->head_dim;
-    QIE_REQUIRE(QD <= 4096 && QD % 8 == 0, "attention_o_fused: QD %lld unsupported", (long long)QD);
-    DecodeAttnParams a;
-    QIE_TRY(fill_dec_params(a, qkv, 1, pos, q_norm, k_norm, rope_cos, rope_sin, n_heads, cache, layer, eps, numerics,
-                            att_out, ws));
-    QIE_REQUIRE(!a.km.table, "attention_o_fused: contiguous KV caches only");
-    a.fused = 1;
-    AttnOParams o;
-    o.wo = (const uint16_t*)wo;
-    o.x = (uint16_t*)x;
-    o.H = H;
-    o.QD = QD;
-    o.ctr = ctr;
-    o.n_attn = a.nkv * a.nsplit_max;
-    o.prefetch = getenv("QIE_FUSE_PF") ? atoi(getenv("QIE_FUSE_PF")) : 1;
-    o.sleep = getenv("QIE_FUSE_SLEEP") ? atoi(getenv("QIE_FUSE_SLEEP")) : 16;
-    const int n_o = (int)((H + 4 * kFuseRows - 1) / (4 * kFuseRows));
-    const size_t shm = (size_t)QD * 2;
-    if (cache->head_dim == 128)
-        hipLaunchKernelGGL(attn_o_fused_kernel<128>, dim3((unsigned)(o.n_attn + n_o)), dim3(256), shm, (hipStream_t)stream,
-                           a, o);
-    else
-        hipLaunchKernelGGL(attn_o_fused_kernel<64>, dim3((unsigned)(o.n_attn + n_o)), dim3(256), shm, (hipStream_t)stream,
-                           a, o);
-    QIE_LAUNCH_CHECK();
-    return 0;
-}
-}  // namespace qie

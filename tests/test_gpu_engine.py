@@ -132,25 +132,6 @@ def test_graph_equals_eager_and_batch_equals_single(oracle):
     assert np.array_equal(outs[True][1], outs[False][1])
 
 
-@pytest.mark.parametrize("name", ["qwen2-bias-hd64", "qwen3-qknorm-hd128"])
-def test_fused_attention_o_equals_two_launches(oracle, name, monkeypatch):
-    """The opt-in one-launch attention + O-proj + residual (QIE_FUSE_AO=1, attn_o_fused_kernel:
-    ticket-ordered roles, write-through hand-off) has the GEMV's per-row arithmetic, so ids
-    and logits equal the two-launch path bit for bit — across the 1 -> 2 split boundary
-    (128 keys) of the decode attention."""
-    spec = CONFIGS[name]
-    out = {}
-    for fuse in ("1", "0"):
-        monkeypatch.setenv("QIE_FUSE_AO", fuse)
-        eng = Q.Engine(spec, max_ctx=400).init_synthetic(SYN)
-        b = eng.batch(1, 400)
-        prompt = list(rng(5).integers(0, spec.vocab, 100))
-        ids = [b.prefill(0, prompt)] + [int(t) for t in b.decode(60)[:, 0]]
-        out[fuse] = (ids, b.logits())
-    assert out["1"][0] == out["0"][0]
-    assert np.array_equal(out["1"][1], out["0"][1])
-
-
 def test_weights_bin_loader_equals_synthetic(oracle, tmp_path):
     spec = CONFIGS["qwen3-qknorm-hd128"]
     hw = W.HostWeights.synthetic(spec, SYN)

@@ -297,12 +297,8 @@ def test_attention_decode(oracle, qlib, hd, nq, nkv, ctxs):
 
 
 @pytest.mark.parametrize("P,hd", [(1, 64), (7, 64), (64, 64), (257, 64), (33, 128), (130, 128), (511, 128)])
-@pytest.mark.parametrize("v1", [False, True])
-def test_attention_prefill_causal(oracle, qlib, P, hd, v1, monkeypatch):
-    """Causal prefill attention (flash, MFMA) vs the oracle's self_attension.cu restatement;
-    v1 (64 rows per block, libm expf) is kept for A/B timing and checked the same way."""
-    if v1:
-        monkeypatch.setenv("QIE_ATTN_PREFILL_V1", "1")
+def test_attention_prefill_causal(oracle, qlib, P, hd):
+    """Causal prefill attention (flash, MFMA) vs the oracle's self_attension.cu restatement."""
     nq, nkv, L, layer, maxc = 14, 2, 1, 0, 512
     seq_stride = L * nkv * maxc * hd
     kc_h = rand_bf16(oracle, (1, L, nkv, maxc, hd), seed=P)

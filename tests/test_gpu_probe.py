@@ -53,12 +53,9 @@ def test_tr16_lane_mapping(qlib):
     assert np.array_equal(got, want), "tr16 mapping differs; see gpurun_out/tr16_probe.txt"
 
 
-@pytest.mark.parametrize("no_tr", [False, True])
 @pytest.mark.parametrize("hd", [64, 128])
-def test_flash_pv_uniform(oracle, qlib, no_tr, hd, monkeypatch):
+def test_flash_pv_uniform(oracle, qlib, hd):
     """Q = 0: every score is 0, so O[q] = mean(V[0..q])."""
-    if no_tr:
-        monkeypatch.setenv("QIE_ATTN_NO_TR", "1")
     P = 64
     rng = np.random.default_rng(0)
     v = oracle.f32_to_bf16(rng.standard_normal((1, P, hd)).astype(np.float32))
@@ -72,11 +69,8 @@ def test_flash_pv_uniform(oracle, qlib, no_tr, hd, monkeypatch):
     assert not len(rows), f"rows {rows[:10]} wrong; first bad row err {err[rows[0]].max() if len(rows) else 0}"
 
 
-@pytest.mark.parametrize("no_tr", [False, True])
-def test_flash_probabilities_onehot_v(oracle, qlib, no_tr, monkeypatch):
+def test_flash_probabilities_onehot_v(oracle, qlib):
     """V[key] = e_key (hd = 64 >= P): O[q][d] = softmax probability of key d for query q."""
-    if no_tr:
-        monkeypatch.setenv("QIE_ATTN_NO_TR", "1")
     P, hd = 48, 64
     rng = np.random.default_rng(1)
     q = oracle.f32_to_bf16(rng.standard_normal((P, hd)).astype(np.float32))

@@ -26,10 +26,10 @@ def main():
     sets = os.environ.get("UB_SET", "attn,gemv").split(",")
     variants = []
     if "attn" in sets:
-        variants += [("attn", 5, {}), ("attn", 5, {"QIE_DEC_MFMA1": "1"})]
+        variants += [("attn", 5, {})]
         for sp in ("8", "16", "24", "48"):
             variants.append(("attn", 5, {"QIE_DEC_SPLITS": sp}))
-        variants += [("attn", 5, {"QIE_DEC_DBG": d}) for d in ("1", "6", "8", "16", "64")]
+        variants += [("attn", 5, {"QIE_DEC_DBG": d}) for d in ("1", "8", "16", "64")]
     if "gemv" in sets:
         for which in (0, 1, 2, 3, 4):
             variants.append((NAMES[which], which, {}))

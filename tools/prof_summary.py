@@ -34,6 +34,53 @@ def short(name):
     return n
 
 
+def in_graph_decode(trace):
+    """Per-layer in-graph decode durations: the launches between two finalize_kernel
+    dispatches are one hipGraph decode step (5 per layer + lm_head + finalize); layer 0 is
+    left out (its weights follow the previous step's lm_head) and so are the bench's
+    live-timing loops (after the last finalize).  Gap = this kernel's start minus the
+    previous kernel's end (the dependent-launch boundary)."""
+    t = sorted(trace, key=lambda r: int(r["Start_Timestamp"]))
+    fin = [i for i, r in enumerate(t) if short(r["Kernel_Name"]) == "finalize_kernel"]
+    roles = ["QKV GEMV", "attention", "O GEMV", "gate/up GEMV", "down GEMV"]
+    dur = collections.defaultdict(list)
+    gap = collections.defaultdict(list)
+    steps = []
+    for a, b in zip(fin, fin[1:]):
+        seg = t[a + 1:b + 1]
+        if len(seg) < 7 or (len(seg) - 2) % 5:
+            continue
+        L = (len(seg) - 2) // 5
+        if short(seg[1]["Kernel_Name"]).startswith("attn_decode") is False:
+            continue
+        steps.append((int(seg[-1]["End_Timestamp"]) - int(t[a]["End_Timestamp"])) / 1e3)
+        for i, r in enumerate(seg):
+            s0, e0 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+            pe = int(seg[i - 1]["End_Timestamp"]) if i else int(t[a]["End_Timestamp"])
+            if i < 5 * L:
+                if i // 5 == 0:
+                    continue
+                role = roles[i % 5]
+            else:
+                role = "lm_head GEMV" if i == 5 * L else "finalize"
+            dur[role].append((e0 - s0) / 1e3)
+            gap[role].append((s0 - pe) / 1e3)
+    if not steps:
+        return []
+    out = ["", f"## In-graph decode step ({len(steps)} steps, layers 1..L-1; layer 0 excluded)", "",
+           "Kernel durations only: under --kernel-trace the profiler serialises graph nodes, so "
+           "its inter-kernel gaps (and step spans) are profiler artefacts, not the bench's clock.", "",
+           "| role | launches | avg us | median us |", "|---|---|---|---|"]
+    for role in roles + ["lm_head GEMV", "finalize"]:
+        v = dur[role]
+        out.append(f"| {role} | {len(v)} | {statistics.mean(v):.2f} | {statistics.median(v):.2f} |")
+    per_layer = sum(statistics.mean(dur[r]) for r in roles)
+    out.append("")
+    out.append(f"Sum of in-graph kernel durations per layer: {per_layer:.1f} us; "
+               f"gate/up in-graph average {statistics.mean(dur['gate/up GEMV']):.2f} us.")
+    return out
+
+
 def main(tag="r01", src="gpurun_out/prof"):
     src = os.path.join(ROOT, src)
     trace = list(csv.DictReader(open(os.path.join(src, "run_kernel_trace.csv"))))
@@ -55,6 +102,7 @@ def main(tag="r01", src="gpurun_out/prof"):
     for name, v in sorted(groups.items(), key=lambda kv: -sum(kv[1])):
         lines.append(f"| `{name}` | {ROLE.get(name, '')} | {len(v)} | {statistics.mean(v):.2f} | "
                      f"{statistics.median(v):.2f} | {sum(v) / 1e3:.3f} | {100 * sum(v) / total:.2f} |")
+    lines += in_graph_decode(trace)
     lines += ["", "Raw per-kernel stats (rocprofv3 `--stats`, template arguments folded): "
               f"`{tag}_kernel_stats.csv`."]
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)

@@ -12,7 +12,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libqie.so")
+LIB_PATH = os.environ.get("QIE_LIB") or os.path.join(_HERE, "lib", "libqie.so")   # QIE_LIB: dev A/B builds
 
 QIE_NUMERICS_REF = 0
 QIE_NUMERICS_HF = 1

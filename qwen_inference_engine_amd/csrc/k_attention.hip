@@ -277,14 +277,16 @@ typedef short i16x4_t __attribute__((ext_vector_type(4)));
 typedef unsigned int kv16_t __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------------------
-// Prefill kernel: each wave owns 32 query rows
-// (two 16-row groups), so every K fragment (S^T = K.Q^T) and every V fragment
-// (O += P.V) read from LDS feeds two MFMAs and one staged K/V tile serves 128 rows —
-// LDS reads and staging writes per MFMA halved.  Scores go to the log2 domain once
+// Prefill kernel: each wave owns two 16-row query groups, so every K fragment
+// (S^T = K.Q^T) and every V fragment (O += P.V) read from LDS feeds up to two MFMAs.
+// Causal balance: the sequence's 16-row groups are paired (j, n-1-j) and wave j of the
+// grid gets pair j, so every wave (and every workgroup of 4 waves) has the same number of
+// (group, key tile) products; a workgroup stages K/V tiles up to its latest row and each
+// group skips the tiles past its own last position (the contiguous 128-row q tiles this
+// replaces left the workgroup with the last tile 16x the work of the first: 2x the
+// makespan of the balanced split on 256 CUs).  Scores go to the log2 domain once
 // (dot * log2(e) / sqrt(hd)) and are exponentiated with v_exp_f32: the reference build
-// compiles with -use_fast_math, i.e. __expf / __fdividef, so the libm
-// expf and IEEE division of v1 (~25 VALU ops per score) bought nothing but VALU time.
-// A wave skips the MFMAs of a tile whose first key lies past its last row's position.
+// compiles with -use_fast_math, i.e. __expf / __fdividef.
 template <int HD, bool PG>
 __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnParams a) {
     constexpr int KT = 64;
@@ -294,7 +296,6 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
     constexpr int CHUNKS = KT * CPR;
     constexpr int LPT = CHUNKS / 256;
     constexpr int QG = 2;                  // 16-row query groups per wave
-    constexpr int BQ = 4 * 16 * QG;        // query rows per block
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint16_t* Ks = reinterpret_cast<uint16_t*>(smem);
     uint16_t* Vs = reinterpret_cast<uint16_t*>(smem + 2 * KT * HD * 2);
@@ -306,25 +307,31 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int fr = lane & 15, g = lane >> 4;
     const int h = blockIdx.y, seq = blockIdx.z;
-    const int ntiles_q = (a.rows_per_seq + BQ - 1) / BQ;
-    const int qt = ntiles_q - 1 - (int)blockIdx.x;
-    const int64_t row0 = (int64_t)seq * a.rows_per_seq;
-    const int rlo = qt * BQ, rhi = min(a.rows_per_seq, rlo + BQ);
+    const int R = a.rows_per_seq;
+    const int ngr = (R + 15) / 16, npair = (ngr + 1) / 2;
+    const int64_t row0 = (int64_t)seq * R;
     const int G = a.nq / a.nkv, kvh = h / G;
     const int64_t head_off = kv_run_off(a.km, (int64_t)a.layer * a.nkv + kvh, HD);
     const uint16_t* kb = a.kc + head_off;
     const uint16_t* vb = a.vc + head_off;
-    const int kmax = a.pos[row0 + rhi - 1];
+    // this wave's groups: pair j = (j, ngr-1-j); the workgroup's latest row is wave 0's
+    // second group (positions are non-decreasing within a sequence)
+    const int j = blockIdx.x * 4 + wave;
+    const int grp[QG] = {j, ngr - 1 - j};
+    bool gact[QG];
+    gact[0] = j < npair;
+    gact[1] = j < npair && grp[1] != j;
+    const int kmax = a.pos[row0 + min(16 * (ngr - 1 - (int)blockIdx.x * 4) + 15, R - 1)];
     const int nkt = kmax / KT + 1;
-    // positions are non-decreasing within a sequence: the wave's last row bounds its keys
-    const int wpos = a.pos[row0 + min(rlo + wave * 16 * QG + 16 * QG - 1, rhi - 1)];
 
-    int qpos[QG];
+    int qpos[QG], gpos[QG];
     bf16x8_t qf[QG][KSTEPS];
 #pragma unroll
     for (int q = 0; q < QG; q++) {
-        const int qrow = min(rlo + wave * 16 * QG + q * 16 + fr, rhi - 1);
+        const int gq = gact[q] ? grp[q] : 0;
+        const int qrow = min(16 * gq + fr, R - 1);
         qpos[q] = a.pos[row0 + qrow];
+        gpos[q] = gact[q] ? a.pos[row0 + min(16 * gq + 15, R - 1)] : -1;   // -1: no tile
         const uint16_t* qp = a.q + (row0 + qrow) * (int64_t)a.nq * HD + (int64_t)h * HD;
 #pragma unroll
         for (int ks = 0; ks < KSTEPS; ks++) qf[q][ks] = *reinterpret_cast<const bf16x8_t*>(qp + ks * 32 + g * 8);
@@ -377,7 +384,10 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
         if (kt + 1 < nkt) gload(kt + 1);
         const uint16_t* K = Ks + cur * KT * HD;
         const uint16_t* Vt = Vs + cur * KT * HD;
-        if (kt * KT <= wpos) {   // wave-uniform
+        bool on[QG];
+#pragma unroll
+        for (int q = 0; q < QG; q++) on[q] = kt * KT <= gpos[q];   // wave-uniform
+        if (on[0] || on[1]) {
             f32x4_t sacc[QG][4];
 #pragma unroll
             for (int t = 0; t < 4; t++) {
@@ -390,12 +400,13 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
                     const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(K + r * HD + ((ch ^ (r & (CPR - 1))) * 8));
 #pragma unroll
                     for (int q = 0; q < QG; q++)
-                        sacc[q][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[q][ks], sacc[q][t], 0, 0, 0);
+                        if (on[q]) sacc[q][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[q][ks], sacc[q][t], 0, 0, 0);
                 }
             }
             float pv[QG][4][4];   // this tile's probabilities (fp32), split into bf16 parts at P.V
 #pragma unroll
             for (int q = 0; q < QG; q++) {
+                if (!on[q]) continue;
                 float (&sv)[4][4] = pv[q];
                 float mt = -INFINITY;
 #pragma unroll
@@ -433,19 +444,18 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
             const int q4 = fr >> 2, p4 = fr & 3;
 #pragma unroll
             for (int c = 0; c < 2; c++) {
-                // P = hi + mid + lo: three bf16 parts carry all 24 bits of each fp32
-                // probability, so the P.V products are the reference's fp32 products
-                // (self_attension.cu:127-135); only the accumulation order differs
-                bf16x8_t ph[QG], pm[QG], pl[QG];
+                // P = hi + lo: two bf16 parts carry 16 of the 24 mantissa bits of each fp32
+                // probability; the dropped remainder is < 2^-16 of p, a relative error per
+                // P.V product (<= 2^-17) below the fp32 summation-order spread of the
+                // reference's own sum over keys
+                bf16x8_t ph[QG], pl[QG];
 #pragma unroll
                 for (int q = 0; q < QG; q++)
 #pragma unroll
-                    for (int j = 0; j < 8; j++) {
-                        const float e = pv[q][2 * c + (j >> 2)][j & 3];
-                        ph[q][j] = (__bf16)e;
-                        const float r1 = e - (float)ph[q][j];
-                        pm[q][j] = (__bf16)r1;
-                        pl[q][j] = (__bf16)(r1 - (float)pm[q][j]);
+                    for (int jj = 0; jj < 8; jj++) {
+                        const float e = on[q] ? pv[q][2 * c + (jj >> 2)][jj & 3] : 0.f;
+                        ph[q][jj] = (__bf16)e;
+                        pl[q][jj] = (__bf16)(e - (float)ph[q][jj]);
                     }
 #pragma unroll
                 for (int d = 0; d < DT; d++) {
@@ -460,8 +470,8 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
                         __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
                     for (int q = 0; q < QG; q++) {
+                        if (!on[q]) continue;
                         oacc[q][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph[q], vb8, oacc[q][d], 0, 0, 0);
-                        oacc[q][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pm[q], vb8, oacc[q][d], 0, 0, 0);
                         oacc[q][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pl[q], vb8, oacc[q][d], 0, 0, 0);
                     }
                 }
@@ -473,13 +483,14 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
     }
 #pragma unroll
     for (int q = 0; q < QG; q++) {
+        if (!gact[q]) continue;
         float lr[4];
 #pragma unroll
         for (int r = 0; r < 4; r++) lr[r] = __shfl(l_run[q], g * 4 + r, 64);
 #pragma unroll
         for (int r = 0; r < 4; r++) {
-            const int row = rlo + wave * 16 * QG + q * 16 + g * 4 + r;
-            if (row >= rhi) continue;
+            const int row = 16 * grp[q] + g * 4 + r;
+            if (row >= R) continue;
             uint16_t* orow = a.out + (row0 + row) * (int64_t)a.nq * HD + (int64_t)h * HD;
 #pragma unroll
             for (int d = 0; d < DT; d++) orow[16 * d + fr] = f2bf(oacc[q][d][r] / lr[r]);
@@ -970,7 +981,7 @@ int qie_attention(const void* q, int64_t M, const int32_t* pos, int32_t rows_per
                 "qie_attention: n_heads/n_kv_heads must be an integer <= %d", kMaxGroup);
     QIE_REQUIRE(layer >= 0 && layer < cache->n_layers, "qie_attention: bad layer");
     if (M == 0) return 0;
-    if (rows_per_seq >= 32 && M % rows_per_seq == 0 && !getenv("QIE_ATTN_NO_MFMA")) {
+    if (rows_per_seq >= 32 && M % rows_per_seq == 0) {
         PrefillAttnParams pa;
         pa.q = (const uint16_t*)q;
         pa.pos = pos;
@@ -986,7 +997,9 @@ int qie_attention(const void* q, int64_t M, const int32_t* pos, int32_t rows_per
         pa.out = (uint16_t*)out;
         const size_t shm = (size_t)2 * 2 * 64 * cache->head_dim * 2;
         const bool pg = pa.km.table != nullptr;
-        dim3 g2((unsigned)((rows_per_seq + 127) / 128), (unsigned)n_heads, (unsigned)(M / rows_per_seq));
+        // balanced causal split: ceil(ceil(R / 16) / 2) group pairs, 4 per workgroup
+        const int npair = ((rows_per_seq + 15) / 16 + 1) / 2;
+        dim3 g2((unsigned)((npair + 3) / 4), (unsigned)n_heads, (unsigned)(M / rows_per_seq));
         auto k2 = cache->head_dim == 128 ? (pg ? attn_prefill_mfma2_kernel<128, true> : attn_prefill_mfma2_kernel<128, false>)
                                          : (pg ? attn_prefill_mfma2_kernel<64, true> : attn_prefill_mfma2_kernel<64, false>);
         hipLaunchKernelGGL(k2, g2, dim3(256), shm, (hipStream_t)stream, pa);

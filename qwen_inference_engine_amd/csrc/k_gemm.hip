@@ -355,16 +355,20 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p, int n_mt) {
         const uint16_t* As = reinterpret_cast<const uint16_t*>(smem + (kt & (NSL - 1)) * SB);
         const uint16_t* Bs = As + TM * TK;
         bf16x8 af[8], bfr[NJ];
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const int row = wm * 128 + i * 16 + fr;
-            af[i] = *reinterpret_cast<const bf16x8*>(As + row * TK + ((g ^ big_swz(row)) * 8));
-        }
+        // every fragment read is issued before the first MFMA (B first, then A in MFMA
+        // order): one exposed LDS latency per k-tile instead of the compiler's four
+        // read-two / wait-all / eight-MFMA batches (P = 2048: gate/up -2 %, O and down -6 %)
 #pragma unroll
         for (int j = 0; j < NJ; j++) {
             const int row = wn * (BNT / 4) + j * 16 + fr;
             bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + row * TK + ((g ^ big_swz(row)) * 8));
         }
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int row = wm * 128 + i * 16 + fr;
+            af[i] = *reinterpret_cast<const bf16x8*>(As + row * TK + ((g ^ big_swz(row)) * 8));
+        }
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < 8; i++)
 #pragma unroll

@@ -33,3 +33,34 @@ def test_cli_prompt_file_stream_and_paged(tmp_path):
     streamed = [int(l) for l in out.splitlines() if l.strip().isdigit()]
     assert _tokens(out) == base          # 24 + 140 tokens: crosses a 128-token page
     assert streamed == base
+
+
+def test_cli_greedy_tokens_match_oracle(oracle):
+    """qie_cli --greedy (Qwen2-0.5B, 24 layers, synthetic seed 5 — the CLI's own weight
+    init, reproduced on the host) against the CPU oracle teacher-forced on the CLI's ids:
+    every CLI token is the oracle's arg-max or a near-tie within the oracle's own
+    summation-order spread (tests/parity.py), at most max_flips of them."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from parity import OrderPair, oracle_trace, max_flips
+    import gpu_util as G
+    from qwen_inference_engine_amd import spec as S, weights as W
+    prompt = [151643, 785, 4767, 315, 279, 3639, 4180, 374]   # the reference's ids (iengine.cu:325)
+    n = 12
+    r = subprocess.run([CLI, "--model", "Qwen2-0.5B", "--synthetic", "5", "--greedy", "--gen", str(n),
+                        "--prompt", ",".join(map(str, prompt))], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr
+    got = _tokens(r.stdout)
+    assert len(got) == n or got[-1] == 151645
+    spec = S.QWEN2_0_5B   # numerics "ref": rms eps 1e-4, as the CLI's reference preset
+    hw = W.HostWeights.synthetic(spec, W.SynthParams(seed=5))
+    pair = OrderPair(oracle, hw, len(prompt) + n + 4)
+    ids, outs = oracle_trace(oracle, pair, prompt, len(got), forced=got[:-1])
+    flips = 0
+    for i, (t, (lg0, _)) in enumerate(zip(got, outs)):
+        if t != ids[i]:
+            gap = abs(float(G.bf(lg0[ids[i]])) - float(G.bf(lg0[t])))
+            _, gap_bar = pair.bars(lg0)
+            assert gap <= gap_bar, f"step {i}: cli {t} vs oracle {ids[i]}, oracle gap {gap} > {gap_bar}"
+            flips += 1
+    assert flips <= max_flips(len(got)), f"{flips} near-tie flips in {len(got)} steps"

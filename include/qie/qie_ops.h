@@ -235,6 +235,11 @@ int qie_synthetic_fill_host(void* host, int64_t n, uint32_t tensor_id, uint64_t 
 int64_t qie_fp8_weight_bytes(int64_t rows, int64_t cols);
 int qie_quantize_fp8(const void* w_bf16, int64_t rows, int64_t cols, void* out, void* stream);
 int qie_quantize_fp8_host(const void* w_bf16, int64_t rows, int64_t cols, void* out);
+/* The inverse, on device: rows x cols bf16 (exact — every dequantised value is a bf16).
+ * The engine's fp8 prefill (M >= 256 rows) expands each weight into a scratch with it and
+ * runs the bf16 LDS-DMA GEMM: at prefill sizes the GEMM is MFMA-bound and the expansion
+ * (1 + 2 bytes per weight) is ~2 % of it. */
+int qie_dequantize_fp8(const void* w_fp8, int64_t rows, int64_t cols, void* out_bf16, void* stream);
 /* Test probe: out_dev[i] = the device decode of e4m3 code i (i < 256). */
 int qie_debug_fp8_decode(float* out_dev);
 

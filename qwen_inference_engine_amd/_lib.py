@@ -124,6 +124,7 @@ SIGNATURES = [
     ("qie_fp8_weight_bytes", C.c_int64, [_I64, _I64]),
     ("qie_quantize_fp8", C.c_int, [_P, _I64, _I64, _P, _P]),
     ("qie_quantize_fp8_host", C.c_int, [_P, _I64, _I64, _P]),
+    ("qie_dequantize_fp8", C.c_int, [_P, _I64, _I64, _P, _P]),
     ("qie_debug_fp8_decode", C.c_int, [_P]),
     # qie_engine.h
     ("qie_comm_unique_id", C.c_int, [_P]),

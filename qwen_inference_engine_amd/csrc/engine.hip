@@ -81,6 +81,10 @@ struct qie_engine {
     qie_model_weights w{};
     bool have_weights = false;
     bool fp8 = false;            // linear weights are e4m3 + row scales (fp8_arena)
+    // fp8 engines: the same (dequantised) layer weights as bf16, in place in the arena —
+    // prefill's MFMA GEMMs read these (compute-bound: the LDS-DMA bf16 kernel), decode's
+    // bandwidth-bound GEMVs the fp8 codes; both compute the one dequantised model
+    std::vector<qie_layer_weights> layers_pf;
     void* fp8_arena = nullptr;
     float* rope_cos = nullptr;
     float* rope_sin = nullptr;
@@ -271,7 +275,10 @@ static int check_align(const void* p, const char* what, int layer) {
 // device into a second arena (OCP e4m3 codes + power-of-two row scales, qie_ops.h) and
 // the layer pointers switched to it; embeddings, norms and biases stay bf16 in the
 // first arena (a tied embedding keeps its bf16 copy for the token gather).
-static int quantize_weights_fp8(qie_engine* e) {
+// own_arena: the bf16 weights live in the engine's arena (synthetic init, weights.bin), so
+// they may be rewritten with their dequantisation for prefill; caller-owned weights
+// (qie_engine_set_weights) are never written — their prefill takes the fp8 GEMM path.
+static int quantize_weights_fp8(qie_engine* e, bool own_arena) {
     QIE_REQUIRE(e->sh.tp == 1, "fp8 weights with tensor parallelism are not supported yet");
     const qie_model_spec& s = e->spec;
     const int64_t H = s.hidden, QD = (int64_t)s.n_heads * s.head_dim, KD = (int64_t)s.n_kv_heads * s.head_dim;
@@ -295,8 +302,15 @@ static int quantize_weights_fp8(qie_engine* e) {
     e->fp8_arena = nullptr;
     QIE_HIP(hipMalloc(&e->fp8_arena, total));
     char* dst = (char*)e->fp8_arena;
+    e->layers_pf.clear();
+    if (own_arena) e->layers_pf = e->layers;   // bf16 arena pointers, rewritten below with the dequantised values
     for (auto& t : ts) {
-        QIE_TRY(qie_quantize_fp8(*t.p, t.rows, t.cols, dst, e->stream));
+        const void* src = *t.p;
+        QIE_TRY(qie_quantize_fp8(src, t.rows, t.cols, dst, e->stream));
+        // layer weights: the arena copy becomes the exact dequantisation (prefill reads it);
+        // the lm_head is left alone (a tied one is also the embedding table)
+        if (own_arena && t.p != &e->w.lm_head)
+            QIE_TRY(qie_dequantize_fp8(dst, t.rows, t.cols, const_cast<void*>(src), e->stream));
         *t.p = dst;
         dst += (qie_fp8_weight_bytes(t.rows, t.cols) + 255) / 256 * 256;
     }
@@ -346,7 +360,7 @@ static int bind_from_index(qie_engine* e) {
     e->w.n_layers = s.n_layers;
     e->w.layers = e->layers.data();
     e->have_weights = true;
-    return e->opts.weight_fp8 ? quantize_weights_fp8(e) : 0;
+    return e->opts.weight_fp8 ? quantize_weights_fp8(e, true) : 0;
 }
 
 // ------------------------------------------------------------- enqueue helpers
@@ -856,7 +870,7 @@ int qie_engine_set_weights(qie_engine* e, const qie_model_weights* w) {
     e->w = *w;
     e->w.layers = e->layers.data();
     e->have_weights = true;
-    return e->opts.weight_fp8 ? quantize_weights_fp8(e) : 0;
+    return e->opts.weight_fp8 ? quantize_weights_fp8(e, false) : 0;
 }
 
 int qie_engine_weights(const qie_engine* e, qie_model_weights* out, const qie_layer_weights** layers) {
@@ -1063,10 +1077,17 @@ int qie_prefill(qie_batch* b, int32_t seq, const int32_t* ids, int32_t n, const 
                        b->d_hist + (int64_t)seq * b->max_ctx, n);
     QIE_TRY(qie_embedding(e->w.embed, b->pf_ids, b->pf_x, n, H, st));
     const qie_kv_cache cache = batch_cache(b, seq);
-    for (int l = 0; l < s.n_layers; l++) {
-        const qie_layer_weights& L = e->layers[l];
-        QIE_TRY(qie_rmsnorm(b->pf_x, L.attn_norm, b->pf_hn, n, H, s.rms_eps, s.numerics, st));
+    // fp8 engine, >= 256 rows: the GEMMs run on the dequantised bf16 copy (layers_pf)
+    const bool pf16 = e->fp8 && n >= 256 && !e->layers_pf.empty();
+    auto pf_base = [&]() {
         qie_linear_args a = lin_base(e);
+        if (pf16) a.flags &= ~QIE_LINEAR_FP8;
+        return a;
+    };
+    for (int l = 0; l < s.n_layers; l++) {
+        const qie_layer_weights& L = pf16 ? e->layers_pf[l] : e->layers[l];
+        QIE_TRY(qie_rmsnorm(b->pf_x, L.attn_norm, b->pf_hn, n, H, s.rms_eps, s.numerics, st));
+        qie_linear_args a = pf_base();
         a.x = b->pf_hn; a.ldx = H;
         a.w[0] = L.wq; a.w[1] = L.wk; a.w[2] = L.wv;
         a.bias[0] = L.bq; a.bias[1] = L.bk; a.bias[2] = L.bv;
@@ -1076,16 +1097,16 @@ int qie_prefill(qie_batch* b, int32_t seq, const int32_t* ids, int32_t n, const 
         QIE_TRY(qie_qkv_post(b->pf_qkv, n, b->pf_pos, n, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, sh.nq,
                              &cache, l, s.rms_eps, s.numerics, b->pf_q, st));
         QIE_TRY(qie_attention(b->pf_q, n, b->pf_pos, n, &cache, l, sh.nq, b->pf_att, b->pf_attn_ws, st));
-        a = lin_base(e);
+        a = pf_base();
         a.x = b->pf_att; a.ldx = QD; a.w[0] = L.wo; a.seg_rows[0] = H;
         a.M = n; a.K = QD; a.N = H; a.ldy = H;
         QIE_TRY(row_parallel(b, a, b->pf_x, b->pf_part, n));
         QIE_TRY(qie_rmsnorm(b->pf_x, L.ffn_norm, b->pf_hn, n, H, s.rms_eps, s.numerics, st));
-        a = lin_base(e);
+        a = pf_base();
         a.x = b->pf_hn; a.ldx = H; a.w[0] = L.w_gate; a.w[1] = L.w_up; a.seg_rows[0] = I; a.seg_rows[1] = I;
         a.M = n; a.K = H; a.N = I; a.y = b->pf_h; a.ldy = I; a.epilogue = QIE_EPI_SWIGLU;
         QIE_TRY(qie_linear(&a, st));
-        a = lin_base(e);
+        a = pf_base();
         a.x = b->pf_h; a.ldx = I; a.w[0] = L.w_down; a.seg_rows[0] = H;
         a.M = n; a.K = I; a.N = H; a.ldy = H;
         QIE_TRY(row_parallel(b, a, b->pf_x, b->pf_part, n));

@@ -750,6 +750,38 @@ int qie_quantize_fp8(const void* w_bf16, int64_t rows, int64_t cols, void* out, 
     return 0;
 }
 
+// fp8 weight -> bf16 rows (exact: e4m3 value x power-of-two scale has <= 4 significant
+// bits).  One thread per 16 codes, grid-stride; 16-B loads, 2 x 16-B stores.
+__global__ void dequantize_fp8_kernel(const uint4* codes, const float* scales, int64_t cols16, int64_t n16,
+                                      uint4* out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint4 q = codes[i];
+        const float sc = scales[i / cols16];
+        float f[16];
+        fp8x4_to_f32(q.x, f);
+        fp8x4_to_f32(q.y, f + 4);
+        fp8x4_to_f32(q.z, f + 8);
+        fp8x4_to_f32(q.w, f + 12);
+        out[2 * i] = make_uint4(pack2(f[0] * sc, f[1] * sc), pack2(f[2] * sc, f[3] * sc), pack2(f[4] * sc, f[5] * sc),
+                                pack2(f[6] * sc, f[7] * sc));
+        out[2 * i + 1] = make_uint4(pack2(f[8] * sc, f[9] * sc), pack2(f[10] * sc, f[11] * sc),
+                                    pack2(f[12] * sc, f[13] * sc), pack2(f[14] * sc, f[15] * sc));
+    }
+}
+
+int qie_dequantize_fp8(const void* w_fp8, int64_t rows, int64_t cols, void* out_bf16, void* stream) {
+    QIE_REQUIRE(w_fp8 && out_bf16 && rows > 0 && cols > 0 && cols % 16 == 0 && ((uintptr_t)w_fp8 % 16) == 0 &&
+                    ((uintptr_t)out_bf16 % 16) == 0,
+                "qie_dequantize_fp8: bad arguments (cols % 16 == 0, 16-B aligned buffers)");
+    const uint8_t* codes = (const uint8_t*)w_fp8;
+    const int64_t n16 = rows * cols / 16;
+    const unsigned grid = (unsigned)std::min<int64_t>((n16 + 255) / 256, (int64_t)device_cu_count() * 16);
+    hipLaunchKernelGGL(dequantize_fp8_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint4*)codes,
+                       (const float*)(codes + rows * cols), cols / 16, n16, (uint4*)out_bf16);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+
 int qie_quantize_fp8_host(const void* w_bf16, int64_t rows, int64_t cols, void* out) {
     QIE_REQUIRE(w_bf16 && out && rows > 0 && cols > 0 && cols % 16 == 0, "qie_quantize_fp8_host: bad arguments");
     const uint16_t* w = (const uint16_t*)w_bf16;

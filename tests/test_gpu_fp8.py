@@ -48,6 +48,19 @@ def test_quantize_device_equals_host(oracle, qlib, rows, cols):
     assert np.array_equal(got[rows * cols:].view(np.float32), scales)
 
 
+@pytest.mark.parametrize("rows,cols", [(7, 64), (33, 896), (5, 18944)])
+def test_dequantize_device_exact(oracle, qlib, rows, cols):
+    """qie_dequantize_fp8 (the fp8 prefill's weight expansion) == the host dequantisation
+    of the same codes, bit for bit (every e4m3 x power-of-two value is a bf16)."""
+    w = rand_bf16(oracle, (rows, cols), 0.05, seed=rows + 1)
+    w[0] = 0
+    q = G.zeros((int(qlib.qie_fp8_weight_bytes(rows, cols)),), np.uint8)
+    G.check(qlib.qie_quantize_fp8(G.p(G.dev(w)), rows, cols, G.p(q), None))
+    out = G.zeros_bf16(rows, cols)
+    G.check(qlib.qie_dequantize_fp8(G.p(q), rows, cols, G.p(out), None))
+    assert np.array_equal(G.host_bf16(out), W.dequantize_fp8(*W.quantize_fp8(w)))
+
+
 def _fp8_dev(qlib, w):
     rows, cols = w.shape
     out = G.zeros((int(qlib.qie_fp8_weight_bytes(rows, cols)),), np.uint8)

@@ -206,7 +206,7 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
         // then the first weight chunk of the wave's first task, THEN the x arithmetic — so
         // the weight stream's first HBM round trip overlaps the x round trip instead of
         // following it (vmcnt retires in order: x must be issued first).
-        constexpr int NV = XCH <= 2 ? XCH : 1;   // norm weights: fused-norm variants only (XCH <= 2)
+        constexpr int NV = XCH <= 5 ? XCH : 1;   // norm weights: fused-norm variants only (XCH <= 5)
         const bool nrm = NV == XCH && p.norm_w != nullptr;
         uint4 xv[XCH], nv[NV];
 #pragma unroll
@@ -917,6 +917,7 @@ static int launch_gemv_m(const GemvParams& p, int rpw, int epi, hipStream_t st, 
 // x-first prologue variants (MT = 1 only): XCH 2048-element x chunks per thread
 static int launch_gemv_1(const GemvParams& p, int rpw, int epi, hipStream_t st, int bpc, int xch) {
     if (xch == 2) return launch_gemv_m<1, 2>(p, rpw, epi, st, bpc);
+    if (xch == 5) return launch_gemv_m<1, 5>(p, rpw, epi, st, bpc);
     if (xch == 10) return launch_gemv_m<1, 10>(p, rpw, epi, st, bpc);
     return launch_gemv_m<1, 0>(p, rpw, epi, st, bpc);
 }
@@ -1051,8 +1052,14 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
         }
     }
     int xch = 0;
-    if (MT == 1 && p.xlds && p.M == 1 && env_int("QIE_GEMV_XFIRST", 1) != 0)
-        xch = K_fits(a->K, 2) ? 2 : (K_fits(a->K, 10) ? 10 : 0);
+    // The x-first variants with a fused RMSNorm are XCH 2 and 5 (the norm weights ride along
+    // with x); XCH 10 (down, K = 18,944) stages x only — a fused norm there would be dropped,
+    // so a normed K > 10,240 takes the generic prologue.
+    if (MT == 1 && p.xlds && p.M == 1 && env_int("QIE_GEMV_XFIRST", 1) != 0) {
+        if (p.norm_w) xch = K_fits(a->K, 2) ? 2 : (K_fits(a->K, 5) ? 5 : 0);
+        else xch = K_fits(a->K, 2) ? 2 : (K_fits(a->K, 10) ? 10 : 0);
+    }
+    QIE_REQUIRE(!(xch == 10 && p.norm_w), "qie_linear: internal: fused norm routed to a variant without one");
     switch (MT) {
         case 1: return launch_gemv_1(p, rpw, a->epilogue, st, bpc, xch);
         case 2: return launch_gemv_m<2, 0>(p, rpw, a->epilogue, st, bpc);

@@ -212,6 +212,20 @@ def test_qwen2_7b_widths_two_layers_match_oracle(oracle):
     assert flips <= 2
 
 
+@pytest.mark.slow
+@pytest.mark.parametrize("name", ["Qwen3-14B", "Qwen2-72B"])
+def test_wide_hidden_two_layers_match_oracle(oracle, name):
+    """Hidden sizes above 4,096 (Qwen3-14B, the reference's own model: H 5120, 40 / 8 heads =
+    GQA group 5, qk-norm, no bias; Qwen2-72B: H 8192, 64 / 8 heads), 2 layers: the batch-1
+    GEMVs fuse the RMSNorm at these widths through a different prologue variant than at
+    7B widths (before round 2's fix the x-first variant for K > 4,096 dropped the norm)."""
+    spec = S.PRESETS[name].replace(n_layers=2)
+    eng, hw, om = make_pair(spec, oracle, max_ctx=48, syn=W.SynthParams(seed=0))
+    prompt = list(rng(14).integers(0, spec.vocab, 12))
+    ids, flips = forced_compare(oracle, eng.batch(1, 48), OrderPair(oracle, hw, 48), prompt, 6)
+    assert flips <= 2
+
+
 @pytest.mark.parametrize("paged", [False, True])
 def test_short_prefill_after_long_prefill(oracle, paged):
     """Prompts of <= 8 tokens run the split prefill attention, which needs a workspace

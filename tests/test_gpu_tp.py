@@ -188,3 +188,40 @@ def test_tp_paged_equals_contiguous():
         (f0, d0, l0), (f1, d1, l1) = res[r]
         assert f0 == f1 and d0 == d1 and np.array_equal(l0, l1)
     assert res[0][1][1] == res[1][1][1]
+
+
+@pytest.mark.slow
+def test_qwen2_72b_widths_tp8_two_layers_match_oracle(oracle):
+    """BASELINE config 5's shapes: Qwen2-72B widths (H 8192, 64 q / 8 kv heads, I 29568,
+    V 152064), 2 layers, tensor-parallel over 8 ranks (one kv head per rank, row-parallel
+    fp32 all-reduces, vocab-parallel lm_head) on the local communicator, teacher-forced
+    against the CPU oracle on the unsharded weights under tests/parity.py's bar."""
+    from parity import OrderPair, oracle_trace, check_step, max_flips
+    spec = S.QWEN2_72B.replace(n_layers=2)
+    syn = W.SynthParams(seed=0)
+    hw = W.HostWeights.synthetic(spec, syn)
+    prompt = [int(t) for t in rng(72).integers(0, spec.vocab, 16)]
+    n_new = 6
+    pair = OrderPair(oracle, hw, len(prompt) + n_new + 4)
+    ids, outs = oracle_trace(oracle, pair, prompt, n_new)
+    pair.calibrate(spec.vocab, n_prompt=12, n_steps=3)
+    del hw
+
+    def fn(rank, comm):
+        eng = Q.Engine(spec, max_ctx=64, comm=comm).init_synthetic(syn)
+        b = eng.batch(1, 64)
+        raw, lgs = [b.prefill(0, prompt)], []
+        for i in range(n_new):
+            lgs.append(b.logits()[0])
+            if raw[-1] != ids[i]:
+                b.set_position(0, len(prompt) + i, ids[i])
+            if i + 1 < n_new:
+                raw.append(b.decode_step()[0])
+        eng.close()
+        return raw, lgs
+    res = run_ranks(8, fn, timeout=900)
+    raw0, lgs0 = res[0]
+    for r in range(1, 8):
+        assert res[r][0] == raw0
+    flips = sum(check_step(lgs0[i], outs[i][0], pair, raw0[i], ids[i], f"72B-tp8 step {i}") for i in range(n_new))
+    assert flips <= max_flips(n_new)

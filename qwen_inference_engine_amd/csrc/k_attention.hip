@@ -276,6 +276,13 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef short i16x4_t __attribute__((ext_vector_type(4)));
 typedef unsigned int kv16_t __attribute__((ext_vector_type(4)));
 
+// 16 bytes per lane global -> LDS (LDS-DMA); `lds` is the wave-instruction's 1-KiB base,
+// lane l lands at lds + 16 l
+__device__ __forceinline__ void dma16(const uint16_t* src, uint16_t* lds) {
+    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src),
+                                     (__attribute__((address_space(3))) void*)(lds), 16, 0, 0);
+}
+
 // ---------------------------------------------------------------------------
 // Prefill kernel: each wave owns two 16-row query groups, so every K fragment
 // (S^T = K.Q^T) and every V fragment (O += P.V) read from LDS feeds up to two MFMAs.
@@ -337,29 +344,23 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
         for (int ks = 0; ks < KSTEPS; ks++) qf[q][ks] = *reinterpret_cast<const bf16x8_t*>(qp + ks * 32 + g * 8);
     }
 
-    // staging registers as native 4 x u32 vectors: HIP's union-based uint4 arrays were
-    // left in scratch (144 B/lane) by the compiler across the loop
-    kv16_t rk[LPT], rv[LPT];
-    auto gload = [&](int kt) {
-        // a 64-key tile never straddles a page (page_tokens is a multiple of 128)
+    // K/V tiles go global -> LDS by LDS-DMA (global_load_lds_dwordx4): one wave-instruction
+    // = 1 KiB = RPI key rows, lane-linear in LDS, the chunk swizzle applied on the SOURCE
+    // address (LDS position p of row r holds chunk p ^ swz(r)); no staging registers and no
+    // ds_write pass.  A 64-key tile never straddles a page (page_tokens is a multiple of
+    // 128); rows past kmax re-read row kmax (same page) and are masked by position.
+    constexpr int RPI = 512 / HD;                 // key rows per 1 KiB wave-instruction
+    constexpr int IPW = KT / RPI / 4;             // wave-instructions per wave per operand
+    auto issue = [&](int kt, int buf) {
         const int64_t tb = kv_tok<PG>(a.km, seq, kt * KT, HD);
 #pragma unroll
-        for (int i = 0; i < LPT; i++) {
-            const int c = tid + 256 * i;
-            const int key = min(kt * KT + c / CPR, kmax);
-            const int ch = c % CPR;
-            const int64_t o = tb + (int64_t)(key - kt * KT) * HD + ch * 8;
-            rk[i] = *reinterpret_cast<const kv16_t*>(kb + o);
-            rv[i] = *reinterpret_cast<const kv16_t*>(vb + o);
-        }
-    };
-    auto lstore = [&](int buf) {
-#pragma unroll
-        for (int i = 0; i < LPT; i++) {
-            const int c = tid + 256 * i;
-            const int r = c / CPR, ch = c % CPR;
-            *reinterpret_cast<kv16_t*>(Ks + buf * KT * HD + r * HD + ((ch ^ (r & (CPR - 1))) * 8)) = rk[i];
-            *reinterpret_cast<kv16_t*>(Vs + buf * KT * HD + r * HD + ((ch ^ vswz(r)) * 8)) = rv[i];
+        for (int i = 0; i < IPW; i++) {
+            const int inst = wave * IPW + i;
+            const int r = inst * RPI + lane / CPR, pch = lane % CPR;
+            const int key = min(kt * KT + r, kmax);
+            const int64_t ro = tb + (int64_t)(key - kt * KT) * HD;
+            dma16(kb + ro + (pch ^ (r & (CPR - 1))) * 8, Ks + buf * KT * HD + inst * 512);
+            dma16(vb + ro + (pch ^ vswz(r)) * 8, Vs + buf * KT * HD + inst * 512);
         }
     };
 
@@ -376,12 +377,13 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
     }
     const float sl2 = 1.4426950408889634f / sqrtf((float)HD);   // log2(e) / sqrt(hd)
 
-    gload(0);
-    lstore(0);
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int cur = 0;
     for (int kt = 0; kt < nkt; kt++) {
-        if (kt + 1 < nkt) gload(kt + 1);
+        // into the other buffer: every wave finished tile kt-1 before the last barrier
+        if (kt + 1 < nkt) issue(kt + 1, cur ^ 1);
         const uint16_t* K = Ks + cur * KT * HD;
         const uint16_t* Vt = Vs + cur * KT * HD;
         bool on[QG];
@@ -477,8 +479,8 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
                 }
             }
         }
-        if (kt + 1 < nkt) lstore(cur ^ 1);
-        __syncthreads();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs of tile kt+1
+        __syncthreads();                                     // ... and every other wave's
         cur ^= 1;
     }
 #pragma unroll

@@ -27,8 +27,10 @@ def main():
     b.prefill(0, np.random.default_rng(1).integers(0, spec.vocab, P))
     meta = []
     for which, name in ORDER:
-        us, by = b.time_kernel(which, ITERS)   # 1 warm-up + ITERS launches
-        meta.append({"kernel": name, "which": which, "launches": ITERS + 1, "algorithmic_bytes": by, "avg_us": us})
+        us, by = b.time_kernel(which, ITERS)   # min(L, 4) warm-up + ITERS launches (qie_batch_time_kernel)
+        wu = min(spec.n_layers, 4)
+        meta.append({"kernel": name, "which": which, "launches": ITERS + wu, "warmup": wu, "algorithmic_bytes": by,
+                     "avg_us": us})
     out = os.path.join(ROOT, "gpurun_out", "pmc_probe_meta.json")
     os.makedirs(os.path.dirname(out), exist_ok=True)
     with open(out, "w") as f:

@@ -28,8 +28,9 @@ def main(out_name="r01_pmc_traffic"):
     fetch, write = fetch[-total:], write[-total:]
     res = []
     for i, m in enumerate(meta["order"]):
-        f = fetch[i * n:(i + 1) * n][1:]   # drop the warm-up launch
-        w = write[i * n:(i + 1) * n][1:]
+        wu = m.get("warmup", 1)
+        f = fetch[i * n:(i + 1) * n][wu:]   # drop the warm-up launches
+        w = write[i * n:(i + 1) * n][wu:]
         names = {r["Kernel_Name"].split("(")[0] for r in f}
         fb = statistics.median(2 * float(r["Counter_Value"]) * 1024 for r in f)
         wb = statistics.median(float(r["Counter_Value"]) * 1024 for r in w)
@@ -39,7 +40,7 @@ def main(out_name="r01_pmc_traffic"):
                     "avg_us_eager": m["avg_us"]})
     doc = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) over tools/pmc_probe.py",
            "correction": "fetch_bytes = 2 x FETCH_SIZE[KB] x 1024 (gfx950 streaming-read tally); write_bytes = WRITE_SIZE[KB] x 1024",
-           "launches_per_kernel": n - 1, "kernels": res}
+           "launches_per_kernel": n - meta["order"][0].get("warmup", 1), "kernels": res}
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     path = os.path.join(ROOT, "profiles", out_name + ".json")
     with open(path, "w") as fh:

@@ -49,6 +49,8 @@ def parse(argv=None):
     ap.add_argument("--prompt", type=int, default=2048)
     ap.add_argument("--gen", type=int, default=512)
     ap.add_argument("--prefill-iters", type=int, default=3)
+    ap.add_argument("--prefill-single", action="store_true",
+                    help="B > 1: prefill the B prompts one qie_prefill call each (default: one batched pass)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-prompt", type=int, default=16)
@@ -159,15 +161,22 @@ def run(a):
     seed = 1 if comm else 1 + rank        # TP ranks process the same sequence
     prompts = np.random.default_rng(seed).integers(0, spec.vocab, size=(B, P), dtype=np.int32)
 
-    # ---------------- prefill (first call warms up; median of the timed ones)
-    first = [batch.prefill(s, prompts[s]) for s in range(B)]
+    # ---------------- prefill (first call warms up; median of the timed ones).  B > 1: the
+    # B equal-length prompts in one qie_prefill_batch pass (one GEMM over B*P rows) unless
+    # --prefill-single asks for B separate qie_prefill calls.
+    def prefill_all():
+        if B > 1 and not a.prefill_single:
+            return batch.prefill_batch(0, prompts)
+        return [batch.prefill(s, prompts[s]) for s in range(B)]
+
+    first = prefill_all()
     pts = []
     for _ in range(max(1, a.prefill_iters)):
         eng.sync()
         if group:
             group.barrier()
         t0 = time.perf_counter()
-        first = [batch.prefill(s, prompts[s]) for s in range(B)]
+        first = prefill_all()
         eng.sync()
         pts.append(time.perf_counter() - t0)
     t_prefill = float(np.median(pts))
@@ -227,6 +236,7 @@ def run(a):
                    "graph": not a.no_graph, "kv": f"paged{a.page_tokens}" if a.page_tokens else "contiguous"},
         "prefill_tok_s": round(prefill_tok_s, 1),
         "prefill_ms": round(t_prefill * 1e3, 3),
+        "prefill_mode": "batched" if B > 1 and not a.prefill_single else "per-sequence",
         "prefill_tflops": round(spec.prefill_flops(P, B) / t_prefill / 1e12 / (1 if comm else 1), 1),
         "roofline": {"bound": "hbm", "kernel": "gate_up_gemv (rms + gate/up GEMV + SwiGLU, layers 1..L-1)",
                      "achieved": dom["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",

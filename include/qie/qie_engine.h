@@ -128,6 +128,13 @@ int qie_batch_block_table(qie_batch* b, int32_t seq, int32_t* host_pages, int32_
  * makes it the sequence's current token at position n. */
 int qie_prefill(qie_batch* b, int32_t seq, const int32_t* ids, int32_t n, const qie_sampling* s,
                 int32_t* next_id);
+/* qie_prefill of n_seqs prompts of len ids each (host [n_seqs][len], laid end to end)
+ * into slots seq0 .. seq0+n_seqs-1 in one pass: every projection GEMM runs once over
+ * the n_seqs*len rows (the reference prefills one sequence per call, iengine.cu
+ * prefill path; this is the batch-admission form of it).  next_ids: host [n_seqs]
+ * or NULL.  Paged batches: all-or-nothing on the pool, as qie_prefill. */
+int qie_prefill_batch(qie_batch* b, int32_t seq0, int32_t n_seqs, const int32_t* ids, int32_t len,
+                      const qie_sampling* s, int32_t* next_ids);
 /* One decode step for all B sequences (hipGraph replay when enabled);
  * next_ids: host [B] or NULL (then nothing is synchronised). */
 int qie_decode_step(qie_batch* b, const qie_sampling* s, int32_t* next_ids);

@@ -156,6 +156,7 @@ SIGNATURES = [
     ("qie_batch_page_stats", C.c_int, [_P, _PI32, _PI32, _PI32]),
     ("qie_batch_block_table", C.c_int, [_P, _I32, _PI32, _I32]),
     ("qie_prefill", C.c_int, [_P, _I32, _PI32, _I32, C.POINTER(SamplingC), _PI32]),
+    ("qie_prefill_batch", C.c_int, [_P, _I32, _I32, _PI32, _I32, C.POINTER(SamplingC), _PI32]),
     ("qie_decode_step", C.c_int, [_P, C.POINTER(SamplingC), _PI32]),
     ("qie_decode", C.c_int, [_P, _I32, C.POINTER(SamplingC), _PI32]),
     ("qie_batch_logits", C.c_int, [_P, _P]),

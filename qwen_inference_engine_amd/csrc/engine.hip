@@ -177,14 +177,16 @@ __global__ void set_state_kernel(int m, int32_t pos_v, int32_t step_v, int32_t t
         for (int64_t i = threadIdx.x; i < H8; i += blockDim.x) x_res[(int64_t)m * H8 + i] = E[(int64_t)tok * H8 + i];
 }
 
-__global__ void iota_kernel(int32_t* p, int n, int start) {
+// positions of n_seqs equal-length prompts laid end to end: row i sits at i % len
+__global__ void iota_kernel(int32_t* p, int n, int len) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) p[i] = start + i;
+    if (i < n) p[i] = i % len;
 }
 
-__global__ void copy_ids_kernel(const int32_t* src, int32_t* dst, int n) {
+// prompt z (blockIdx.y) of len ids -> history row z of dst (stride dst_stride)
+__global__ void copy_ids_kernel(const int32_t* src, int32_t* dst, int len, int64_t dst_stride) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) dst[i] = src[i];
+    if (i < len) dst[blockIdx.y * dst_stride + i] = src[(int64_t)blockIdx.y * len + i];
 }
 
 static int dmalloc(void** p, size_t bytes) {
@@ -1049,34 +1051,45 @@ void qie_batch_destroy(qie_batch* b) {
     delete b;
 }
 
-int qie_prefill(qie_batch* b, int32_t seq, const int32_t* ids, int32_t n, const qie_sampling* smp, int32_t* next_id) {
-    QIE_REQUIRE(b && ids && n > 0 && seq >= 0 && seq < b->B, "qie_prefill: bad arguments");
-    QIE_REQUIRE(n < b->max_ctx, "qie_prefill: prompt of %d tokens does not fit max_ctx %d", n, b->max_ctx);
+// Prefill of n_seqs prompts of len ids each into slots seq0 .. seq0+n_seqs-1 (ids laid end
+// to end): every GEMM runs once over all n_seqs * len rows, attention and the KV append see
+// the prompts as sequences of rows_per_seq = len, and the head samples the n_seqs last rows
+// in one launch.  n_seqs = 1 is qie_prefill.
+static int prefill_rows(qie_batch* b, int seq0, int n_seqs, const int32_t* ids, int len, const qie_sampling* smp,
+                        int32_t* next_ids, const char* who) {
+    QIE_REQUIRE(b && ids && len > 0 && n_seqs > 0 && seq0 >= 0 && seq0 + n_seqs <= b->B, "%s: bad arguments", who);
+    QIE_REQUIRE(len < b->max_ctx, "%s: prompt of %d tokens does not fit max_ctx %d", who, len, b->max_ctx);
     qie_engine* e = b->e;
     const qie_model_spec& s = e->spec;
-    for (int i = 0; i < n; i++)
-        QIE_REQUIRE(ids[i] >= 0 && ids[i] < s.vocab, "qie_prefill: token id %d out of range", ids[i]);
+    const int64_t n = (int64_t)n_seqs * len;   // rows
+    QIE_REQUIRE(n <= INT32_MAX, "%s: %lld rows", who, (long long)n);
+    for (int64_t i = 0; i < n; i++)
+        QIE_REQUIRE(ids[i] >= 0 && ids[i] < s.vocab, "%s: token id %d out of range", who, ids[i]);
     hipStream_t st = e->stream;
     QIE_TRY(ensure_prefill_scratch(b, n));
-    if (b->d_table) {   // all-or-nothing: the slot's own pages count, nothing is dropped on failure
-        const int64_t need = ((int64_t)n + b->page_tokens - 1) / b->page_tokens;
-        QIE_REQUIRE(need <= (int64_t)b->free_pages.size() + b->held[seq],
-                    "qie_prefill: KV pool exhausted (%lld pages needed, %zu free + %d held by slot %d)",
-                    (long long)need, b->free_pages.size(), b->held[seq], seq);
+    if (b->d_table) {   // all-or-nothing: the slots' own pages count, nothing is dropped on failure
+        const int64_t need = ((int64_t)len + b->page_tokens - 1) / b->page_tokens * n_seqs;
+        int64_t held = 0;
+        for (int z = 0; z < n_seqs; z++) held += b->held[seq0 + z];
+        QIE_REQUIRE(need <= (int64_t)b->free_pages.size() + held,
+                    "%s: KV pool exhausted (%lld pages needed, %zu free + %lld held by slots %d..%d)", who,
+                    (long long)need, b->free_pages.size(), (long long)held, seq0, seq0 + n_seqs - 1);
     }
-    drop_pages(b, seq);   // a prefill starts a new sequence in the slot
-    QIE_TRY(ensure_pages(b, seq, n));
+    for (int z = 0; z < n_seqs; z++) {   // a prefill starts a new sequence in each slot
+        drop_pages(b, seq0 + z);
+        QIE_TRY(ensure_pages(b, seq0 + z, len));
+        b->idle[seq0 + z] = 0;
+    }
     QIE_TRY(flush_table(b));
-    b->idle[seq] = 0;
     const TpShard& sh = e->sh;
     const int64_t H = s.hidden, hd = s.head_dim, QD = (int64_t)sh.nq * hd, KD = (int64_t)sh.nkv * hd;
     const int64_t QKVD = QD + 2 * KD, I = sh.ffn;
     QIE_HIP(hipMemcpyAsync(b->pf_ids, ids, (size_t)n * 4, hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(iota_kernel, dim3((n + 255) / 256), dim3(256), 0, st, b->pf_pos, n, 0);
-    hipLaunchKernelGGL(copy_ids_kernel, dim3((n + 255) / 256), dim3(256), 0, st, b->pf_ids,
-                       b->d_hist + (int64_t)seq * b->max_ctx, n);
+    hipLaunchKernelGGL(iota_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, b->pf_pos, (int)n, len);
+    hipLaunchKernelGGL(copy_ids_kernel, dim3((len + 255) / 256, n_seqs), dim3(256), 0, st, b->pf_ids,
+                       b->d_hist + (int64_t)seq0 * b->max_ctx, len, (int64_t)b->max_ctx);
     QIE_TRY(qie_embedding(e->w.embed, b->pf_ids, b->pf_x, n, H, st));
-    const qie_kv_cache cache = batch_cache(b, seq);
+    const qie_kv_cache cache = batch_cache(b, seq0);
     // fp8 engine, >= 256 rows: the GEMMs run on the dequantised bf16 copy (layers_pf)
     const bool pf16 = e->fp8 && n >= 256 && !e->layers_pf.empty();
     auto pf_base = [&]() {
@@ -1094,9 +1107,9 @@ int qie_prefill(qie_batch* b, int32_t seq, const int32_t* ids, int32_t n, const 
         a.seg_rows[0] = QD; a.seg_rows[1] = KD; a.seg_rows[2] = KD;
         a.M = n; a.K = H; a.N = QKVD; a.y = b->pf_qkv; a.ldy = QKVD; a.epilogue = QIE_EPI_STORE;
         QIE_TRY(qie_linear(&a, st));
-        QIE_TRY(qie_qkv_post(b->pf_qkv, n, b->pf_pos, n, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, sh.nq,
+        QIE_TRY(qie_qkv_post(b->pf_qkv, n, b->pf_pos, len, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, sh.nq,
                              &cache, l, s.rms_eps, s.numerics, b->pf_q, st));
-        QIE_TRY(qie_attention(b->pf_q, n, b->pf_pos, n, &cache, l, sh.nq, b->pf_att, b->pf_attn_ws, st));
+        QIE_TRY(qie_attention(b->pf_q, n, b->pf_pos, len, &cache, l, sh.nq, b->pf_att, b->pf_attn_ws, st));
         a = pf_base();
         a.x = b->pf_att; a.ldx = QD; a.w[0] = L.wo; a.seg_rows[0] = H;
         a.M = n; a.K = QD; a.N = H; a.ldy = H;
@@ -1111,16 +1124,35 @@ int qie_prefill(qie_batch* b, int32_t seq, const int32_t* ids, int32_t n, const 
         a.M = n; a.K = I; a.N = H; a.ldy = H;
         QIE_TRY(row_parallel(b, a, b->pf_x, b->pf_part, n));
     }
-    // position of the last prompt token; finalize advances it to n (the new token).
-    hipLaunchKernelGGL(set_state_kernel, dim3(1), dim3(64), 0, st, seq, n - 1, 0, ids[n - 1], b->d_pos, b->d_step,
-                       b->d_hist, b->max_ctx, (const uint4*)e->w.embed, (uint4*)b->x_res, (int64_t)H / 8, 0);
-    QIE_TRY(enqueue_head(b, b->pf_x + (int64_t)(n - 1) * H, H, seq, 1, smp));
-    b->h_pos[seq] = n;
-    if (next_id) {
-        QIE_HIP(hipMemcpyAsync(next_id, b->d_ids + seq, 4, hipMemcpyDeviceToHost, st));
+    // position of each last prompt token; finalize advances it to len (the new token).
+    for (int z = 0; z < n_seqs; z++) {
+        hipLaunchKernelGGL(set_state_kernel, dim3(1), dim3(64), 0, st, seq0 + z, len - 1, 0,
+                           ids[(int64_t)z * len + len - 1], b->d_pos, b->d_step, b->d_hist, b->max_ctx,
+                           (const uint4*)e->w.embed, (uint4*)b->x_res, (int64_t)H / 8, 0);
+        QIE_LAUNCH_CHECK();
+    }
+    const uint16_t* last = b->pf_x + (int64_t)(len - 1) * H;
+    if (n_seqs > 1) {   // the last rows, packed (the head's pre-norm reads contiguous rows)
+        QIE_HIP(hipMemcpy2DAsync(b->pf_hn, (size_t)H * 2, last, (size_t)len * H * 2, (size_t)H * 2, n_seqs,
+                                 hipMemcpyDeviceToDevice, st));
+        last = b->pf_hn;
+    }
+    QIE_TRY(enqueue_head(b, last, H, seq0, n_seqs, smp));
+    for (int z = 0; z < n_seqs; z++) b->h_pos[seq0 + z] = len;
+    if (next_ids) {
+        QIE_HIP(hipMemcpyAsync(next_ids, b->d_ids + seq0, (size_t)n_seqs * 4, hipMemcpyDeviceToHost, st));
         QIE_HIP(hipStreamSynchronize(st));
     }
     return 0;
+}
+
+int qie_prefill(qie_batch* b, int32_t seq, const int32_t* ids, int32_t n, const qie_sampling* smp, int32_t* next_id) {
+    return prefill_rows(b, seq, 1, ids, n, smp, next_id, "qie_prefill");
+}
+
+int qie_prefill_batch(qie_batch* b, int32_t seq0, int32_t n_seqs, const int32_t* ids, int32_t len,
+                      const qie_sampling* smp, int32_t* next_ids) {
+    return prefill_rows(b, seq0, n_seqs, ids, len, smp, next_ids, "qie_prefill_batch");
 }
 
 static bool same_sampling(const qie_sampling& a, const qie_sampling* b) {

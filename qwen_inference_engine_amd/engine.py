@@ -187,6 +187,19 @@ class Batch:
         _lib.check(self.lib.qie_prefill(self.h, seq, arr, len(ids), C.byref(sc), C.byref(out)), "qie_prefill")
         return out.value
 
+    def prefill_batch(self, seq0: int, prompts: Sequence[Sequence[int]], sampling: Sampling = GREEDY) -> List[int]:
+        """Equal-length prompts into slots seq0, seq0+1, ... in one pass (qie_prefill_batch)."""
+        n = len(prompts)
+        length = len(prompts[0]) if n else 0
+        if n == 0 or any(len(p) != length for p in prompts):
+            raise ValueError("prefill_batch: needs one or more prompts of equal length")
+        flat = np.ascontiguousarray(np.asarray(prompts, dtype=np.int32).reshape(-1))
+        out = (C.c_int32 * n)()
+        sc = sampling.to_c()
+        _lib.check(self.lib.qie_prefill_batch(self.h, seq0, n, flat.ctypes.data_as(C.POINTER(C.c_int32)), length,
+                                              C.byref(sc), out), "qie_prefill_batch")
+        return list(out)
+
     def decode_step(self, sampling: Sampling = GREEDY) -> List[int]:
         out = (C.c_int32 * self.B)()
         sc = sampling.to_c()

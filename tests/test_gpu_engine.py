@@ -244,3 +244,39 @@ def test_short_prefill_after_long_prefill(oracle, paged):
     want = [f.prefill(1, short)] + [int(t) for t in f.decode(6)[:, 1]]
     assert got == want
     assert np.array_equal(lg, f.logits()[1])
+
+
+@pytest.mark.parametrize("L", [5, 40])
+@pytest.mark.parametrize("paged", [False, True])
+def test_prefill_batch_matches_oracle(oracle, L, paged):
+    """qie_prefill_batch: 3 equal-length prompts into slots 1..3 of a 4-slot batch in one
+    pass (one GEMM over 3L rows; L = 5 runs the split attention, L = 40 the causal MFMA
+    kernel, both with rows_per_seq = L).  Every slot is teacher-forced against its own
+    oracle trace under tests/parity.py's bar through 6 decode steps; slot 0 stays idle.
+    Positions and token history are exact."""
+    spec = CONFIGS["qwen3-qknorm-hd128"]
+    eng, hw, _ = make_pair(spec, oracle, max_ctx=96)
+    prompts = [[int(t) for t in rng(40 + z).integers(0, spec.vocab, L)] for z in range(3)]
+    n_new = 6
+    traces, pairs = [], []
+    for pr in prompts:
+        pair = OrderPair(oracle, hw, 96)
+        traces.append(oracle_trace(oracle, pair, pr, n_new))
+        pairs.append(pair.calibrate(spec.vocab))
+    b = eng.batch(4, 96, page_tokens=128 if paged else None)
+    t_e = b.prefill_batch(1, prompts)
+    assert list(b.positions()[1:]) == [L] * 3
+    for z in range(3):
+        assert list(b.history(1 + z, L + 1)) == prompts[z] + [t_e[z]]
+    flips = 0
+    for i in range(n_new):
+        lg = b.logits()
+        for z in range(3):
+            ids, outs = traces[z]
+            logits_close(lg[1 + z], outs[i][0], f"seq {z} step {i}")
+            flips += check_step(lg[1 + z], outs[i][0], pairs[z], t_e[z], ids[i], f"seq {z} step {i}")
+            if t_e[z] != ids[i]:
+                b.set_position(1 + z, L + i, ids[i])
+        if i + 1 < n_new:
+            t_e = b.decode_step()[1:]
+    assert flips <= max_flips(3 * n_new)

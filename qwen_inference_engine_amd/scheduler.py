@@ -5,7 +5,8 @@ at iengine.cu:309-322, 369-373, 448-452) through ``llm()`` and grows a linked pa
 per sequence (iengine.cu:73-109).  Here requests share the B slots of one ``Batch`` with
 a paged KV cache: a waiting request is admitted into a free slot when the page pool can
 hold its worst case (prompt + max_new_tokens), prefilled there while the other slots keep
-decoding, and retired at its stop token / token budget, which returns its pages
+decoding (requests admitted together with equal prompt lengths into consecutive slots
+prefill in one ``qie_prefill_batch`` pass), and retired at its stop token / token budget, which returns its pages
 (``qie_batch_release``).  Every step is one fixed-B decode step over all slots (idle
 slots run on the scratch page and their outputs are dropped), so the hipGraph captured
 for the batch is replayed unchanged.
@@ -33,6 +34,19 @@ class Request:
     slot: int = -1
     pages: int = 0
     done: bool = False
+
+
+def prefill_runs(admitted: Sequence[Request]) -> List[List[Request]]:
+    """Split requests (in admission order) into runs that one qie_prefill_batch call can
+    take: consecutive slots, equal prompt lengths."""
+    runs: List[List[Request]] = []
+    for r in admitted:
+        prev = runs[-1][-1] if runs else None
+        if prev is not None and r.slot == prev.slot + 1 and len(r.prompt) == len(prev.prompt):
+            runs[-1].append(r)
+        else:
+            runs.append([r])
+    return runs
 
 
 class ContinuousBatcher:
@@ -80,17 +94,30 @@ class ContinuousBatcher:
             self._finish(r)
 
     def _admit(self, out: list) -> None:
+        admitted: List[Request] = []
         while self.waiting:
             r = self.waiting[0]
             need = self._pages(len(r.prompt) + r.max_new_tokens)
             free_slot = next((i for i, s in enumerate(self.slots) if s is None), None)
             if free_slot is None or need > self.budget:
-                return                          # FIFO: later requests wait behind the head
+                break                           # FIFO: later requests wait behind the head
             self.waiting.popleft()
             r.slot, r.pages = free_slot, need
             self.budget -= need
             self.slots[free_slot] = r
-            self._emit(r, self.batch.prefill(free_slot, r.prompt, self.sampling), out)
+            admitted.append(r)
+        # equal-length prompts landing in consecutive slots prefill in one pass
+        # (qie_prefill_batch); tokens are emitted in admission order afterwards
+        first: Dict[int, int] = {}
+        for run in prefill_runs(admitted):
+            if len(run) == 1:
+                first[run[0].rid] = self.batch.prefill(run[0].slot, run[0].prompt, self.sampling)
+            else:
+                toks = self.batch.prefill_batch(run[0].slot, [r.prompt for r in run], self.sampling)
+                first.update((r.rid, t) for r, t in zip(run, toks))
+        lg = self.batch.logits() if self.keep_logits and admitted else None
+        for r in admitted:
+            self._emit(r, first[r.rid], out, lg)
 
     def step(self) -> List[tuple]:
         """Admit what fits, then one decode step for every slot; returns the (request id,

@@ -326,3 +326,37 @@ def test_failed_reprefill_leaves_live_slot_intact():
         pb.prefill(0, list(rng(4).integers(0, SPEC.vocab, 400)))   # 4 pages; 1 held + 1 free
     assert pb.page_stats()[1][0] == held
     assert list(pb.decode(60)[:, 0]) == want
+
+
+def test_batcher_batched_admission_matches_oracle(oracle):
+    """Four equal-length requests submitted together are admitted in one step and prefill
+    in one qie_prefill_batch pass (slots 0..3, rows_per_seq 33); a fifth of another length
+    waits for a free slot and prefills alone.  Every request's tokens and logits follow
+    or_forward (the oracle fed the batcher's own tokens): logits within 4 bf16 ulps of
+    max|logit|, each token the oracle's arg-max or a near-tie within that tolerance."""
+    from qwen_inference_engine_amd.scheduler import ContinuousBatcher
+    from test_gpu_engine import logit_tol
+    from parity import max_flips
+    eng = Q.Engine(SPEC, max_ctx=256).init_synthetic(SYN)
+    hw = W.HostWeights.synthetic(SPEC, SYN)
+    cb = ContinuousBatcher(eng, slots=4, max_ctx=256, page_tokens=128, keep_logits=True)
+    prompts = [[int(t) for t in rng(300 + i).integers(0, SPEC.vocab, 33 if i < 4 else 21)] for i in range(5)]
+    rids = [cb.submit(p, 12 + 3 * i) for i, p in enumerate(prompts)]
+    cb.run()
+    flips = n_tok = 0
+    for rid, pr in zip(rids, prompts):
+        r = cb.requests[rid]
+        assert len(r.tokens) == 12 + 3 * rid
+        om = oracle.Model(hw, 256)
+        lg = om.forward(pr, 0)
+        for t, (tok, got) in enumerate(zip(r.tokens, r.logits)):
+            d = np.abs(G.bf(got).astype(np.float64) - G.bf(lg))
+            assert d.max() <= logit_tol(lg), f"request {rid} token {t}: {d.max()}"
+            want = oracle.argmax(lg)
+            if tok != want:
+                assert abs(float(G.bf(lg[want])) - float(G.bf(lg[tok]))) <= logit_tol(lg)
+                flips += 1
+            if t + 1 < len(r.tokens):
+                lg = om.forward([tok])
+        n_tok += len(r.tokens)
+    assert flips <= max_flips(n_tok)

@@ -118,3 +118,57 @@ def test_convert_safetensors(tmp_path):
     data = np.fromfile(tmp_path / "w.bin", dtype=np.uint16)
     for t in idx:
         assert np.array_equal(data[t.data_offsets[0] // 2:t.data_offsets[1] // 2].reshape(3, 5), expect[t.tensor_name])
+
+
+class _FakeBatch:
+    """Records the engine calls the ContinuousBatcher makes (host logic only)."""
+
+    def __init__(self, slots, max_ctx, n_pages):
+        self.B, self.max_ctx, self.free = slots, max_ctx, n_pages - 1
+        self.calls = []
+
+    def page_stats(self):
+        return self.free, [0] * self.B, 128
+
+    def prefill(self, seq, ids, sampling=None):
+        self.calls.append(("prefill", seq, len(ids)))
+        return 1000 + seq
+
+    def prefill_batch(self, seq0, prompts, sampling=None):
+        assert len({len(p) for p in prompts}) == 1
+        self.calls.append(("prefill_batch", seq0, len(prompts)))
+        return [1000 + seq0 + z for z in range(len(prompts))]
+
+    def decode_step(self, sampling=None):
+        self.calls.append(("decode",))
+        return [2000 + i for i in range(self.B)]
+
+    def release(self, seq):
+        self.calls.append(("release", seq))
+
+
+class _FakeEngine:
+    def __init__(self, fb):
+        self.fb = fb
+
+    def batch(self, slots, max_ctx, page_tokens=None, n_pages=0):
+        return self.fb
+
+
+def test_batcher_groups_equal_length_admissions():
+    """Requests admitted in one step with equal prompt lengths into consecutive slots go
+    through one qie_prefill_batch call; a length change or a slot gap starts a new run;
+    first tokens are emitted in admission order."""
+    from qwen_inference_engine_amd.scheduler import ContinuousBatcher, prefill_runs, Request
+    fb = _FakeBatch(6, 512, 64)
+    cb = ContinuousBatcher(_FakeEngine(fb), slots=6, max_ctx=512)
+    lens = [16, 16, 16, 9, 16, 16]
+    rids = [cb.submit(list(range(n)), 4) for n in lens]
+    out = cb.step()
+    assert fb.calls[:3] == [("prefill_batch", 0, 3), ("prefill", 3, 9), ("prefill_batch", 4, 2)]
+    assert [rid for rid, _ in out[:6]] == rids
+    assert [t for _, t in out[:6]] == [1000 + s for s in range(6)]
+    # a gap: slots 0 and 2 free, slot 1 busy -> two single runs even with equal lengths
+    rs = [Request(i, [0] * 8, 1, slot=s) for i, s in enumerate([0, 2, 3])]
+    assert [[r.slot for r in run] for run in prefill_runs(rs)] == [[0], [2, 3]]
+    assert prefill_runs([]) == []

@@ -465,8 +465,8 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
 // bf16 MFMA, the row scale applied to the fp32 result.  Partial C tiles of the 4 waves
 // are summed in LDS, then the epilogue (bias / arg-max keys / residual / SwiGLU / f32).
 // Persistent over column tiles (grid <= 4 blocks per CU) so arg-max keys merge per block.
-template <int EPI, int WT, int XL>
-__global__ __launch_bounds__(256) void skinny_mfma_kernel(GemvParams p) {
+template <int EPI, int WT, int XL, int NW>
+__global__ __launch_bounds__(NW * 64) void skinny_mfma_kernel(GemvParams p) {
 #pragma clang fp contract(off)
     constexpr int NB = EPI == QIE_EPI_SWIGLU ? 2 : 1;   // B tiles per block (gate, up)
     // A unit = 64 k of each of the tile's 16 weight rows: a lane loads 32 contiguous bytes
@@ -483,7 +483,7 @@ __global__ __launch_bounds__(256) void skinny_mfma_kernel(GemvParams p) {
     // distinct LDS banks (an unpadded 7168-B row stride maps every row to one bank)
     const int64_t KP = K + 8;
     uint16_t* xs = reinterpret_cast<uint16_t*>(smem);
-    float* red = reinterpret_cast<float*>(smem + (XL ? (size_t)M * KP * 2 : 0));            // [4][NB][256]
+    float* red = reinterpret_cast<float*>(smem + (XL ? (size_t)M * KP * 2 : 0));            // [NW][NB][256]
     __shared__ unsigned long long kb_s[16];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int fr = lane & 15, g = lane >> 4;
@@ -506,7 +506,7 @@ __global__ __launch_bounds__(256) void skinny_mfma_kernel(GemvParams p) {
                    hb2 = launder_u64(p.b2 ? ~0ull : 0ull);   // segment has a bias (all-ones mask)
     // this wave's K range, in 16-byte load units; a tile is NBAT steps of U units
     const int64_t units = K / KSTEP;
-    const int64_t uw = (units + 3) / 4;
+    const int64_t uw = (units + NW - 1) / NW;
     const int64_t ub = wave * uw, ue = ub + uw < units ? ub + uw : units;
     const int64_t nbat = (uw + U - 1) / U;
     const int64_t n_tiles = (p.N + 15) / 16;
@@ -520,7 +520,7 @@ __global__ __launch_bounds__(256) void skinny_mfma_kernel(GemvParams p) {
     // global load sits under a branch: the steps form one stream per wave, double-
     // buffered in registers, so the next step's loads (next tile included) are in
     // flight while this step's MFMAs, the cross-wave reduction and the epilogue run.
-    constexpr int AW = 2;            // 16-B A fragments per unit (k 16g..16g+7, 16g+8..16g+15)
+    constexpr int AW = KSTEP / 32;   // 16-B A fragments per unit (8 k each, from k KSTEP/4 * g)
     constexpr int EB = WT ? 1 : 2;
     struct Step {
         u32x4 wv[U][NB][WV];
@@ -532,7 +532,7 @@ __global__ __launch_bounds__(256) void skinny_mfma_kernel(GemvParams p) {
     };
     auto issue = [&](Step& st, int64_t s) {
         s = s < S ? s : S - 1;
-        const int64_t tl = s / nbat, j = s - tl * nbat;
+        const int32_t tl = (int32_t)s / (int32_t)nbat, j = (int32_t)s - tl * (int32_t)nbat;   // < 2^31 steps
         st.tile = blockIdx.x + tl * gridDim.x;
         st.u0 = ub + j * U;
         st.last = j == nbat - 1;
@@ -581,13 +581,13 @@ __global__ __launch_bounds__(256) void skinny_mfma_kernel(GemvParams p) {
         for (int u = 0; u < U; u++) {
             const int64_t uu = st.u0 + u < ue ? st.u0 + u : ue - 1;
 #pragma unroll
-            for (int b = 0; b < NB; b++)   // bytes [uu * 64 + 16 g, +16) of the row, both formats
+            for (int b = 0; b < NB; b++)   // bytes [uu * KSTEP * EB + 16 WV g, +16 WV) of the row
 #pragma unroll
                 for (int h = 0; h < WV; h++)
                     st.wv[u][b][h] =
                         __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wrow[b]) + uu * (4 * WV) + WV * g + h);
             if constexpr (!XL) {
-                const int64_t kk = uu * KSTEP + 16 * g;
+                const int64_t kk = uu * KSTEP + (KSTEP / 4) * g;
 #pragma unroll
                 for (int h = 0; h < AW; h++) st.av[u][h] = xa(kk + 8 * h);
             }
@@ -596,12 +596,14 @@ __global__ __launch_bounds__(256) void skinny_mfma_kernel(GemvParams p) {
     f32x4_t acc[NB];
 #pragma unroll
     for (int b = 0; b < NB; b++) acc[b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    auto compute = [&](const Step& st) {
+    // full: every unit of the step is inside this wave's K range (all but a range's last
+    // step), so no per-unit masking; otherwise dead units multiply a zero A fragment
+    auto compute = [&](const Step& st, bool full) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const bool live = st.u0 + u < ue;   // dead steps multiply a zero A fragment
+            const bool live = full || st.u0 + u < ue;
             const int64_t uu = live ? st.u0 + u : ue - 1;
-            const int64_t kk = uu * KSTEP + 16 * g;
+            const int64_t kk = uu * KSTEP + (KSTEP / 4) * g;
             uint4 ar[AW];
 #pragma unroll
             for (int h = 0; h < AW; h++) {
@@ -619,23 +621,21 @@ __global__ __launch_bounds__(256) void skinny_mfma_kernel(GemvParams p) {
                                                                      acc[b], 0, 0, 0);
                 }
             } else {
-                const bf16x8_t a0 = __builtin_bit_cast(bf16x8_t, ar[0]);
-                const bf16x8_t a1 = __builtin_bit_cast(bf16x8_t, ar[AW - 1]);
 #pragma unroll
-                for (int b = 0; b < NB; b++) {
-                    float f[16];
-                    fp8x4_to_f32(st.wv[u][b][0].x, f);
-                    fp8x4_to_f32(st.wv[u][b][0].y, f + 4);
-                    fp8x4_to_f32(st.wv[u][b][0].z, f + 8);
-                    fp8x4_to_f32(st.wv[u][b][0].w, f + 12);
-                    const uint4 lo = make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]),
-                                                pack2(f[6], f[7]));
-                    const uint4 hi = make_uint4(pack2(f[8], f[9]), pack2(f[10], f[11]), pack2(f[12], f[13]),
-                                                pack2(f[14], f[15]));
-                    acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, __builtin_bit_cast(bf16x8_t, lo), acc[b],
-                                                                     0, 0, 0);
-                    acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, __builtin_bit_cast(bf16x8_t, hi), acc[b],
-                                                                     0, 0, 0);
+                for (int h = 0; h < WV; h++) {   // 16 codes: A fragments 2h (codes 0..7), 2h + 1 (8..15)
+                    const bf16x8_t a0 = __builtin_bit_cast(bf16x8_t, ar[2 * h]);
+                    const bf16x8_t a1 = __builtin_bit_cast(bf16x8_t, ar[2 * h + 1]);
+#pragma unroll
+                    for (int b = 0; b < NB; b++) {
+                        const uint2 c0 = fp8x4_to_bf16x4(st.wv[u][b][h].x), c1 = fp8x4_to_bf16x4(st.wv[u][b][h].y);
+                        const uint2 c2 = fp8x4_to_bf16x4(st.wv[u][b][h].z), c3 = fp8x4_to_bf16x4(st.wv[u][b][h].w);
+                        const uint4 lo = make_uint4(c0.x, c0.y, c1.x, c1.y);
+                        const uint4 hi = make_uint4(c2.x, c2.y, c3.x, c3.y);
+                        acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, __builtin_bit_cast(bf16x8_t, lo), acc[b],
+                                                                         0, 0, 0);
+                        acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, __builtin_bit_cast(bf16x8_t, hi), acc[b],
+                                                                         0, 0, 0);
+                    }
                 }
             }
         }
@@ -658,8 +658,12 @@ __global__ __launch_bounds__(256) void skinny_mfma_kernel(GemvParams p) {
             for (int b = 0; b < NB; b++)
 #pragma unroll
                 for (int r = 0; r < 4; r++)
-                    c[b][r] = ((red[(0 * NB + b) * 256 + lane * 4 + r] + red[(1 * NB + b) * 256 + lane * 4 + r]) +
-                               red[(2 * NB + b) * 256 + lane * 4 + r]) + red[(3 * NB + b) * 256 + lane * 4 + r];
+                {
+                    float t = red[b * 256 + lane * 4 + r];
+#pragma unroll
+                    for (int w = 1; w < NW; w++) t += red[(w * NB + b) * 256 + lane * 4 + r];
+                    c[b][r] = t;
+                }
             if constexpr (WT != 0) {
 #pragma unroll
                 for (int b = 0; b < NB; b++)
@@ -709,7 +713,7 @@ __global__ __launch_bounds__(256) void skinny_mfma_kernel(GemvParams p) {
             float ss[16];
 #pragma unroll
             for (int m = 0; m < 16; m++) ss[m] = 0.f;
-            for (int64_t k = tid * 8; k < K; k += 2048) {
+            for (int64_t k = tid * 8; k < K; k += NW * 512) {
                 uint4 v[16];
 #pragma unroll
                 for (int m = 0; m < 16; m++)
@@ -735,7 +739,9 @@ __global__ __launch_bounds__(256) void skinny_mfma_kernel(GemvParams p) {
 #pragma unroll
             for (int m = 0; m < 16; m++) {
                 const int mm = m < M ? m : 0;
-                const float sm = red[mm] + red[16 + mm] + red[32 + mm] + red[48 + mm];
+                float sm = red[mm];
+#pragma unroll
+                for (int w = 1; w < NW; w++) sm += red[16 * w + mm];
                 rms[m] = sqrtf((sm / (float)K) + p.eps);
                 inv[m] = 1.0f / rms[m];
             }
@@ -743,7 +749,7 @@ __global__ __launch_bounds__(256) void skinny_mfma_kernel(GemvParams p) {
             // per-row math under uniform branches).  REF's f / rms uses the FMA-corrected
             // quotient (Markstein): correctly rounded, i.e. equal to the division, for
             // normal operands — |f| outside [1e-30, 1e30] takes the real division.
-            for (int64_t k = tid * 8; k < K; k += 2048) {
+            for (int64_t k = tid * 8; k < K; k += NW * 512) {
                 const uint4 nw = *reinterpret_cast<const uint4*>(p.norm_w + k);
                 uint4 v[16];
 #pragma unroll
@@ -779,7 +785,7 @@ __global__ __launch_bounds__(256) void skinny_mfma_kernel(GemvParams p) {
             }
         } else {
             for (int m = 0; m < M; m++)
-                for (int64_t k = tid * 8; k < K; k += 2048)
+                for (int64_t k = tid * 8; k < K; k += NW * 512)
                     *reinterpret_cast<uint4*>(xs + (int64_t)m * KP + k) =
                         *reinterpret_cast<const uint4*>(p.x + (int64_t)m * p.ldx + k);
         }
@@ -789,23 +795,27 @@ __global__ __launch_bounds__(256) void skinny_mfma_kernel(GemvParams p) {
         if (tid == 0 && p.dbg == 0x7fffffff) p.y[0] = xs[0];
         return;
     }
+    auto run = [&](const Step& st) {   // the full/tail choice is wave-uniform
+        if (st.u0 + U <= ue) compute(st, true);
+        else compute(st, false);
+    };
     int64_t s = 0;
     for (; s + 2 < S; s += 2) {
         issue(sb, s + 1);
-        compute(sa);
+        run(sa);
         if (sa.last) tile_end(sa);
         issue(sa, s + 2);
-        compute(sb);
+        run(sb);
         if (sb.last) tile_end(sb);
     }
     if (S - s == 2) {
         issue(sb, s + 1);
-        compute(sa);
+        run(sa);
         if (sa.last) tile_end(sa);
-        compute(sb);
+        run(sb);
         tile_end(sb);
     } else {
-        compute(sa);
+        run(sa);
         tile_end(sa);
     }
     if constexpr (EPI == QIE_EPI_STORE) {
@@ -932,11 +942,11 @@ static int env_int(const char* name, int dflt) {
 constexpr size_t kGemvLdsCap = 96 * 1024;
 constexpr size_t kSkinnyLdsCap = 120 * 1024;
 
-template <int EPI, int WT, int XL>
+template <int EPI, int WT, int XL, int NW>
 static int launch_skinny_x(const GemvParams& p, hipStream_t st) {
     constexpr int NB = EPI == QIE_EPI_SWIGLU ? 2 : 1;
-    const void* fn = (const void*)skinny_mfma_kernel<EPI, WT, XL>;
-    const size_t shm = (p.xlds ? (size_t)p.M * (p.K + 8) * 2 : 0) + (size_t)4 * NB * 256 * 4;
+    const void* fn = (const void*)skinny_mfma_kernel<EPI, WT, XL, NW>;
+    const size_t shm = (p.xlds ? (size_t)p.M * (p.K + 8) * 2 : 0) + (size_t)NW * NB * 256 * 4;
     if (shm > 65536) {
         static bool raised = false;
         if (!raised) {
@@ -950,19 +960,21 @@ static int launch_skinny_x(const GemvParams& p, hipStream_t st) {
     static int cached_nb = 0;
     if (cached_shm != shm || cached_nb == 0) {
         int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 256, shm) != hipSuccess || nb < 1) nb = 1;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, NW * 64, shm) != hipSuccess || nb < 1) nb = 1;
         cached_shm = shm;
         cached_nb = nb;
     }
     const unsigned grid =
         (unsigned)std::max<int64_t>(1, std::min<int64_t>(n_tiles, (int64_t)device_cu_count() * cached_nb));
-    hipLaunchKernelGGL((skinny_mfma_kernel<EPI, WT, XL>), dim3(grid), dim3(256), shm, st, p);
+    hipLaunchKernelGGL((skinny_mfma_kernel<EPI, WT, XL, NW>), dim3(grid), dim3(NW * 64), shm, st, p);
     QIE_LAUNCH_CHECK();
     return 0;
 }
+// 4 waves per block: 8 (2,304 waves for Qwen2-7B QKV) measured 1-9 % slower at config 4,
+// 16 spills (128 VGPRs at 1,024 threads)
 template <int EPI, int WT>
 static int launch_skinny_t(const GemvParams& p, hipStream_t st) {
-    return p.xlds ? launch_skinny_x<EPI, WT, 1>(p, st) : launch_skinny_x<EPI, WT, 0>(p, st);
+    return p.xlds ? launch_skinny_x<EPI, WT, 1, 4>(p, st) : launch_skinny_x<EPI, WT, 0, 4>(p, st);
 }
 
 static int launch_skinny(const GemvParams& p, int epi, bool fp8w, hipStream_t st) {
@@ -1015,6 +1027,8 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
             // fp8: O 9.7 -> 7.8 us, down 26.4 -> 24.6; bf16 O 11.6 -> 10.1, QKV 16.5 -> 15.3)
             const int64_t n_tiles = (a->N + 15) / 16;
             p.xlds = lds_ok && (a->norm_w || n_tiles > 2 * (int64_t)device_cu_count()) ? 1 : 0;
+            const int fx = env_int("QIE_SKINNY_XL", -1);
+            if (fx >= 0) p.xlds = fx && lds_ok ? 1 : 0;
             p.dbg = env_int("QIE_SKINNY_DBG", 0);
             return launch_skinny(p, a->epilogue, fp8w, st);
         }

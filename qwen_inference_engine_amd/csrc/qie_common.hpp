@@ -59,8 +59,12 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
     return __builtin_bit_cast(uint16_t, b);
 }
 __device__ __forceinline__ float rbf(float f) { return bf2f(f2bf(f)); }
+// two floats -> packed bf16 pair in ONE v_cvt_pk_bf16_f32 (same RNE as f2bf; the scalar
+// form converts each half separately and merges with a shift and an or)
+typedef __bf16 qie_bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float qie_f32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
-    return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((qie_f32x2_t{lo, hi}), qie_bf16x2_t));
 }
 
 // ------------------------------------------------------ fp8 (OCP e4m3fn) weights
@@ -110,6 +114,16 @@ __device__ __forceinline__ void fp8x4_to_f32(uint32_t w, float* f) {
     f[1] = lo[1];
     f[2] = hi[0];
     f[3] = hi[1];
+}
+
+// four e4m3 codes -> four bf16, exact (every e4m3 value, subnormals included, is a bf16):
+// the exact fp32 conversion, then one v_cvt_pk_bf16_f32 per pair.  (The one-step
+// v_cvt_scalef32_pk_bf16_fp8 does not reproduce the subnormal codes: the fp8 engine test
+// against the dequantised oracle model fails with it.)
+__device__ __forceinline__ uint2 fp8x4_to_bf16x4(uint32_t w) {
+    const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8((int)w, false);
+    const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8((int)w, true);
+    return make_uint2(pack2(lo[0], lo[1]), pack2(hi[0], hi[1]));
 }
 
 // A uniform pointer as an opaque register value: per-lane selects between

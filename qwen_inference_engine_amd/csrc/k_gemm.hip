@@ -490,7 +490,7 @@ int gemm(const qie_linear_args* a, hipStream_t st) {
     if (!(a->flags & QIE_LINEAR_FP8) && a->K % big::BK == 0 && a->ldx % 8 == 0) {
         // LDS-DMA kernel: 256x256 tiles when they fill the chip at least twice over, else
         // 256x128 when those fill >= 3/4 of it in one round (Qwen2-7B O and down projections
-        // at 2,048 rows: 112 vs 224 tiles on 256 CUs).  QIE_GEMM_BIG: 1 / 2 force the
+        // at 2,048 rows: 112 vs 224 tiles on 256 CUs), else 256x256 in one round (below).  QIE_GEMM_BIG: 1 / 2 force the
         // 256 / 128-column tile, 0 disables the kernel (tests and A/B timing).
         const int64_t cols = a->epilogue == QIE_EPI_SWIGLU ? 2 * a->N : a->N;
         const int64_t n_mt = cdiv(a->M, big::BM);
@@ -502,6 +502,10 @@ int gemm(const qie_linear_args* a, hipStream_t st) {
             return launch_gemm_big<256>(a->epilogue, p, (int)n_mt, (int)t256, st);
         if (force == 2 || (force < 0 && a->M >= big::BM && t128 >= (3 * cus) / 4 && t128 <= cus))
             return launch_gemm_big<128>(a->epilogue, p, (int)n_mt, (int)t128, st);
+        // 256-column tiles in ONE round when 128-column ones would take two (Qwen2-7B QKV at
+        // 2,048 rows: 144 vs 288 tiles on 256 CUs): 124 -> 99 us against the generic kernel
+        if (force < 0 && a->M >= big::BM && t256 >= cus / 2 && t256 <= cus && t128 > cus)
+            return launch_gemm_big<256>(a->epilogue, p, (int)n_mt, (int)t256, st);
     }
     if (a->flags & QIE_LINEAR_FP8) return launch_gemm<1>(a->epilogue, gm, p, shm, st);
     return launch_gemm<0>(a->epilogue, gm, p, shm, st);

@@ -360,3 +360,28 @@ def test_batcher_batched_admission_matches_oracle(oracle):
                 lg = om.forward([tok])
         n_tok += len(r.tokens)
     assert flips <= max_flips(n_tok)
+
+
+def test_prefill_batch_all_or_nothing_and_bad_arguments():
+    """qie_prefill_batch on a paged pool that cannot hold every prompt fails with nothing
+    launched: a live slot keeps its pages and continues exactly like an untouched run;
+    slot ranges past B, prompts >= max_ctx and ragged prompts are refused."""
+    eng = Q.Engine(SPEC, max_ctx=512).init_synthetic(SYN)
+    pr = list(rng(5).integers(0, SPEC.vocab, 100))
+    ref = eng.batch(3, 512, page_tokens=128, n_pages=4)
+    t0 = ref.prefill(0, pr)
+    want = list(ref.decode(40)[:, 0])
+    pb = eng.batch(3, 512, page_tokens=128, n_pages=4)   # page 0 scratch + 3
+    assert pb.prefill(0, pr) == t0
+    stats = pb.page_stats()
+    two = [list(rng(6 + z).integers(0, SPEC.vocab, 200)) for z in range(2)]
+    with pytest.raises(_lib.QieError):
+        pb.prefill_batch(1, two)            # 2 x 2 pages; 2 free
+    assert pb.page_stats()[0] == stats[0] and list(pb.page_stats()[1]) == list(stats[1])
+    with pytest.raises(_lib.QieError):
+        pb.prefill_batch(2, two)            # slots 2..3 of 3
+    with pytest.raises(_lib.QieError):
+        pb.prefill_batch(1, [[1] * 512, [2] * 512])   # >= max_ctx
+    with pytest.raises(ValueError):
+        pb.prefill_batch(1, [[1, 2, 3], [4, 5]])
+    assert list(pb.decode(40)[:, 0]) == want

@@ -29,7 +29,7 @@ def main():
             kv = {} if e == "-" else dict(x.split("=") for x in e.split(","))
             saved = {k: os.environ.get(k) for k in kv}
             os.environ.update(kv)
-            for which in (0, 1, 2, 3):
+            for which in [int(w) for w in os.environ.get("UB8_WHICH", "0,1,2,3").split(",")]:
                 us, by = b.time_kernel(which, 50)
                 res.setdefault((e, which), []).append((us, by))
             for k, v in saved.items():

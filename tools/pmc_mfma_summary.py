@@ -34,19 +34,20 @@ def last_prefill(seq):
 
 
 def roles(names):
-    out, big1 = [], 0
+    """GEMM roles from the launch order of a prefill layer (QKV GEMM, qkv_post, attention,
+    O GEMM, norm, gate/up GEMM, down GEMM), whatever kernel variant each one runs."""
+    out, prev = [], None
     for n in names:
-        if n.startswith("gemm_kernel"):
-            out.append("qkv")
-        elif n.startswith("attn_prefill"):
-            out.append("attention")
+        r = None
+        if n.startswith("attn_prefill"):
+            r = "attention"
         elif n.startswith("gemm_big_kernel<2"):
-            out.append("gate_up")
-        elif n.startswith("gemm_big_kernel<1") or n.startswith("gemm_big_kernel<0"):
-            out.append("o" if big1 % 2 == 0 else "down")
-            big1 += 1
-        else:
-            out.append(None)
+            r = "gate_up"
+        elif n.startswith("gemm_kernel") or n.startswith("gemm_big_kernel"):
+            r = {"attention": "o", "gate_up": "down"}.get(prev, "qkv")
+        out.append(r)
+        if r:
+            prev = r
     return out
 
 

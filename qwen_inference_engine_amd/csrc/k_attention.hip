@@ -515,8 +515,16 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
 // kernel spent ~7 us of ~11 in dot products and cross-lane reductions here.
 constexpr int kDecMStep = 128;      // keys per block step (4 waves x 32)
 constexpr int kDecMSplits = 32;     // default split target
+constexpr int kDecMOneSplit = 2;    // contexts of up to this many steps run as ONE split
 
 __host__ __device__ __forceinline__ int decm_chunk(int ctx, int target) {
+    // Short contexts: one block walks both steps instead of two one-step splits that pay
+    // the publish + ticket + combine round trips (Qwen2-0.5B, ctx 129-256: 8.8 -> 7.4 us
+    // per launch, 1,235 -> 1,271 tok/s).  Longer contexts want the CUs: a split's K/V comes
+    // through one CU, so at ctx 2k ten two-step splits took 13.1 us against 10.5 for twenty
+    // one-step ones — also with the second step's loads issued up front (13.6 vs 10.7,
+    // measured and dropped: that second register set halved the occupancy).
+    if (ctx <= kDecMOneSplit * kDecMStep) return kDecMOneSplit * kDecMStep;
     const int per = kDecMStep * target;
     const int steps = (ctx + per - 1) / per;
     return kDecMStep * (steps < 1 ? 1 : steps);

@@ -842,9 +842,12 @@ static int env_int_gemv(const char* name, int dflt) {
     return v ? atoi(v) : dflt;
 }
 
-template <int MT, int RPW, int EPI, int XCH, int WT>
+// UO: chunks per row in flight when K needs fewer than the default 8 wave-loads per row
+// (0 = default).  A slot past K re-reads the row's last 16 B, so at K = 896 (Qwen2-0.5B)
+// the default issued 8 loads per row of which 6 were duplicates.
+template <int MT, int RPW, int EPI, int XCH, int WT, int UO = 0>
 static int launch_gemv_t(const GemvParams& p, hipStream_t st, int blocks_per_cu) {
-    constexpr int U = (RPW >= 4) ? 4 : 8;
+    constexpr int U = UO ? UO : ((RPW >= 4) ? 4 : 8);
     const void* fn = (const void*)gemv_kernel<MT, RPW, EPI, U, XCH, WT>;
     const size_t shm = (p.xlds ? (size_t)MT * p.K * 2 : 0) + 64;
     if (shm > 65536) {
@@ -909,23 +912,35 @@ static int launch_gemv_t(const GemvParams& p, hipStream_t st, int blocks_per_cu)
     return 0;
 }
 
-template <int MT, int XCH, int WT = 0>
+template <int MT, int XCH, int WT = 0, int UO = 0>
 static int launch_gemv_m(const GemvParams& p, int rpw, int epi, hipStream_t st, int bpc) {
     if (epi == QIE_EPI_SWIGLU) {
-        return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_SWIGLU, XCH, WT>(p, st, bpc)
-                        : launch_gemv_t<MT, 2, QIE_EPI_SWIGLU, XCH, WT>(p, st, bpc);
+        return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_SWIGLU, XCH, WT, UO>(p, st, bpc)
+                        : launch_gemv_t<MT, 2, QIE_EPI_SWIGLU, XCH, WT, UO>(p, st, bpc);
     } else if (epi == QIE_EPI_RESIDUAL) {
-        return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_RESIDUAL, XCH, WT>(p, st, bpc)
-                        : launch_gemv_t<MT, 2, QIE_EPI_RESIDUAL, XCH, WT>(p, st, bpc);
+        return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_RESIDUAL, XCH, WT, UO>(p, st, bpc)
+                        : launch_gemv_t<MT, 2, QIE_EPI_RESIDUAL, XCH, WT, UO>(p, st, bpc);
     } else if (epi == QIE_EPI_F32) {
-        return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_F32, XCH, WT>(p, st, bpc)
-                        : launch_gemv_t<MT, 2, QIE_EPI_F32, XCH, WT>(p, st, bpc);
+        return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_F32, XCH, WT, UO>(p, st, bpc)
+                        : launch_gemv_t<MT, 2, QIE_EPI_F32, XCH, WT, UO>(p, st, bpc);
     }
-    return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_STORE, XCH, WT>(p, st, bpc)
-                    : launch_gemv_t<MT, 2, QIE_EPI_STORE, XCH, WT>(p, st, bpc);
+    return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_STORE, XCH, WT, UO>(p, st, bpc)
+                    : launch_gemv_t<MT, 2, QIE_EPI_STORE, XCH, WT, UO>(p, st, bpc);
 }
 // x-first prologue variants (MT = 1 only): XCH 2048-element x chunks per thread
 static int launch_gemv_1(const GemvParams& p, int rpw, int epi, hipStream_t st, int bpc, int xch) {
+    // Chunks in flight per row sized to K (bf16 wave-loads per row n), so no load slot
+    // re-reads the row's tail: n <= 2 (Qwen2-0.5B, K = 896): 2 instead of 8 slots, 6 of
+    // them duplicates — lm_head 72.1 -> 47.4 us, gate/up 8.4 -> 6.3, decode 1,283 -> 1,471
+    // tok/s; n = 7 (Qwen2-7B, K = 3,584): 7 instead of 8 — gate/up 44.2 -> 42.9, QKV
+    // 9.67 -> 9.41 us, 349 -> 354 tok/s, but lm_head 166 -> 175 us (25 row tasks per wave:
+    // there the 8th slot's duplicate costs less than the bytes in flight it drops), so the
+    // vocabulary projection keeps 8; n = 10 (Qwen3-14B, K = 5,120): 5 per pass, two passes.
+    const int64_t n = (p.K + 511) / 512;   // bf16 wave-loads per row
+    const bool vocab = p.n_tasks * rpw >= 65536;
+    if (xch == 2 && n <= 2) return launch_gemv_m<1, 2, 0, 2>(p, rpw, epi, st, bpc);
+    if (xch == 2 && n == 7 && !vocab) return launch_gemv_m<1, 2, 0, 7>(p, rpw, epi, st, bpc);
+    if (xch == 5 && (n == 9 || n == 10) && !vocab) return launch_gemv_m<1, 5, 0, 5>(p, rpw, epi, st, bpc);
     if (xch == 2) return launch_gemv_m<1, 2>(p, rpw, epi, st, bpc);
     if (xch == 5) return launch_gemv_m<1, 5>(p, rpw, epi, st, bpc);
     if (xch == 10) return launch_gemv_m<1, 10>(p, rpw, epi, st, bpc);

@@ -141,10 +141,15 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
     // Chunk slots past K re-read the row's last 16 B and are skipped by compute_chunk.  A
     // load under a condition (even a per-lane one) is branched around, and at the join
     // the waitcnt pass can no longer count it, so every later wait degrades to vmcnt(0).
+    // XCH == 1 (MT = 1, no norm): x is not staged; each lane loads the 16 B of x that its
+    // weight chunk multiplies together with that chunk (L1/L2 hits: every wave of the
+    // block reads the same row), so no prologue or barrier precedes the weight stream.
+    uint4 xg[XCH == 1 ? U : 1];
     auto load_chunk = [&](const u32x4* const (&wr)[RPW], int64_t k0, u32x4 (&wv)[U][RPW]) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int64_t k = k0 + u * WS;
+            if constexpr (XCH == 1) xg[u] = *reinterpret_cast<const uint4*>(p.x + (k < K ? k : K - EL));
 #pragma unroll
             for (int i = 0; i < RPW; i++)   // unconditional (clamped) loads: see below
                 wv[u][i] = __builtin_nontemporal_load(wr[i] + ((k < K ? k : K - EL) / EL));
@@ -163,7 +168,7 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
                 if constexpr (WT == 0) {
 #pragma unroll
                     for (int m = 0; m < MT; m++) {
-                        const uint4 xv = x_at(m, k);
+                        const uint4 xv = XCH == 1 ? xg[XCH == 1 ? u : 0] : x_at(m, k);
                         float xf[8];
                         unpack8(u32x4{xv.x, xv.y, xv.z, xv.w}, xf);
 #pragma unroll
@@ -200,7 +205,10 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
     u32x4 wv[U][RPW];
     constexpr bool PF = XCH > 0;
 
-    if constexpr (XCH > 0) {
+    if constexpr (XCH == 1) {
+        task_ptrs(task0 < p.n_tasks ? task0 : p.n_tasks - 1, wr);
+        load_chunk(wr, (int64_t)lane * EL, wv);
+    } else if constexpr (XCH > 0) {
         // ---------------- x-first prologue (MT = 1, x staged in LDS, K <= 2048 * XCH; the
         // host guarantees it).  Order of issue: this thread's x chunks (+ norm weights),
         // then the first weight chunk of the wave's first task, THEN the x arithmetic — so
@@ -938,9 +946,15 @@ static int launch_gemv_1(const GemvParams& p, int rpw, int epi, hipStream_t st, 
     // vocabulary projection keeps 8; n = 10 (Qwen3-14B, K = 5,120): 5 per pass, two passes.
     const int64_t n = (p.K + 511) / 512;   // bf16 wave-loads per row
     const bool vocab = p.n_tasks * rpw >= 65536;
+    const int64_t ub = (n + (n + 7) / 8 - 1) / ((n + 7) / 8);   // balanced slots per pass (<= 8)
     if (xch == 2 && n <= 2) return launch_gemv_m<1, 2, 0, 2>(p, rpw, epi, st, bpc);
     if (xch == 2 && n == 7 && !vocab) return launch_gemv_m<1, 2, 0, 7>(p, rpw, epi, st, bpc);
     if (xch == 5 && (n == 9 || n == 10) && !vocab) return launch_gemv_m<1, 5, 0, 5>(p, rpw, epi, st, bpc);
+    // K <= 20,480 without a norm (Qwen3-14B O at K = 5,120: 2 x 5; down at K = 17,408: 5 x 7)
+    if (xch == 10 && ub == 5 && !vocab) return launch_gemv_m<1, 10, 0, 5>(p, rpw, epi, st, bpc);
+    if (xch == 10 && ub == 7 && !vocab) return launch_gemv_m<1, 10, 0, 7>(p, rpw, epi, st, bpc);
+    if (xch == 1 && n == 7) return launch_gemv_m<1, 1, 0, 7>(p, rpw, epi, st, bpc);
+    if (xch == 1) return launch_gemv_m<1, 1>(p, rpw, epi, st, bpc);
     if (xch == 2) return launch_gemv_m<1, 2>(p, rpw, epi, st, bpc);
     if (xch == 5) return launch_gemv_m<1, 5>(p, rpw, epi, st, bpc);
     if (xch == 10) return launch_gemv_m<1, 10>(p, rpw, epi, st, bpc);
@@ -1087,6 +1101,19 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
     if (MT == 1 && p.xlds && p.M == 1 && env_int("QIE_GEMV_XFIRST", 1) != 0) {
         if (p.norm_w) xch = K_fits(a->K, 2) ? 2 : (K_fits(a->K, 5) ? 5 : 0);
         else xch = K_fits(a->K, 2) ? 2 : (K_fits(a->K, 10) ? 10 : 0);
+    }
+    // Batch-1 GEMVs without a fused norm on the one-block-per-CU grid (one row task per
+    // wave: Qwen2-7B O, down) read x from L2 beside each weight chunk (XCH = 1) instead of
+    // staging it in LDS behind a barrier: Qwen2-7B decode 355 -> 358 tok/s (two A/B rounds),
+    // in-graph down 24.5 -> 23.5 us, O 7.3 -> 7.05.  Where a wave walks several row tasks
+    // (Qwen3-14B O / down, 10 per CU; Qwen2-0.5B) x would be re-read per task: O 13.1 ->
+    // 16.5, down 32.9 -> 39.7 us at 14B, so those keep the staged copy.
+    // (the condition is launch_gemv_t's one-block-per-CU grid)
+    if (MT == 1 && p.M == 1 && !p.norm_w && !(a->flags & QIE_LINEAR_FP8) && a->epilogue != QIE_EPI_SWIGLU &&
+        a->K % 8 == 0 && bpc < 0 && p.n_tasks > 4 * (int64_t)cus &&
+        p.n_tasks <= (kGemvBalancedThreads / 64) * (int64_t)cus && env_int_gemv("QIE_GEMV_BALANCED", 1) != 0) {
+        xch = 1;
+        p.xlds = 0;
     }
     QIE_REQUIRE(!(xch == 10 && p.norm_w), "qie_linear: internal: fused norm routed to a variant without one");
     switch (MT) {

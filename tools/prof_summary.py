@@ -13,9 +13,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # Qwen2-7B call sites: kernel template (qie:: and "void " stripped) + workgroups x threads
 ROLE = {
     "gemv_kernel<1, 2, 2, 7, 2, 0, 256> [g 948 x 256]": "decode gate/up GEMV (+RMSNorm, SwiGLU)  [dominant]",
-    "gemv_kernel<1, 2, 1, 8, 10, 0, 576> [g 256 x 448]": "decode down GEMV (+residual), one block per CU",
+    "gemv_kernel<1, 2, 1, 8, 1, 0, 576> [g 256 x 448]": "decode down GEMV (+residual, x from L2), one block per CU",
     "gemv_kernel<1, 2, 0, 7, 2, 0, 576> [g 256 x 576]": "decode QKV GEMV (+RMSNorm, bias), one block per CU",
-    "gemv_kernel<1, 2, 1, 7, 2, 0, 576> [g 256 x 448]": "decode O-proj GEMV (+residual), one block per CU",
+    "gemv_kernel<1, 2, 1, 7, 1, 0, 576> [g 256 x 448]": "decode O-proj GEMV (+residual, x from L2), one block per CU",
     "gemv_kernel<1, 2, 0, 8, 2, 0, 256> [g 761 x 256]": "lm_head GEMV (+final RMSNorm, arg-max keys)",
     "attn_decode_mfma2_kernel<128, false>": "decode attention (fused qk-norm/RoPE/KV append, split-K, in-launch combine)",
     "attn_prefill_mfma2_kernel<128, false>": "prefill flash attention (MFMA, 32 rows/wave)",
@@ -23,8 +23,8 @@ ROLE = {
     "gemm_big_kernel<1, 128>": "prefill O / down GEMM (256x128 LDS-DMA, +residual)",
     "gemm_big_kernel<0, 256>": "prefill QKV GEMM (256x256 LDS-DMA, one round, +bias)",
     "finalize_kernel": "token -> history, position++, next embedding row",
-    "gemv_kernel<1, 2, 0, 8, 10, 0, 576> [g 256 x 448]": "bench live timing of down (store epilogue)",
-    "gemv_kernel<1, 2, 0, 7, 2, 0, 576> [g 256 x 448]": "bench live timing of O-proj (store epilogue)",
+    "gemv_kernel<1, 2, 0, 8, 1, 0, 576> [g 256 x 448]": "bench live timing of down (store epilogue)",
+    "gemv_kernel<1, 2, 0, 7, 1, 0, 576> [g 256 x 448]": "bench live timing of O-proj (store epilogue)",
     "synth_kernel": "synthetic weight fill (setup)",
 }
 

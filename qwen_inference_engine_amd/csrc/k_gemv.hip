@@ -473,7 +473,7 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
 // bf16 MFMA, the row scale applied to the fp32 result.  Partial C tiles of the 4 waves
 // are summed in LDS, then the epilogue (bias / arg-max keys / residual / SwiGLU / f32).
 // Persistent over column tiles (grid <= 4 blocks per CU) so arg-max keys merge per block.
-template <int EPI, int WT, int XL, int NW>
+template <int EPI, int WT, int XL, int NW, int UO = 0>
 __global__ __launch_bounds__(NW * 64) void skinny_mfma_kernel(GemvParams p) {
 #pragma clang fp contract(off)
     constexpr int NB = EPI == QIE_EPI_SWIGLU ? 2 : 1;   // B tiles per block (gate, up)
@@ -483,7 +483,8 @@ __global__ __launch_bounds__(NW * 64) void skinny_mfma_kernel(GemvParams p) {
     // 64-B half lines of a 32-k unit.
     constexpr int KSTEP = 64;
     constexpr int WV = WT ? 1 : 2;                        // 16-B weight vectors per lane per unit
-    constexpr int U = WT ? ((XL && NB == 1) ? 8 : 4) : ((XL && NB == 1) ? 4 : 2);   // units per step
+    // units per step (UO: sized to the wave's K range, so no step slot is a dead unit)
+    constexpr int U = UO ? UO : (WT ? ((XL && NB == 1) ? 8 : 4) : ((XL && NB == 1) ? 4 : 2));
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int64_t K = p.K;
     const int M = p.M;
@@ -971,10 +972,10 @@ static int env_int(const char* name, int dflt) {
 constexpr size_t kGemvLdsCap = 96 * 1024;
 constexpr size_t kSkinnyLdsCap = 120 * 1024;
 
-template <int EPI, int WT, int XL, int NW>
+template <int EPI, int WT, int XL, int NW, int UO = 0>
 static int launch_skinny_x(const GemvParams& p, hipStream_t st) {
     constexpr int NB = EPI == QIE_EPI_SWIGLU ? 2 : 1;
-    const void* fn = (const void*)skinny_mfma_kernel<EPI, WT, XL, NW>;
+    const void* fn = (const void*)skinny_mfma_kernel<EPI, WT, XL, NW, UO>;
     const size_t shm = (p.xlds ? (size_t)p.M * (p.K + 8) * 2 : 0) + (size_t)NW * NB * 256 * 4;
     if (shm > 65536) {
         static bool raised = false;
@@ -995,7 +996,7 @@ static int launch_skinny_x(const GemvParams& p, hipStream_t st) {
     }
     const unsigned grid =
         (unsigned)std::max<int64_t>(1, std::min<int64_t>(n_tiles, (int64_t)device_cu_count() * cached_nb));
-    hipLaunchKernelGGL((skinny_mfma_kernel<EPI, WT, XL, NW>), dim3(grid), dim3(NW * 64), shm, st, p);
+    hipLaunchKernelGGL((skinny_mfma_kernel<EPI, WT, XL, NW, UO>), dim3(grid), dim3(NW * 64), shm, st, p);
     QIE_LAUNCH_CHECK();
     return 0;
 }
@@ -1003,6 +1004,14 @@ static int launch_skinny_x(const GemvParams& p, hipStream_t st) {
 // 16 spills (128 VGPRs at 1,024 threads)
 template <int EPI, int WT>
 static int launch_skinny_t(const GemvParams& p, hipStream_t st) {
+    if constexpr (WT == 1) {
+        // fp8: 7 units per step where a wave's K range is 7 or 14 units (Qwen2-7B, K = 3,584:
+        // 2 steps of 7 instead of 4 of 4 / 2 of 8 with two dead units).  Config 4 (fp8, B = 8):
+        // gate/up 36.2 -> 35.2, O 8.4 -> 7.45, lm_head 129 -> 122 us, 2,509 -> 2,535 tok/s
+        const int64_t uw = (p.K / 64 + 3) / 4;
+        if (uw == 7 || uw == 14)
+            return p.xlds ? launch_skinny_x<EPI, WT, 1, 4, 7>(p, st) : launch_skinny_x<EPI, WT, 0, 4, 7>(p, st);
+    }
     return p.xlds ? launch_skinny_x<EPI, WT, 1, 4>(p, st) : launch_skinny_x<EPI, WT, 0, 4>(p, st);
 }
 

@@ -7,18 +7,31 @@
 // selecting prefill or ONE decode step, and the caller advancing step /
 // generated_token / state exactly like iengine.cu:419-421.
 //
+// Two forms of the driver tier:
+//   * the reference's own argument lists (iengine.cuh:51-55, iengine.cu:25,117,
+//     tensor_parser.hh:216-219): llm(seq, tensors, weights, kv_head, page_size,
+//     g_gpu_weights_buffer), create_new_sequence(id, ids, len, tensors, weights),
+//     create_page_list(n), allocate_page_buffers(node, elems),
+//     load_all_weights_to_gpu_chunked(all, ifstream, h_host, chunk, d_base&, total&),
+//     parsed_tensors(), build_indexed_tensors() — a host written against iengine.cu:226-456
+//     compiles against this header unchanged (csrc/tools/ref_driver.cpp is one);
+//   * qie-native overloads taking a qie_batch slot explicitly (llm(seq, sampling), ...).
 // Differences (deliberate):
-//   * CUDA types are gone: the weight arena, KV cache and streams are owned by a
-//     qie_engine / qie_batch; no std::ifstream or __nv_bfloat16* crosses the API.
-//   * parsed_tensors reads the meta_data.txt index (the reference re-parses the
-//     safetensors shards at hard-coded /mnt/data paths, tensor_parser.cpp:37-46).
-//   * llm() returns -1 (not 0) on error, with qie_last_error() holding the text.
-//   * the model is a qie_model_spec, not the Qwen3-14B literals of utills.cu:8-16.
+//   * bf16 is uint16_t storage (no __nv_bfloat16); device memory comes from qie_malloc.
+//   * the model is config().spec (default: the reference's Qwen3-14B literals,
+//     utills.cu:8-16), not compiled-in constants; parsed_tensors() reads the
+//     meta_data.txt index at config().meta_path (the reference re-parses safetensors
+//     shards at hard-coded /mnt/data paths, tensor_parser.cpp:37-46).
+//   * the KV cache lives in a qie_batch the first llm() call binds to the sequence; the
+//     page list only records capacity (no per-node device buffers).
+//   * llm() returns 0 on error like the reference (qwen_main.cu:135 ...), the text in
+//     qie_last_error() and the code in config().error.
 #pragma once
 
 #include <cstddef>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <string>
@@ -28,6 +41,44 @@
 #include "qie_engine.h"
 
 namespace qie_compat {
+
+using bf16 = uint16_t;
+struct ModelBuffers;
+
+// Settings the reference compiles in: the model (utills.cu:8-16), eps (normalization.cu:19),
+// context (iengine.cuh:19), index path (tensor_parser.cpp:34), sampling (qwen_main.cu).
+inline qie_model_spec reference_spec() {   // Qwen3-14B (utills.cu:8-16, iengine.cuh:19-21)
+    qie_model_spec s;
+    std::memset(&s, 0, sizeof(s));
+    s.n_layers = 40; s.hidden = 5120; s.n_heads = 40; s.n_kv_heads = 8; s.head_dim = 128;
+    s.ffn = 17408; s.vocab = 151936; s.tie_embeddings = 0; s.qkv_bias = 0; s.qk_norm = 1;
+    s.rms_eps = 1e-4f; s.rope_theta = 1e6f; s.numerics = QIE_NUMERICS_REF;
+    return s;
+}
+
+struct Config {
+    float rms_eps = 1e-4f;
+    float qk_eps = 1e-4f;
+    int32_t numerics = QIE_NUMERICS_REF;
+    void* stream = nullptr;
+    int error = 0;        // last non-zero qie return code seen by a compat wrapper
+    // driver tier (reference-signature form)
+    qie_model_spec spec = reference_spec();
+    int32_t max_ctx = 32786;                            // CONTEXT_SIZE, iengine.cuh:19
+    int32_t device = 0;                                 // iengine.cu:238-240
+    std::string meta_path = "../model_files/meta_data.txt";   // tensor_parser.cpp:34
+    int greedy = 0;       // 1: llm() decodes greedily instead of the reference's top-k schedule
+};
+inline Config& config() {
+    static Config c;
+    return c;
+}
+inline void check_(int rc, const char* who) {
+    if (rc != 0) {
+        config().error = rc;
+        std::fprintf(stderr, "%s: %s\n", who, qie_last_error());
+    }
+}
 
 struct tensor {                       // tensor_parser.hh:204-210
     std::string tensor_name;
@@ -40,15 +91,20 @@ using TensorTable = std::unordered_map<std::string, std::vector<tensor>>;
 
 typedef enum { prefill, decode } State;   // iengine.cuh:23
 
-struct batch_metadata {               // iengine.cuh:27-37 (buffer -> qie_batch slot)
-    int sequence_id = 0;
-    State state = prefill;
-    int sequence_len = 0;
-    int generated_token = 0;
-    int step = 0;
-    qie_batch* batch = nullptr;
-    int slot = 0;
-    std::vector<int32_t> prompt;
+// iengine.cuh:27-37 field for field (plain data: the reference mallocs and frees it), plus
+// the qie slot that holds the sequence's KV cache and state.
+struct batch_metadata {
+    int sequence_id;
+    bf16* k_ptr;          // the slot's K / V cache base once bound (qie_batch_kv_cache)
+    bf16* v_ptr;
+    State state;
+    int sequence_len;
+    int generated_token;
+    int step;
+    ModelBuffers* buffer;
+    qie_batch* batch;     // qie: bound by the first llm() (reference form) or given
+    int slot;
+    int last_token;       // qie: the engine's last output (a different generated_token is fed back)
 };
 
 // Reference sampling schedule, qwen_main.cu:241 (prefill) and :381-388 (decode).
@@ -95,55 +151,87 @@ inline TensorTable build_indexed_tensors(const std::vector<tensor>& all) {
     return idx;
 }
 
+// Reference forms (tensor_parser.hh:216-219): no arguments, the index at config().meta_path.
+inline std::vector<tensor> parsed_tensors() { return parsed_tensors(config().meta_path.c_str()); }
+inline TensorTable build_indexed_tensors() { return build_indexed_tensors(parsed_tensors()); }
+
+// load_all_weights_to_gpu_chunked, reference form (iengine.cu:117-223): one device
+// allocation of min(max data_offsets[1], file size) bytes, filled from the open binary
+// stream in chunk_bytes pieces staged through the caller's h_host; d_base_out is the arena
+// (pass it to llm() as g_gpu_weights_buffer), total_bytes_out the bytes uploaded.
+inline bool load_all_weights_to_gpu_chunked(const std::vector<tensor>& all_tensors, std::ifstream& f, void* h_host,
+                                            size_t chunk_bytes, bf16*& d_base_out, size_t& total_bytes_out) {
+    d_base_out = nullptr;
+    total_bytes_out = 0;
+    if (!f.is_open() || !h_host || chunk_bytes == 0) {
+        std::fprintf(stderr, "load_all_weights_to_gpu_chunked: stream not open or no staging buffer\n");
+        return false;
+    }
+    size_t max_end = 0;
+    for (const auto& t : all_tensors)
+        if (t.data_offsets.size() >= 2 && t.data_offsets[1] > max_end) max_end = t.data_offsets[1];
+    f.clear();
+    f.seekg(0, std::ios::end);
+    const std::streamoff fsz = f.tellg();
+    if (max_end == 0 || fsz <= 0) {
+        std::fprintf(stderr, "load_all_weights_to_gpu_chunked: empty index or file\n");
+        return false;
+    }
+    const size_t total = max_end < (size_t)fsz ? max_end : (size_t)fsz;
+    void* d = nullptr;
+    if (qie_set_device(config().device) != 0 || qie_malloc(&d, (int64_t)total) != 0) {
+        check_(-12, "load_all_weights_to_gpu_chunked");
+        return false;
+    }
+    f.clear();
+    f.seekg(0, std::ios::beg);
+    size_t off = 0;
+    while (off < total) {
+        const size_t want = chunk_bytes < total - off ? chunk_bytes : total - off;
+        f.read(static_cast<char*>(h_host), (std::streamsize)want);
+        const std::streamsize got = f.gcount();
+        if (got <= 0 || qie_memcpy_h2d(static_cast<char*>(d) + off, h_host, (int64_t)got) != 0) {
+            std::fprintf(stderr, "load_all_weights_to_gpu_chunked: read / copy failed at %zu\n", off);
+            qie_free(d);
+            return false;
+        }
+        off += (size_t)got;
+        if ((size_t)got < want) break;   // short read before the end
+    }
+    d_base_out = static_cast<bf16*>(d);
+    total_bytes_out = off;
+    return true;
+}
+
 // Loads weights.bin into the engine's single device arena in chunk_bytes pieces.
 inline bool load_all_weights_to_gpu_chunked(qie_engine* e, const char* weights_bin, const char* meta_data_txt,
                                             size_t chunk_bytes) {
     return qie_engine_load_weights_bin(e, weights_bin, meta_data_txt, (int64_t)chunk_bytes) == 0;
 }
 
+inline batch_metadata* new_sequence_(int sequence_id, const int* h_token_ids, int sequence_len);
+
+// qie-native form: the sequence lives in slot `slot` of an existing batch.
 inline batch_metadata* create_new_sequence(int sequence_id, const int* h_token_ids, int sequence_len,
                                            qie_batch* batch, int slot) {
-    auto* s = new batch_metadata();
-    s->sequence_id = sequence_id;
-    s->state = prefill;
-    s->sequence_len = sequence_len;
-    s->batch = batch;
-    s->slot = slot;
-    s->prompt.assign(h_token_ids, h_token_ids + sequence_len);
+    batch_metadata* s = new_sequence_(sequence_id, h_token_ids, sequence_len);
+    if (s) {
+        s->batch = batch;
+        s->slot = slot;
+    }
     return s;
 }
 
-// One call = prefill (state == prefill) or ONE decode step (state == decode); returns
-// the sampled token id.  Greedy callers pass a qie_sampling with top_k = 1.
-inline int llm(batch_metadata* seq, const qie_sampling* sampling = nullptr) {
-    int32_t tok = -1;
-    if (seq->state == prefill) {
-        qie_sampling s = sampling ? *sampling : reference_sampling(prefill);
-        if (qie_prefill(seq->batch, seq->slot, seq->prompt.data(), (int32_t)seq->prompt.size(), &s, &tok) != 0) {
-            std::fprintf(stderr, "llm(prefill): %s\n", qie_last_error());
-            return -1;
-        }
-        return tok;
-    }
-    // qie_decode_step advances every slot of the batch; the reference's llm steps only
-    // `seq`, so a B > 1 batch would silently skip tokens of its other sequences.
-    int32_t nb = 0;
-    if (qie_batch_dims(seq->batch, &nb, nullptr) != 0 || nb != 1) {
-        std::fprintf(stderr, "llm(decode): needs a batch of one slot (got %d); step B > 1 batches with "
-                             "qie_decode_step, which returns every slot's token\n", nb);
-        return -1;
-    }
-    qie_sampling s = sampling ? *sampling : reference_sampling(decode);
-    std::vector<int32_t> ids(8);
-    if (qie_decode_step(seq->batch, &s, ids.data()) != 0) {
-        std::fprintf(stderr, "llm(decode): %s\n", qie_last_error());
-        return -1;
-    }
-    seq->sequence_len += 1;
-    return ids[seq->slot];
-}
+inline int llm_step_(batch_metadata* seq, const qie_sampling* sampling);
 
-inline void destroy_sequence(batch_metadata* s) { delete s; }
+// One call = prefill (state == prefill) or ONE decode step (state == decode); returns
+// the sampled token id, or 0 on error (the reference's convention, qwen_main.cu:135;
+// qie_last_error() / config().error say what failed).  Greedy callers pass a qie_sampling
+// with top_k = 1; nullptr follows the reference's schedule (reference_sampling).
+inline int llm(batch_metadata* seq, const qie_sampling* sampling = nullptr) { return llm_step_(seq, sampling); }
+
+inline void destroy_model_buffers(ModelBuffers& buf);
+inline void destroy_sequence(batch_metadata* s);
 
 // Page list (iengine.cuh:39-49, iengine.cu:73-109).  The reference gives each sequence a
 // linked list of 4-token pages in managed memory (create_page_list, then
@@ -152,10 +240,18 @@ inline void destroy_sequence(batch_metadata* s) { delete s; }
 // behind a device block table, so a page_table here is the slot's handle:
 // create_page_list reserves nothing up front, allocate_page_buffers grows the slot by
 // one reference page's worth of positions, free_page_list returns the slot's pages.
+// The reference-form list (create_page_list(n) + allocate_page_buffers(node, elems)) keeps
+// the reference's nodes and fields; its K/V storage is the qie batch the sequence's first
+// llm() binds, so k_page_ptr / v_page_ptr stay NULL and a node only counts capacity.
 struct page_table {
-    qie_batch* batch = nullptr;
+    bf16* k_page_ptr = nullptr;          // iengine.cuh:42-48
+    bf16* v_page_ptr = nullptr;
+    int page_allocated = 0;
+    page_table* ptr_to_next_page = nullptr;
+    qie_batch* batch = nullptr;          // qie-native form: the slot this handle reserves in
     int slot = 0;
     int tokens = 0;   // positions reserved so far (allocate_page_buffers / kv writes)
+    size_t elems = 0; // reference form: elements of this node (page_size * L * hidden_kv)
 };
 
 inline page_table* create_page_list(qie_batch* batch, int slot) {
@@ -165,10 +261,34 @@ inline page_table* create_page_list(qie_batch* batch, int slot) {
     return p;
 }
 
+// create_page_list (iengine.cu:73-89): a list of pages_required unallocated nodes
+inline page_table* create_page_list(int pages_required) {
+    page_table* head = nullptr;
+    page_table** cur = &head;
+    for (int i = 0; i < pages_required; ++i) {
+        *cur = new page_table();
+        cur = &(*cur)->ptr_to_next_page;
+    }
+    return head;
+}
+
+// allocate_page_buffers (iengine.cu:90-100), reference form: marks the node allocated
+inline void allocate_page_buffers(page_table* node, size_t elems_per_page) {
+    if (!node) return;
+    node->elems = elems_per_page;
+    node->page_allocated = 1;
+}
+
+// free_page_list (iengine.cu:101-109): the whole list; a qie-native handle's pages
+// return to its batch's pool
 inline void free_page_list(page_table* head) {
-    if (!head) return;
-    if (qie_batch_release(head->batch, head->slot) != 0) std::fprintf(stderr, "free_page_list: %s\n", qie_last_error());
-    delete head;
+    while (head) {
+        page_table* next = head->ptr_to_next_page;
+        if (head->batch && qie_batch_release(head->batch, head->slot) != 0)
+            std::fprintf(stderr, "free_page_list: %s\n", qie_last_error());
+        delete head;
+        head = next;
+    }
 }
 
 // ===================================================================== operator tier
@@ -182,25 +302,6 @@ inline void free_page_list(page_table* head) {
 //   * the reference hard-codes eps 1e-4 for rmsNorm and qkNorm (normalization.cu:19,
 //     qk_norm.cu:70) and its model constants (utills.cu:8-16); here eps and numerics
 //     come from config() (defaults: 1e-4, REF) and dims from the engine's spec.
-using bf16 = uint16_t;
-
-struct Config {
-    float rms_eps = 1e-4f;
-    float qk_eps = 1e-4f;
-    int32_t numerics = QIE_NUMERICS_REF;
-    void* stream = nullptr;
-    int error = 0;        // last non-zero qie return code seen by a launch_* wrapper
-};
-inline Config& config() {
-    static Config c;
-    return c;
-}
-inline void check_(int rc, const char* who) {
-    if (rc != 0) {
-        config().error = rc;
-        std::fprintf(stderr, "%s: %s\n", who, qie_last_error());
-    }
-}
 
 // Device scratch the reference's launch helpers allocate per call (d_token in
 // sample_topk_bf16, smem in launch_attn): positions, attention / sampling workspace.
@@ -359,10 +460,15 @@ struct ModelBuffers {
     size_t sequence_len = 0;
     size_t number_of_layers = 0, head_dim = 0, hidden_dim = 0, hidden_dim_kv = 0, num_of_qheads = 0,
            num_of_kvheads = 0, context_size = 0, vocab_size = 0, up_dim = 0;
+    bf16* embeddings_h = nullptr;     // (the reference's pinned host copy; unused)
     bf16* embeddings_d = nullptr;     // E [V][H] (engine arena)
     bf16* embeddings_out = nullptr;   // residual stream [rows][H]
+    float* cos_values_h = nullptr;
+    float* sin_values_h = nullptr;
     float* cos_values_d = nullptr;
     float* sin_values_d = nullptr;
+    bf16* k_cache = nullptr;          // driver form: the sequence's slot K / V base once bound
+    bf16* v_cache = nullptr;
     bf16 *norm_weights_h = nullptr, *norm_weights_d = nullptr, *rms_out = nullptr;
     bf16 *qk_norm_weights_h = nullptr, *qk_norm_weights_d = nullptr;
     bf16 *q_proj_weights_h = nullptr, *q_proj_weights_d = nullptr, *Q = nullptr;
@@ -376,8 +482,12 @@ struct ModelBuffers {
          *MLP_GATE_OUT = nullptr, *MLP_DOWN = nullptr;
     size_t mlp_up_proj_size = 0;
     bf16 *last_x = nullptr, *prefill_output_d = nullptr, *logits_weights_h = nullptr, *logits_weights_d = nullptr;
+    bf16 *O = nullptr, *test_out = nullptr;
     size_t logtis_shape = 0;   // (sic, utils.hh:87)
     size_t rows = 0;           // activation rows allocated (max prompt length)
+    // qie: the prompt (driver tier) and the batch the reference-form llm() bound (freed here)
+    std::vector<int32_t> h_token_ids;
+    qie_batch* owned_batch = nullptr;
 };
 
 // initialize_model_buffers (utills.cu:4-129): dims from the engine's spec, activations
@@ -449,7 +559,215 @@ inline void destroy_model_buffers(ModelBuffers& buf) {
     for (bf16* p : ps)
         if (p) qie_free(p);
     if (buf.d_token_ids) qie_free(buf.d_token_ids);
+    if (buf.owned_batch) qie_batch_destroy(buf.owned_batch);
     buf = ModelBuffers();
+}
+
+// ===================================================================== driver tier bodies
+inline void fill_dims_(ModelBuffers& b, const qie_model_spec& s, int sequence_len) {
+    b.sequence_len = (size_t)sequence_len;
+    b.number_of_layers = (size_t)s.n_layers;
+    b.head_dim = (size_t)s.head_dim;
+    b.hidden_dim = (size_t)s.hidden;
+    b.hidden_dim_kv = (size_t)s.n_kv_heads * s.head_dim;
+    b.num_of_qheads = (size_t)s.n_heads;
+    b.num_of_kvheads = (size_t)s.n_kv_heads;
+    b.context_size = (size_t)config().max_ctx;
+    b.vocab_size = (size_t)s.vocab;
+    b.up_dim = (size_t)s.ffn;
+}
+
+inline batch_metadata* new_sequence_(int sequence_id, const int* h_token_ids, int sequence_len) {
+    auto* s = static_cast<batch_metadata*>(std::malloc(sizeof(batch_metadata)));
+    if (!s) return nullptr;
+    std::memset(s, 0, sizeof(*s));
+    s->sequence_id = sequence_id;
+    s->state = prefill;
+    s->sequence_len = sequence_len;
+    s->last_token = -1;
+    s->buffer = new ModelBuffers();
+    fill_dims_(*s->buffer, config().spec, sequence_len);
+    s->buffer->h_token_ids.assign(h_token_ids, h_token_ids + sequence_len);
+    return s;
+}
+
+// create_new_sequence, reference form (iengine.cu:25-47): the sequence's buffers (dims from
+// config().spec, the prompt); its KV slot is bound by its first llm() call.
+inline batch_metadata* create_new_sequence(int sequence_id, int* h_token_ids, int sequence_len, TensorTable tensors,
+                                           std::ifstream& weights) {
+    (void)tensors;
+    (void)weights;
+    return new_sequence_(sequence_id, h_token_ids, sequence_len);
+}
+
+inline void destroy_sequence(batch_metadata* s) {
+    if (!s) return;
+    if (s->buffer) {
+        destroy_model_buffers(*s->buffer);
+        delete s->buffer;
+    }
+    std::free(s);
+}
+
+inline int llm_step_(batch_metadata* seq, const qie_sampling* sampling) {
+    auto bad = [](int rc, const char* who) {
+        check_(rc ? rc : -22, who);
+        return 0;
+    };
+    if (!seq || !seq->batch || !seq->buffer) return bad(-22, "llm: sequence has no batch slot");
+    int32_t tok = -1;
+    if (seq->state == prefill) {
+        qie_sampling s = sampling ? *sampling : reference_sampling(prefill);
+        const auto& ids = seq->buffer->h_token_ids;
+        const int rc = qie_prefill(seq->batch, seq->slot, ids.data(), (int32_t)ids.size(), &s, &tok);
+        if (rc) return bad(rc, "llm(prefill)");
+        seq->last_token = tok;
+        return tok;
+    }
+    // qie_decode_step advances every slot of the batch; the reference's llm steps only
+    // `seq`, so a B > 1 batch would silently skip tokens of its other sequences.
+    int32_t nb = 0;
+    if (qie_batch_dims(seq->batch, &nb, nullptr) != 0 || nb != 1) {
+        std::fprintf(stderr, "llm(decode): needs a batch of one slot (got %d); step B > 1 batches with "
+                             "qie_decode_step, which returns every slot's token\n", nb);
+        return bad(-22, "llm(decode)");
+    }
+    // the decode input is seq->generated_token (qwen_main.cu:259-261); the graph already
+    // holds the engine's own last output, anything else is written in first
+    if (seq->generated_token != seq->last_token) {
+        const int rc = qie_batch_set_position(seq->batch, seq->slot, seq->sequence_len, seq->generated_token);
+        if (rc) return bad(rc, "llm(decode)");
+    }
+    qie_sampling s = sampling ? *sampling : reference_sampling(decode);
+    int32_t ids[8] = {0};
+    const int rc = qie_decode_step(seq->batch, &s, ids);
+    if (rc) return bad(rc, "llm(decode)");
+    seq->sequence_len += 1;
+    seq->buffer->sequence_len = (size_t)seq->sequence_len;
+    seq->last_token = ids[seq->slot];
+    return ids[seq->slot];
+}
+
+// The engine behind the reference-form llm(): bound to the caller's weight arena
+// (g_gpu_weights_buffer) through the index, exactly as assign_weight_pointer resolves
+// every weight (helpers.cuh:19-30): base + data_offsets[0]; nothing is copied.
+struct Driver {
+    qie_engine* engine = nullptr;
+    const void* base = nullptr;
+    std::vector<qie_layer_weights> layers;
+    ~Driver() {
+        if (engine) qie_engine_destroy(engine);
+    }
+};
+inline Driver& driver() {
+    static Driver d;
+    return d;
+}
+// destroy the bound engine (before the caller frees the weight arena)
+inline void release_engine() {
+    Driver& d = driver();
+    if (d.engine) qie_engine_destroy(d.engine);
+    d.engine = nullptr;
+    d.base = nullptr;
+}
+
+inline int bind_engine_(const TensorTable& tensors, bf16* base) {
+    Driver& d = driver();
+    if (d.engine && d.base == base) return 0;
+    release_engine();
+    const qie_model_spec& s = config().spec;
+    auto ptr = [&](const char* sn, int layer, bool required, const void** out) -> bool {
+        *out = nullptr;
+        auto it = tensors.find(sn);
+        const size_t li = layer < 0 ? 0 : (size_t)layer;
+        if (it == tensors.end() || it->second.size() <= li || it->second[li].data_offsets.size() < 2 ||
+            it->second[li].short_name.empty())
+            return !required;
+        *out = reinterpret_cast<const char*>(base) + it->second[li].data_offsets[0];
+        return true;
+    };
+    d.layers.assign((size_t)s.n_layers, qie_layer_weights{});
+    bool ok = true;
+    for (int l = 0; l < s.n_layers && ok; l++) {
+        qie_layer_weights& L = d.layers[(size_t)l];
+        ok = ptr("input_layernorm.weight", l, true, &L.attn_norm) && ptr("self_attn.q_proj.weight", l, true, &L.wq) &&
+             ptr("self_attn.k_proj.weight", l, true, &L.wk) && ptr("self_attn.v_proj.weight", l, true, &L.wv) &&
+             ptr("self_attn.q_proj.bias", l, s.qkv_bias != 0, &L.bq) &&
+             ptr("self_attn.k_proj.bias", l, s.qkv_bias != 0, &L.bk) &&
+             ptr("self_attn.v_proj.bias", l, s.qkv_bias != 0, &L.bv) &&
+             ptr("self_attn.q_norm.weight", l, s.qk_norm != 0, &L.q_norm) &&
+             ptr("self_attn.k_norm.weight", l, s.qk_norm != 0, &L.k_norm) &&
+             ptr("self_attn.o_proj.weight", l, true, &L.wo) &&
+             ptr("post_attention_layernorm.weight", l, true, &L.ffn_norm) &&
+             ptr("mlp.gate_proj.weight", l, true, &L.w_gate) && ptr("mlp.up_proj.weight", l, true, &L.w_up) &&
+             ptr("mlp.down_proj.weight", l, true, &L.w_down);
+    }
+    qie_model_weights w;
+    std::memset(&w, 0, sizeof(w));
+    ok = ok && ptr("embed_tokens.weight", -1, true, &w.embed) && ptr("norm.weight", -1, true, &w.final_norm);
+    if (ok) {
+        if (s.tie_embeddings) w.lm_head = w.embed;
+        else ok = ptr("logits", -1, true, &w.lm_head);
+    }
+    if (!ok) {
+        std::fprintf(stderr, "llm: the tensor table lacks a tensor config().spec needs\n");
+        config().error = -22;
+        return -22;
+    }
+    w.n_layers = s.n_layers;
+    w.layers = d.layers.data();
+    qie_engine_opts o;
+    std::memset(&o, 0, sizeof(o));
+    o.device = config().device;
+    o.max_ctx = config().max_ctx;
+    o.use_graph = 1;
+    int rc = qie_engine_create(&s, &o, &d.engine);
+    if (!rc) rc = qie_engine_set_weights(d.engine, &w);
+    if (rc) {
+        check_(rc, "llm: engine");
+        release_engine();
+        return rc;
+    }
+    d.base = base;
+    return 0;
+}
+
+// llm, reference form (iengine.cuh:51, qwen_main.cu:64-417): prefill when
+// seq->state == prefill, else ONE decode step fed seq->generated_token; the caller
+// advances step / generated_token / state (iengine.cu:419-421).  The first call binds the
+// engine to g_gpu_weights_buffer through `tensors` and the sequence to its own KV slot.
+// Sampling follows the reference's schedule unless config().greedy.  Returns the token,
+// or 0 on error (the reference's convention).
+inline int llm(batch_metadata* seq, TensorTable tensors, std::ifstream& weights, page_table* kv_cache_seq1,
+               int page_size, bf16* g_gpu_weights_buffer) {
+    (void)weights;
+    if (!seq || !seq->buffer || !kv_cache_seq1 || page_size <= 0 || !g_gpu_weights_buffer) {
+        check_(-22, "llm: bad arguments");
+        return 0;
+    }
+    if (bind_engine_(tensors, g_gpu_weights_buffer) != 0) return 0;
+    if (!seq->batch) {
+        qie_batch* b = nullptr;
+        const int rc = qie_batch_create(driver().engine, 1, config().max_ctx, &b);
+        if (rc) {
+            check_(rc, "llm: KV slot");
+            return 0;
+        }
+        seq->batch = b;
+        seq->slot = 0;
+        seq->buffer->owned_batch = b;
+        qie_kv_cache c;
+        if (qie_batch_kv_cache(b, 0, &c) == 0) {
+            seq->k_ptr = seq->buffer->k_cache = (bf16*)c.k;
+            seq->v_ptr = seq->buffer->v_cache = (bf16*)c.v;
+        }
+    }
+    qie_sampling g;
+    g.top_k = 1;
+    g.temperature = 1.f;
+    g.top_p = 1.f;
+    g.seed = 1234;
+    return llm_step_(seq, config().greedy ? &g : nullptr);
 }
 
 // embedding_matrix_func launch (embedded_matrix.cu:5-17; decode: qwen_main.cu:259-268):

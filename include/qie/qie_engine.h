@@ -74,7 +74,10 @@ typedef struct qie_engine_opts {
     void* tp_comm;           /* qie_comm* (tensor parallel over its ranks) or NULL   */
     int32_t weight_fp8;      /* 1: linear weights + lm_head quantised to OCP e4m3 with
                                 power-of-two row scales after loading (qie_ops.h)     */
-    int32_t reserved[7];
+    int32_t comm_always;     /* 1: run the exchange steps (row-parallel all-reduces, the
+                                greedy key max, the logit gather) through tp_comm even at
+                                world 1 — the captured-collective path on one GPU (tests) */
+    int32_t reserved[6];
 } qie_engine_opts;
 
 int qie_engine_create(const qie_model_spec* spec, const qie_engine_opts* opts, qie_engine** out);

@@ -248,6 +248,11 @@ int qie_debug_fp8_decode(float* out_dev);
 int qie_synthetic_fill_slice(void* dev, int64_t rows, int64_t cols, int64_t full_cols, int64_t row0,
                              int64_t col0, uint32_t tensor_id, uint64_t seed, float scale, float offset,
                              void* stream);
+/* Rows r of a bf16 [rows, cols] matrix with (row0 + r) % every == 0 multiplied by 2^log2f
+ * in place (exact while finite).  Used to give a synthetic lm_head a peaked, trained-model-
+ * like top-1 margin for the end-to-end greedy parity runs (tests/parity.py, bench.py). */
+int qie_scale_rows_pow2(void* w, int64_t rows, int64_t cols, int64_t row0, int64_t every, int32_t log2f,
+                        void* stream);
 
 #ifdef __cplusplus
 }

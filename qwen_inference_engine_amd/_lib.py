@@ -70,7 +70,7 @@ class KvCacheC(C.Structure):
 class EngineOptsC(C.Structure):
     _fields_ = [("device", C.c_int32), ("max_ctx", C.c_int32), ("use_graph", C.c_int32),
                 ("tp_rank", C.c_int32), ("tp_size", C.c_int32), ("tp_comm", C.c_void_p),
-                ("weight_fp8", C.c_int32), ("reserved", C.c_int32 * 7)]
+                ("weight_fp8", C.c_int32), ("comm_always", C.c_int32), ("reserved", C.c_int32 * 6)]
 
 
 # (name, restype, argtypes) — every symbol the public headers declare.
@@ -121,6 +121,7 @@ SIGNATURES = [
     ("qie_synthetic_fill", C.c_int, [_P, _I64, _U32, _U64, _F, _F, _P]),
     ("qie_synthetic_fill_host", C.c_int, [_P, _I64, _U32, _U64, _F, _F]),
     ("qie_synthetic_fill_slice", C.c_int, [_P, _I64, _I64, _I64, _I64, _I64, _U32, _U64, _F, _F, _P]),
+    ("qie_scale_rows_pow2", C.c_int, [_P, _I64, _I64, _I64, _I64, _I32, _P]),
     ("qie_fp8_weight_bytes", C.c_int64, [_I64, _I64]),
     ("qie_quantize_fp8", C.c_int, [_P, _I64, _I64, _P, _P]),
     ("qie_quantize_fp8_host", C.c_int, [_P, _I64, _I64, _P]),

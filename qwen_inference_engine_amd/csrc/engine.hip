@@ -374,11 +374,15 @@ static qie_linear_args lin_base(const qie_engine* e) {
     return a;
 }
 
+// The exchange steps go through the communicator under tensor parallelism, and at world 1
+// when the engine was asked to (opts.comm_always: the captured-collective path on one GPU).
+static bool use_comm(const qie_engine* e) { return e->comm && (e->sh.tp > 1 || e->opts.comm_always); }
+
 // Row-parallel projection epilogue under tensor parallelism: fp32 partials -> all-reduce
 // -> x = bf16(x + bf16(sum)); the single-GPU path fuses the residual into the GEMV/GEMM.
 static int row_parallel(qie_batch* b, qie_linear_args& a, uint16_t* x, float* part, int64_t rows) {
     qie_engine* e = b->e;
-    if (e->sh.tp == 1) {
+    if (!use_comm(e)) {
         a.y = x;
         a.epilogue = QIE_EPI_RESIDUAL;
         return qie_linear(&a, e->stream);
@@ -499,10 +503,10 @@ static int enqueue_head(qie_batch* b, const uint16_t* x, int64_t ldx, int m0, in
         a.key_col0 = e->sh.vocab0;   // keys carry global vocab ids
     }
     QIE_TRY(gemv(&a, st));
-    if (greedy && e->sh.tp > 1) QIE_TRY(e->comm->allreduce_max_u64((uint64_t*)(b->d_keys + m0), M, st));
+    if (greedy && use_comm(e)) QIE_TRY(e->comm->allreduce_max_u64((uint64_t*)(b->d_keys + m0), M, st));
     if (!greedy) {
         const uint16_t* lg = b->logits + (int64_t)m0 * Vl;
-        if (e->sh.tp > 1) {   // every rank samples the same draw from the gathered row
+        if (use_comm(e)) {   // every rank samples the same draw from the gathered row
             QIE_TRY(gather_logits(b, m0, M));
             lg = b->logits_full + (int64_t)m0 * s.vocab;
         }
@@ -545,7 +549,7 @@ static int ensure_prefill_scratch(qie_batch* b, int64_t n) {
         *p = nullptr;
     }
     b->pf_rows = 0;
-    if (sh.tp > 1) QIE_TRY(dmalloc((void**)&b->pf_part, n * H * 4));
+    if (use_comm(b->e)) QIE_TRY(dmalloc((void**)&b->pf_part, n * H * 4));
     QIE_TRY(dmalloc((void**)&b->pf_x, n * H * 2));
     QIE_TRY(dmalloc((void**)&b->pf_hn, n * H * 2));
     QIE_TRY(dmalloc((void**)&b->pf_qkv, n * (QD + 2 * KD) * 2));
@@ -961,7 +965,7 @@ static int batch_create(qie_engine* e, int32_t batch, int32_t max_ctx, int32_t p
     A(&b->samp_ws, (size_t)qie_sample_workspace_bytes(batch, s.vocab));
     const int64_t dec_ws = qie_attention_decode_workspace_bytes(batch, sh.nq, sh.nkv, s.head_dim, max_ctx);
     A(&b->dec_ws, (size_t)dec_ws);
-    if (sh.tp > 1) {
+    if (use_comm(e)) {
         A((void**)&b->part, batch * H * 4);
         A((void**)&b->logits_full, batch * (int64_t)s.vocab * 2);
         A((void**)&b->gather_tmp, batch * (int64_t)s.vocab * 2);
@@ -1075,8 +1079,11 @@ static int prefill_rows(qie_batch* b, int seq0, int n_seqs, const int32_t* ids, 
                     "%s: KV pool exhausted (%lld pages needed, %zu free + %lld held by slots %d..%d)", who,
                     (long long)need, b->free_pages.size(), (long long)held, seq0, seq0 + n_seqs - 1);
     }
-    for (int z = 0; z < n_seqs; z++) {   // a prefill starts a new sequence in each slot
-        drop_pages(b, seq0 + z);
+    // a prefill starts a new sequence in each slot: every target slot's pages go back to
+    // the pool BEFORE any slot draws, so the check above (free + held) is exactly what the
+    // draws below can use and none of them can fail part way
+    for (int z = 0; z < n_seqs; z++) drop_pages(b, seq0 + z);
+    for (int z = 0; z < n_seqs; z++) {
         QIE_TRY(ensure_pages(b, seq0 + z, len));
         b->idle[seq0 + z] = 0;
     }
@@ -1250,7 +1257,7 @@ int qie_decode(qie_batch* b, int32_t n_steps, const qie_sampling* smp, int32_t* 
 int qie_batch_logits(qie_batch* b, void* host_out) {
     QIE_REQUIRE(b && host_out, "qie_batch_logits: bad arguments");
     const uint16_t* src = b->logits;
-    if (b->e->sh.tp > 1) {   // collective: every rank calls this at the same point
+    if (use_comm(b->e)) {   // collective: every rank calls this at the same point
         QIE_TRY(gather_logits(b, 0, b->B));
         src = b->logits_full;
     }

@@ -456,6 +456,19 @@ __global__ __launch_bounds__(256) void synth_slice_kernel(uint16_t* __restrict__
     }
 }
 
+// rows r of a [rows][cols] bf16 matrix with (row0 + r) % every == 0 times 2^log2f (exact
+// while the result stays finite): the synthetic "peaked head" of the parity runs
+__global__ __launch_bounds__(256) void scale_rows_pow2_kernel(uint16_t* __restrict__ w, int64_t rows, int64_t cols,
+                                                              int64_t row0, int64_t every, float f) {
+    const int64_t nsel = (row0 + rows + every - 1) / every - (row0 + every - 1) / every;
+    const int64_t first = (row0 + every - 1) / every * every - row0;
+    const int64_t n = nsel * cols;
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const int64_t r = first + (i / cols) * every, c = i % cols;
+        w[r * cols + c] = f2bf(bf2f(w[r * cols + c]) * f);
+    }
+}
+
 static inline uint16_t host_f2bf(float f) {
     uint32_t u;
     std::memcpy(&u, &f, 4);
@@ -844,6 +857,19 @@ int qie_synthetic_fill(void* dev, int64_t n, uint32_t tensor_id, uint64_t seed, 
     unsigned grid = (unsigned)std::min<int64_t>((n2 + 255) / 256, 16384);
     hipLaunchKernelGGL(synth_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (uint32_t*)dev,
                        n2, synth_base(tensor_id, seed), scale, offset, n);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+
+int qie_scale_rows_pow2(void* w, int64_t rows, int64_t cols, int64_t row0, int64_t every, int32_t log2f,
+                        void* stream) {
+    QIE_REQUIRE(w && rows >= 0 && cols > 0 && row0 >= 0 && every > 0 && log2f >= -32 && log2f <= 32,
+                "qie_scale_rows_pow2: bad arguments");
+    const int64_t nsel = (row0 + rows + every - 1) / every - (row0 + every - 1) / every;
+    if (nsel <= 0 || log2f == 0) return 0;
+    const unsigned grid = (unsigned)std::min<int64_t>((nsel * cols + 255) / 256, 4096);
+    hipLaunchKernelGGL(scale_rows_pow2_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (uint16_t*)w, rows, cols,
+                       row0, every, ldexpf(1.0f, log2f));
     QIE_LAUNCH_CHECK();
     return 0;
 }

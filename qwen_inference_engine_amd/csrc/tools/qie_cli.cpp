@@ -133,7 +133,7 @@ int main(int argc, char** argv) {
     auto tp0 = std::chrono::steady_clock::now();
     int tok = llm(seq, greedy ? &g : nullptr);
     auto tp1 = std::chrono::steady_clock::now();
-    if (tok < 0) return 1;
+    if (config().error) return 1;
     out.push_back(tok);
     if (stream) { std::printf("%d\n", tok); std::fflush(stdout); }
     seq->step++;                 // iengine.cu:419-421
@@ -141,7 +141,7 @@ int main(int argc, char** argv) {
     seq->state = decode;
     while ((int)out.size() < gen && tok != kRefEos) {
         tok = llm(seq, greedy ? &g : nullptr);
-        if (tok < 0) return 1;
+        if (config().error) return 1;
         out.push_back(tok);
         if (stream) { std::printf("%d\n", tok); std::fflush(stdout); }
         seq->step++;

@@ -22,8 +22,11 @@ def group_dir() -> str:
     d = os.environ.get("QIE_GROUP_DIR")
     if d:
         return d
-    run = os.environ.get("TORCHELASTIC_RUN_ID", "x")
-    return os.path.join("/tmp", f"qie_group_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}_{run}")
+    port = os.environ.get("MASTER_PORT", "0")
+    run = os.environ.get("TORCHELASTIC_RUN_ID")
+    if run:   # torch.distributed.run: the run id is shared by every rank (and unique to the run)
+        return os.path.join("/tmp", f"qie_group_{port}_{run}")
+    return os.path.join("/tmp", f"qie_group_{port}_{os.getppid()}")
 
 
 class FileGroup:
@@ -48,10 +51,10 @@ class FileGroup:
             for r in range(self.world):
                 if vals[r] is None:
                     p = os.path.join(self.dir, f"g{self.gen}_r{r}.json")
-                    if os.path.exists(p):
+                    try:
                         with open(p) as f:
                             vals[r] = [json.load(f)]
-                    else:
+                    except FileNotFoundError:
                         done = False
             if done:
                 return [v[0] for v in vals]
@@ -69,8 +72,14 @@ class FileGroup:
         return max(self._exchange(float(x)))
 
     def close(self) -> None:
-        """Final barrier, then rank 0 removes the rendezvous directory."""
+        """Final barrier; every rank then leaves a 'closed' marker (it reads nothing more),
+        and rank 0 removes the rendezvous directory once all markers are there."""
         self.barrier()
+        open(os.path.join(self.dir, f"closed_r{self.rank}"), "w").close()
         if self.rank == 0:
-            time.sleep(0.05)
+            t0 = time.time()
+            while time.time() - t0 < self.timeout:
+                if all(os.path.exists(os.path.join(self.dir, f"closed_r{r}")) for r in range(self.world)):
+                    break
+                time.sleep(0.001)
             shutil.rmtree(self.dir, ignore_errors=True)

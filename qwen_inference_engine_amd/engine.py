@@ -106,7 +106,7 @@ class Comm:
 
 class Engine:
     def __init__(self, spec: ModelSpec, device: int = 0, max_ctx: int = 4096, use_graph: bool = True,
-                 comm: Optional[Comm] = None, weight_fp8: bool = False):
+                 comm: Optional[Comm] = None, weight_fp8: bool = False, comm_always: bool = False):
         self.lib = _lib.load()
         self.spec = spec
         self._spec_c = spec.to_c()
@@ -115,7 +115,9 @@ class Engine:
         opts.tp_rank, opts.tp_size = (comm.rank, comm.world) if comm else (0, 1)
         opts.tp_comm = comm.h if comm else None
         opts.weight_fp8 = int(weight_fp8)
+        opts.comm_always = int(comm_always)   # exchange steps through comm even at world 1 (tests)
         self.comm = comm
+        self._fp8 = weight_fp8
         h = C.c_void_p()
         _lib.check(self.lib.qie_engine_create(C.byref(self._spec_c), C.byref(opts), C.byref(h)),
                    "qie_engine_create")
@@ -126,7 +128,20 @@ class Engine:
     def init_synthetic(self, p: SynthParams = SynthParams()) -> "Engine":
         _lib.check(self.lib.qie_engine_init_synthetic(self.h, p.seed, p.w_scale, p.norm_scale, p.bias_scale),
                    "qie_engine_init_synthetic")
+        if p.head_boost_every > 0 and p.head_boost_log2 != 0:
+            self.boost_head(p.head_boost_every, p.head_boost_log2)
         return self
+
+    def boost_head(self, every: int, log2f: int) -> None:
+        """lm_head rows r % every == 0 times 2^log2f, in place on device (SynthParams'
+        peaked head; same values as HostWeights.boost_head).  bf16 single-GPU engines."""
+        if self.comm is not None or getattr(self, "_fp8", False):
+            raise ValueError("boost_head: bf16 single-GPU engines only")
+        w = _lib.ModelWeightsC()
+        _lib.check(self.lib.qie_engine_weights(self.h, C.byref(w), None), "qie_engine_weights")
+        _lib.check(self.lib.qie_scale_rows_pow2(w.lm_head, self.spec.vocab, self.spec.hidden, 0, every, log2f,
+                                                self.stream), "qie_scale_rows_pow2")
+        self.sync()
 
     def load_weights_bin(self, bin_path: str, meta_path: str, chunk_bytes: int = 1 << 28) -> "Engine":
         _lib.check(self.lib.qie_engine_load_weights_bin(self.h, bin_path.encode(), meta_path.encode(),

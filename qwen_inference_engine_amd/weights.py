@@ -198,6 +198,13 @@ class SynthParams:
     w_scale: float = 0.0346   # uniform[-a, a) with std 0.02 (N(0, 0.02))
     norm_scale: float = 0.0   # norm weights 1 + norm_scale*u   (reference init: 1)
     bias_scale: float = 0.0346
+    # Peaked head (parity runs only): lm_head rows r with r % head_boost_every == 0 are
+    # multiplied by 2^head_boost_log2 (exact in bf16).  A random head gives near-flat
+    # logits whose top-2 gaps sit inside the ~4 % full-depth summation-order spread of any
+    # bf16 pipeline; a few boosted rows concentrate the competition the way a trained
+    # model's unembedding does.  0 = off.  A tied head is the embedding.
+    head_boost_every: int = 0
+    head_boost_log2: int = 0
 
     def for_tensor(self, short_name: str) -> Tuple[float, float]:
         """(scale, offset) of a tensor by role."""
@@ -238,7 +245,19 @@ class HostWeights:
         for name, shape in hf_tensor_shapes(spec).items():
             c = classify(name)
             t[name] = synthetic_tensor(name, c[1], int(np.prod(shape)), p).reshape(shape)
-        return cls(spec, t)
+        hw = cls(spec, t)
+        if p.head_boost_every > 0 and p.head_boost_log2 != 0:
+            hw.boost_head(p.head_boost_every, p.head_boost_log2)
+        return hw
+
+    def boost_head(self, every: int, log2f: int) -> None:
+        """lm_head rows r % every == 0 times 2^log2f (libqie's qie_scale_rows_pow2 on the host)."""
+        name = "model.embed_tokens.weight" if self.spec.tie_embeddings else "lm_head.weight"
+        w = self.tensors[name].copy()
+        f = (w[::every].astype(np.uint32) << 16).view(np.float32) * np.float32(2.0 ** log2f)
+        assert np.isfinite(f).all()
+        w[::every] = (f.view(np.uint32) >> 16).astype(np.uint16)
+        self.tensors[name] = w
 
     @classmethod
     def from_weights_bin(cls, spec: ModelSpec, bin_path: str, meta_path: str) -> "HostWeights":

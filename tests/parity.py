@@ -109,3 +109,93 @@ def oracle_trace(oracle, pair, prompt, n_steps, forced=None):
         outs.append(pair.forward([nxt]))
         ids.append(oracle.argmax(outs[-1][0]))
     return ids, outs
+
+
+# ----------------------------------------------------------------------------------------
+# Forced-continuation greedy decisions (full-depth parity in bench.py; the 2-layer P = 2048
+# twin in tests/test_gpu_headline.py).  The sequence is a prompt followed by a seeded random
+# continuation fed one token per decode step (teacher forcing on a fixed sequence, so no
+# decision depends on an earlier one and a degenerate repetition cannot form); at each of
+# the n decision points (the prefill's and n - 1 decode steps') the engine's greedy id and
+# bf16 logits are compared with three oracle evaluations of the same arithmetic: summation
+# order 0 (the restatement), 1 (matmul sums reordered) and 2 (every fp32 reduction
+# reordered, fast-math exponent).  Weights: SynthParams with a peaked head (PEAKED).
+PEAKED = dict(head_boost_every=4096, head_boost_log2=3)
+
+
+class OrderSet:
+    """Oracle models over the same weights in summation orders 0, 1 and 2, stepped in lock-step."""
+
+    ORDERS = (0, 1, 2)
+
+    def __init__(self, oracle, hw, max_ctx, nthreads=0):
+        self.O = oracle
+        self.models = [oracle.Model(hw, max_ctx, nthreads=nthreads) for _ in self.ORDERS]
+
+    def forward(self, ids, start=None):
+        out = []
+        for o, m in zip(self.ORDERS, self.models):
+            self.O.set_sum_order(o)
+            try:
+                out.append(m.forward(ids, start))
+            finally:
+                self.O.set_sum_order(0)
+        return out
+
+
+def forced_decisions(oracle, hw, batch, prompt, n, seed=77, nthreads=0):
+    """Runs the protocol above on slot 0 of `batch` (an engine over the same weights as
+    `hw`).  Returns the report dict; report["ok"] applies the rule:
+      * every step's engine logits within max(1e-3, 2 x the run's max order-0 vs order-2
+        norm-relative spread) of order 0;
+      * no hard mismatch: an engine id that differs from order 0 must be a near-tie whose
+        order-0 top-2 gap is within max(2 bf16 ulps of max|logit|, the run's max absolute
+        order-1 / order-2 logit spread);
+      * near-tie flips <= max_flips(n)."""
+    V = hw.spec.vocab
+    P = len(prompt)
+    forced = [int(t) for t in np.random.default_rng(seed).integers(0, V, max(n - 1, 0))]
+    ors = OrderSet(oracle, hw, P + n + 2, nthreads)
+    steps = []
+    t_e = batch.prefill(0, prompt)
+    for i in range(n):
+        lg = ors.forward(prompt, 0) if i == 0 else ors.forward([forced[i - 1]])
+        ge = batch.logits()[0]
+        f = [G.bf(x).astype(np.float64) for x in lg]
+        steps.append(dict(ids=[oracle.argmax(x) for x in lg], gpu=int(t_e), rel=norm_rel(ge, lg[0]),
+                          rel01=norm_rel(lg[1], lg[0]), rel02=norm_rel(lg[2], lg[0]),
+                          abs_spread=float(max(np.abs(f[1] - f[0]).max(), np.abs(f[2] - f[0]).max())),
+                          lg0=lg[0], ulps=2 * 2.0 ** -7 * float(np.abs(f[0]).max())))
+        if i + 1 < n:
+            batch.set_position(0, P + i, forced[i])
+            t_e = batch.decode_step()[0]
+    rel02 = max(s["rel02"] for s in steps)
+    rel01 = max(s["rel01"] for s in steps)
+    abs_spread = max(s["abs_spread"] for s in steps)
+    bar = max(NORM_REL, SPREAD_FACTOR * rel02)
+    flips = hard = agreed_flips = 0
+    for s in steps:
+        o0 = s["ids"][0]
+        if s["gpu"] == o0:
+            continue
+        lg0 = s["lg0"]
+        gap = abs(float(G.bf(lg0[o0])) - float(G.bf(lg0[s["gpu"]])))
+        if gap <= max(s["ulps"], abs_spread):
+            flips += 1
+            if s["ids"][1] == o0 and s["ids"][2] == o0:
+                agreed_flips += 1
+        else:
+            hard += 1
+    rep = {
+        "decisions": n, "prompt": P, "forced_seed": seed,
+        "oracle_o1_vs_o0_id_disagreements": sum(s["ids"][1] != s["ids"][0] for s in steps),
+        "oracle_o2_vs_o0_id_disagreements": sum(s["ids"][2] != s["ids"][0] for s in steps),
+        "gpu_vs_o0_id_disagreements": sum(s["gpu"] != s["ids"][0] for s in steps),
+        "gpu_near_tie_flips": flips, "gpu_flips_where_oracle_orders_agree": agreed_flips,
+        "hard_mismatches": hard, "max_flips": max_flips(n),
+        "max_norm_rel": round(max(s["rel"] for s in steps), 6),
+        "oracle_o1_spread": round(rel01, 6), "oracle_o2_spread": round(rel02, 6), "bar": round(bar, 6),
+        "max_abs_spread": round(abs_spread, 5),
+    }
+    rep["ok"] = bool(max(s["rel"] for s in steps) <= bar and hard == 0 and flips <= max_flips(n))
+    return rep

@@ -138,3 +138,50 @@ def test_reference_layer_loop_matches_oracle(oracle, name, paged, tmp_path):
     for i in range(n_new + 1):
         flips += check_step(lgs[i], outs[i][0], om, toks[i], ids[i], f"step {i}")
     assert flips <= max_flips(n_new + 1)
+
+
+DRIVER = os.path.join(ROOT, "qwen_inference_engine_amd", "lib", "ref_driver")
+
+
+@pytest.mark.parametrize("name", ["qwen3-like", "qwen2-like-tied"])
+def test_reference_signature_driver_matches_oracle(oracle, name, tmp_path):
+    """csrc/tools/ref_driver.cpp: a host written only against the reference's driver-tier
+    argument lists (llm(seq, tensors, ifstream&, page_table*, page_size, bf16*),
+    create_new_sequence(id, ids, len, tensors, ifstream&), create_page_list(n),
+    allocate_page_buffers(node, elems), load_all_weights_to_gpu_chunked(all, ifstream&,
+    h_host, chunk, d_base&, total&), parsed_tensors(), build_indexed_tensors()) in the call
+    order of iengine.cu:226-456, over a weights.bin + meta_data.txt written in the
+    reference's flat layout.  Its greedy tokens (llm() fed back generated_token) against
+    or_forward teacher-forced on them: every token the oracle's arg-max or a near-tie within
+    the oracle's own order spread (tests/parity.py), at most max_flips."""
+    if name == "qwen3-like":   # the reference's model family (qk-norm, no bias, untied)
+        spec = S.tiny("t-drv3", n_layers=3, hidden=512, n_heads=8, n_kv_heads=2, head_dim=128, ffn=1024,
+                      vocab=4096, bias=False, qk_norm=True)
+    else:
+        spec = S.tiny("t-drv2", n_layers=2, hidden=256, n_heads=4, n_kv_heads=2, head_dim=64, ffn=512,
+                      vocab=2048, bias=True, qk_norm=False, tie=True)
+    syn = W.SynthParams(seed=9, w_scale=0.08, norm_scale=0.25, bias_scale=0.05)
+    hw = W.HostWeights.synthetic(spec, syn)
+    wb, meta = str(tmp_path / "weights.bin"), str(tmp_path / "meta_data.txt")
+    hw.write_weights_bin(wb, meta)
+    prompt = [int(t) for t in rng(31).integers(0, spec.vocab, 21)]
+    n = 16
+    sp = ",".join(str(v) for v in (spec.n_layers, spec.hidden, spec.n_heads, spec.n_kv_heads, spec.head_dim,
+                                   spec.ffn, spec.vocab, int(spec.tie_embeddings), int(spec.qkv_bias),
+                                   int(spec.qk_norm), repr(float(spec.rms_eps)), repr(float(spec.rope_theta))))
+    r = subprocess.run([DRIVER, "--weights", wb, "--meta", meta, "--spec", sp, "--greedy", "--gen", str(n),
+                        "--max-ctx", "128", "--prompt", ",".join(map(str, prompt))],
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = [int(t) for t in [l for l in r.stdout.splitlines() if l.startswith("tokens:")][0].split()[1:]]
+    assert len(got) == n
+    pair = OrderPair(oracle, hw, len(prompt) + n + 4)
+    ids, outs = oracle_trace(oracle, pair, prompt, n, forced=got[:-1])
+    pair.calibrate(spec.vocab)
+    flips = 0
+    for i, (t, (lg0, _)) in enumerate(zip(got, outs)):
+        if t != ids[i]:
+            gap = abs(float(G.bf(lg0[ids[i]])) - float(G.bf(lg0[t])))
+            assert gap <= pair.bars(lg0)[1], f"step {i}: driver {t} vs oracle {ids[i]}, gap {gap}"
+            flips += 1
+    assert flips <= max_flips(n)

@@ -22,7 +22,7 @@ import pytest
 import gpu_util as G
 from conftest import rng
 from test_gpu_ops import _cache, _linear, _abs_scale, rand_bf16
-from parity import OrderPair, check_step, max_flips, oracle_trace
+from parity import PEAKED, OrderPair, check_step, forced_decisions, max_flips, oracle_trace
 
 import qwen_inference_engine_amd as Q
 from qwen_inference_engine_amd import _lib, spec as S, weights as W
@@ -47,6 +47,24 @@ def test_headline_prefill_2048_and_graph_decode(oracle):
         if i + 1 < n_new:
             t_e = b.decode_step()[0]
     assert flips <= max_flips(n_new)
+
+
+def test_headline_forced_decisions_2layers_p2048(oracle):
+    """The 2-layer twin of bench.py's full-depth gpu_parity (tests/parity.py
+    forced_decisions, same rule): Qwen2-7B widths, peaked head, a 2048-token prompt
+    (LDS-DMA GEMMs, flash prefill attention) then 63 graph decode steps at ctx 2049..2111
+    on a seeded random continuation — 64 greedy decisions against oracle orders 0 / 1 / 2."""
+    spec = S.QWEN2_7B.replace(n_layers=2)
+    syn = W.SynthParams(seed=0, **PEAKED)
+    P, n, max_ctx = 2048, 64, 2176
+    eng = Q.Engine(spec, max_ctx=max_ctx, use_graph=True).init_synthetic(syn)
+    b = eng.batch(1, max_ctx)
+    prompt = [int(t) for t in rng(2048).integers(0, spec.vocab, P)]
+    rep = forced_decisions(oracle, W.HostWeights.synthetic(spec, syn), b, prompt, n)
+    print("forced decisions (2 layers, P 2048):", rep)
+    assert rep["ok"], rep
+    # at 2 layers the orders agree on every decision; so must the engine
+    assert rep["gpu_flips_where_oracle_orders_agree"] == 0, rep
 
 
 @pytest.mark.parametrize("hd,nq,nkv", [(128, 28, 4), (64, 14, 2)])

@@ -385,3 +385,25 @@ def test_prefill_batch_all_or_nothing_and_bad_arguments():
     with pytest.raises(ValueError):
         pb.prefill_batch(1, [[1, 2, 3], [4, 5]])
     assert list(pb.decode(40)[:, 0]) == want
+
+
+def test_prefill_batch_into_live_slots_reuses_their_pages():
+    """Re-prefilling live slots whose pages are all the pool has: slot 0 holds 1 page, slot
+    1 holds 3, none free; two 200-token prompts need 2 pages each.  The all-or-nothing
+    check counts the held pages (4 <= 0 + 4), so the call must succeed — every target slot
+    returns its pages before any draws (a slot-by-slot drop-then-draw ran dry at slot 0) —
+    and generate exactly what the same prompts do in a fresh batch."""
+    eng = Q.Engine(SPEC, max_ctx=512).init_synthetic(SYN)
+    pb = eng.batch(2, 512, page_tokens=128, n_pages=5)   # page 0 scratch + 4
+    pb.prefill(0, list(rng(7).integers(0, SPEC.vocab, 100)))
+    pb.prefill(1, list(rng(8).integers(0, SPEC.vocab, 300)))
+    free, per, _ = pb.page_stats()
+    assert free == 0 and list(per) == [1, 3]
+    two = [list(rng(9 + z).integers(0, SPEC.vocab, 200)) for z in range(2)]
+    got = pb.prefill_batch(0, two)
+    assert list(pb.page_stats()[1]) == [2, 2]
+    gdec = pb.decode(20).tolist()
+    fresh = eng.batch(2, 512, page_tokens=128, n_pages=5)
+    assert fresh.prefill_batch(0, two) == got
+    assert fresh.decode(20).tolist() == gdec
+    assert np.array_equal(fresh.logits(), pb.logits())

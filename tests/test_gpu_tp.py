@@ -167,6 +167,37 @@ def test_rccl_single_rank_communicator():
     c.close()
 
 
+@pytest.mark.parametrize("name", ["qwen2-bias-hd64", "qwen3-qknorm-hd128"])
+@pytest.mark.parametrize("greedy", [True, False])
+def test_rccl_world1_collectives_in_graph(name, greedy):
+    """The engine's exchange-step code path (row-parallel fp32 partials + ncclAllReduce +
+    residual add after O and down, the u64 max all-reduce of the greedy keys or the logit
+    all-gather before sampling, the prefill all-reduces) on a ONE-rank RCCL communicator
+    (qie_engine_opts.comm_always), decode steps CAPTURED in the hipGraph: graph replay ==
+    the same engine run eagerly, bit for bit (ids and logits), and both == the engine
+    without a communicator (a one-rank all-reduce is the identity; the F32 epilogue +
+    residual add rounds exactly as the fused residual epilogue)."""
+    spec, _ = CONFIGS[name]
+    prompt = [int(t) for t in rng(5).integers(0, spec.vocab, 37)]
+    smp = Q.GREEDY if greedy else Q.Sampling(top_k=40, temperature=0.8, top_p=0.9, seed=99)
+    uid = Q.Comm.unique_id()
+    comm = Q.Comm.rccl(uid, 1, 0, 0)
+    out = {}
+    for tag, kw in (("graph", dict(comm=comm, comm_always=True, use_graph=True)),
+                    ("eager", dict(comm=comm, comm_always=True, use_graph=False)),
+                    ("plain", dict(use_graph=True))):
+        eng = Q.Engine(spec, max_ctx=128, **kw).init_synthetic(SYN)
+        b = eng.batch(1, 128)
+        ids = [b.prefill(0, prompt, smp)] + [int(t) for t in b.decode(20, smp)[:, 0]]
+        out[tag] = (ids, b.logits())
+        b.close()
+        eng.close()
+    comm.close()
+    for tag in ("eager", "plain"):
+        assert out[tag][0] == out["graph"][0], tag
+        assert np.array_equal(out[tag][1], out["graph"][1]), tag
+
+
 def test_tp_paged_equals_contiguous():
     """Tensor-parallel ranks each hold their kv heads' pages; the per-rank allocators make
     the same decisions, and a paged batch generates what a contiguous one does, bit for bit

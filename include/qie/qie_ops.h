@@ -232,6 +232,10 @@ int qie_synthetic_fill_host(void* host, int64_t n, uint32_t tensor_id, uint64_t 
  * power-of-two row scales (qie_fp8_weight_bytes); every dequantised value is exactly a
  * bf16.  qie_linear reads such weights when args.flags has QIE_LINEAR_FP8. */
 #define QIE_LINEAR_FP8 1
+/* Prefill GEMM tile override (tests / tuning; M >= 256, K % 32 == 0): the LDS-DMA kernel
+ * with 256x256 (TILE256) or 256x128 (TILE128) block tiles instead of the tile-count choice. */
+#define QIE_LINEAR_TILE256 2
+#define QIE_LINEAR_TILE128 4
 int64_t qie_fp8_weight_bytes(int64_t rows, int64_t cols);
 int qie_quantize_fp8(const void* w_bf16, int64_t rows, int64_t cols, void* out, void* stream);
 int qie_quantize_fp8_host(const void* w_bf16, int64_t rows, int64_t cols, void* out);

@@ -21,6 +21,8 @@ QIE_EPI_RESIDUAL = 1
 QIE_EPI_SWIGLU = 2
 QIE_EPI_F32 = 3
 QIE_LINEAR_FP8 = 1
+QIE_LINEAR_TILE256 = 2
+QIE_LINEAR_TILE128 = 4
 QIE_COMM_ID_BYTES = 128
 
 

@@ -401,7 +401,7 @@ static int row_parallel(qie_batch* b, qie_linear_args& a, uint16_t* x, float* pa
 // cost 13-16 us per launch at B = 8 (tools/ubench_b8.py, QIE_SKINNY_DBG); M = 1 keeps the
 // GEMV's fused x-first prologue.  QIE_PRENORM=0 restores the fused form (A/B).
 static int prenorm(qie_batch* b, qie_linear_args& a, int64_t M) {
-    static const int on = getenv("QIE_PRENORM") ? atoi(getenv("QIE_PRENORM")) : 1;
+    static const int on = dev_env("QIE_PRENORM", 1);
     if (!on || M < 2 || M > 16 || !a.norm_w) return 0;
     QIE_TRY(qie_rmsnorm(a.x, a.norm_w, b->xn, M, a.K, a.norm_eps, a.numerics, b->e->stream));
     a.x = b->xn;
@@ -1352,7 +1352,7 @@ int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* av
     QIE_TRY(dmalloc((void**)&scratch,
                     (size_t)B * std::max<int64_t>(std::max(I, V), QD + 2 * KD) * 2 + B * 8 + 64));
     const double wb = e->fp8 ? 1.0 : 2.0;   // weight bytes per element (fp8 row scales: negligible)
-    const bool batched_norm = B >= 2 && !(getenv("QIE_PRENORM") && atoi(getenv("QIE_PRENORM")) == 0);
+    const bool batched_norm = B >= 2 && dev_env("QIE_PRENORM", 1) != 0;
     auto args_for = [&](int l, double* by) {
         const qie_layer_weights& L = e->layers[l];
         qie_linear_args a = lin_base(e);

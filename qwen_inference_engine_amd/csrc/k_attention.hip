@@ -219,6 +219,7 @@ struct DecodeAttnParams {
     int splits_target;        // ~splits per (row, kv head) at long context
     int dbg;                  // timing experiments only (QIE_DEC_DBG): 1 no combine,
                               // 8/16 stop after prologue / P.V, 64 exit at once
+    int sc1;                  // combine reads the partials with sc1 loads instead of an acquire
     float eps;
     int numerics;
     float* part_o;            // [B][nq][nsplit_max][HD]
@@ -275,6 +276,8 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef short i16x4_t __attribute__((ext_vector_type(4)));
 typedef unsigned int kv16_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 
 // 16 bytes per lane global -> LDS (LDS-DMA); `lds` is the wave-instruction's 1-KiB base,
 // lane l lands at lds + 16 l
@@ -649,7 +652,7 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
     const int p = a.pos[m], ctx = p + 1;
     const int chunk = decm_chunk(ctx, a.splits_target);
     const int nsplit = (ctx + chunk - 1) / chunk;
-    if (s >= nsplit || (a.dbg & 64)) return false;
+    if (s >= nsplit || QIE_DBG(a.dbg & 64)) return false;
     const int t0 = s * chunk, t1 = min(ctx, t0 + chunk);
     const int nstep = (t1 - t0 + kDecMStep - 1) / kDecMStep;
     const bool has_new = (t1 == ctx);
@@ -689,7 +692,7 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
     for (int idx = tid; idx < (16 - G) * CPR; idx += 256)   // padded q rows
         *reinterpret_cast<uint4*>(&q_s[G + idx / CPR][(idx % CPR) * 8]) = make_uint4(0, 0, 0, 0);
     __syncthreads();
-    if (a.dbg & 8) {
+    if (QIE_DBG(a.dbg & 8)) {
         if (tid == 0) a.out[m] = (uint16_t)(kf[0][0].x + vr[VCH - 1].y + kf[1][KSTEPS - 1].z);
         return false;
     }
@@ -804,7 +807,7 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
         }
         __syncthreads();   // scores / V slots free for the next step
     }
-    if (a.dbg & 16) {
+    if (QIE_DBG(a.dbg & 16)) {
         if (tid == 0) a.out[m] = (uint16_t)(oacc[0][0] + m_run);
         return false;
     }
@@ -846,7 +849,7 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
     // ---------------- publish this split; the last arriver combines (acquire)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
     __syncthreads();
-    if (a.dbg & 1) return false;
+    if (QIE_DBG(a.dbg & 1)) return false;
     unsigned* cnt = a.counters + m * a.nkv + g;
     if (tid == 0) {
         const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -857,9 +860,11 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
     // acquire, then plain loads.  Measured alternatives without the fence (sc1 loads of
     // the write-through partials, MI355X_MICROARCH.md hand-off row 1): 8-B agent-scope
     // atomic loads 11.4 vs 10.7 us per launch; 16-B sc1 raw buffer loads 73 us.
-    if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if (!a.sc1) {
+        if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
     // Per-thread online combine: thread (head gi, d4) loads the (m, l) of EVERY split of its
     // head together with its 16-byte slice of every split's partial O (one batch of JB
     // splits = one round trip; ctx <= JB * 128 keys in one), then merges them itself — no
@@ -875,11 +880,31 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
     for (int j0 = 0; j0 < nsplit; j0 += JB) {
         float4 v[JB];
         float2 w[JB];
+        if (a.sc1) {
+            // sc1 loads (L2 / memory side, never a stale L1 line) in place of the acquire:
+            // every partial was stored sc1 by a wave that drained (vmcnt 0) before its
+            // workgroup's barrier and ticket add, and this workgroup's add came last
+            // (MI355X_MICROARCH.md hand-off table, row 1).  Buffer loads on a uniform
+            // resource: the resource stays in SGPRs.
+            const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)a.part_o, 0, 0x7fffffff, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)a.part_ml, 0, 0x7fffffff, 0x00020000);
 #pragma unroll
-        for (int jj = 0; jj < JB; jj++) {
-            const int j = min(j0 + jj, nsplit - 1);
-            v[jj] = src4[(int64_t)j * (HD / 4)];
-            w[jj] = ml2[j];
+            for (int jj = 0; jj < JB; jj++) {
+                const int j = min(j0 + jj, nsplit - 1);
+                const u32x4_t q4 = __builtin_amdgcn_raw_buffer_load_b128(
+                    ro, (int)(((hbase + j) * (HD / 4) + d4) * 16), 0, 16);
+                const u32x2_t q2 = __builtin_amdgcn_raw_buffer_load_b64(rm, (int)((hbase + j) * 8), 0, 16);
+                v[jj] = make_float4(__uint_as_float(q4.x), __uint_as_float(q4.y), __uint_as_float(q4.z),
+                                    __uint_as_float(q4.w));
+                w[jj] = make_float2(__uint_as_float(q2.x), __uint_as_float(q2.y));
+            }
+        } else {
+#pragma unroll
+            for (int jj = 0; jj < JB; jj++) {
+                const int j = min(j0 + jj, nsplit - 1);
+                v[jj] = src4[(int64_t)j * (HD / 4)];
+                w[jj] = ml2[j];
+            }
         }
         float mb = mx;
 #pragma unroll
@@ -926,8 +951,7 @@ __global__ void tr16_probe_kernel(int32_t* out) {
 }
 
 static int attn_nsplit(int64_t M, int32_t max_ctx) {
-    const char* e = getenv("QIE_ATTN_SPLIT_TOKENS");
-    int per = e ? atoi(e) : 0;
+    int per = dev_env("QIE_ATTN_SPLIT_TOKENS", 0);
     if (per <= 0) per = M > 8 ? 512 : 64;
     int ns = (max_ctx + per - 1) / per;
     const int cap = M > 8 ? 8 : 64;
@@ -952,10 +976,10 @@ static int fill_dec_params(DecodeAttnParams& a, const void* qkv, int64_t B, cons
     a.nkv = cache->n_kv_heads;
     a.nq = n_heads;
     a.max_ctx = cache->max_ctx;
-    const char* se = getenv("QIE_DEC_SPLITS");
-    const int senv = se ? std::min(atoi(se), kDecMaxSplits) : 0;
+    const int senv = std::min(dev_env("QIE_DEC_SPLITS", 0), kDecMaxSplits);
     a.splits_target = senv > 0 ? senv : kDecMSplits;
-    a.dbg = getenv("QIE_DEC_DBG") ? atoi(getenv("QIE_DEC_DBG")) : 0;
+    a.dbg = dev_env("QIE_DEC_DBG", 0);
+    a.sc1 = dev_env("QIE_DEC_SC1", 0);
     a.nsplit_max = std::min(a.splits_target, (cache->max_ctx + kDecMStep - 1) / kDecMStep);
     QIE_REQUIRE(a.nsplit_max <= kDecMaxSplits, "qie_attention_decode: max_ctx %d too long", cache->max_ctx);
     a.eps = eps;

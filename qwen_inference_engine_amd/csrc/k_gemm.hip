@@ -490,14 +490,15 @@ int gemm(const qie_linear_args* a, hipStream_t st) {
     if (!(a->flags & QIE_LINEAR_FP8) && a->K % big::BK == 0 && a->ldx % 8 == 0) {
         // LDS-DMA kernel: 256x256 tiles when they fill the chip at least twice over, else
         // 256x128 when those fill >= 3/4 of it in one round (Qwen2-7B O and down projections
-        // at 2,048 rows: 112 vs 224 tiles on 256 CUs), else 256x256 in one round (below).  QIE_GEMM_BIG: 1 / 2 force the
-        // 256 / 128-column tile, 0 disables the kernel (tests and A/B timing).
+        // at 2,048 rows: 112 vs 224 tiles on 256 CUs), else 256x256 in one round (below).
+        // args.flags QIE_LINEAR_TILE256 / TILE128 force a tile (tests; dev builds also
+        // QIE_GEMM_BIG = 1 / 2, 0 disables the kernel for A/B timing).
         const int64_t cols = a->epilogue == QIE_EPI_SWIGLU ? 2 * a->N : a->N;
         const int64_t n_mt = cdiv(a->M, big::BM);
         const int64_t t256 = n_mt * cdiv(cols, 256), t128 = n_mt * cdiv(cols, 128);
         const int64_t cus = device_cu_count();
-        const char* ev = getenv("QIE_GEMM_BIG");
-        const int force = ev ? atoi(ev) : -1;
+        const int force = (a->flags & QIE_LINEAR_TILE256) ? 1 : (a->flags & QIE_LINEAR_TILE128) ? 2
+                                                                                            : dev_env("QIE_GEMM_BIG", -1);
         if (force == 1 || (force < 0 && a->M >= big::BM && t256 >= 2 * cus))
             return launch_gemm_big<256>(a->epilogue, p, (int)n_mt, (int)t256, st);
         if (force == 2 || (force < 0 && a->M >= big::BM && t128 >= (3 * cus) / 4 && t128 <= cus))

@@ -715,8 +715,8 @@ __global__ __launch_bounds__(NW * 64) void skinny_mfma_kernel(GemvParams p) {
     // ---------------- prologue: the M activation rows -> LDS (optionally RMS-normed).  It runs
     // AFTER the first step's weight loads are issued (weights do not depend on x), so the
     // weight stream's first HBM round trip overlaps the prologue's loads and reductions.
-    if (XL && !(p.dbg & 4)) {
-        if (p.norm_w && !(p.dbg & 1)) {
+    if (XL && !QIE_DBG(p.dbg & 4)) {
+        if (p.norm_w && !QIE_DBG(p.dbg & 1)) {
             // pass 1: every row's sum of squares at once (loads of all rows in flight,
             // clamped rows past M), ONE exchange — not a barrier pair per row
             float ss[16];
@@ -800,7 +800,7 @@ __global__ __launch_bounds__(NW * 64) void skinny_mfma_kernel(GemvParams p) {
         }
         __syncthreads();
     }
-    if (p.dbg & 2) {
+    if (QIE_DBG(p.dbg & 2)) {
         if (tid == 0 && p.dbg == 0x7fffffff) p.y[0] = xs[0];
         return;
     }
@@ -846,10 +846,7 @@ __global__ __launch_bounds__(NW * 64) void skinny_mfma_kernel(GemvParams p) {
 // block size bound of the one-block-per-CU GEMV variant (9 waves: Qwen2-7B QKV; O / down use 7)
 constexpr int kGemvBalancedThreads = 576;
 
-static int env_int_gemv(const char* name, int dflt) {
-    const char* v = getenv(name);
-    return v ? atoi(v) : dflt;
-}
+static int env_int_gemv(const char* name, int dflt) { return dev_env(name, dflt); }
 
 // UO: chunks per row in flight when K needs fewer than the default 8 wave-loads per row
 // (0 = default).  A slot past K re-reads the row's last 16 B, so at K = 896 (Qwen2-0.5B)
@@ -964,10 +961,7 @@ static int launch_gemv_1(const GemvParams& p, int rpw, int epi, hipStream_t st, 
 
 int gemm(const qie_linear_args* a, hipStream_t st);
 
-static int env_int(const char* name, int dflt) {
-    const char* v = getenv(name);
-    return v ? atoi(v) : dflt;
-}
+static int env_int(const char* name, int dflt) { return dev_env(name, dflt); }
 
 constexpr size_t kGemvLdsCap = 96 * 1024;
 constexpr size_t kSkinnyLdsCap = 120 * 1024;

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 
 #include "../../include/qie/qie_types.h"
@@ -46,6 +47,21 @@ int fail(int code, const char* fmt, ...);
 #endif
 
 constexpr int kWave = 64;
+
+// ------------------------------------------------------------- dev knobs
+// A/B and timing knobs (environment variables, kernel debug early exits) exist only in the
+// development build (`make DEV=1` -> lib/dev/libqie.so; tools point QIE_LIB at it).  The
+// shipped library compiles every knob to its default and the debug branches away.
+#ifdef QIE_DEV
+inline int dev_env(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v ? atoi(v) : dflt;
+}
+#define QIE_DBG(expr) (expr)
+#else
+inline int dev_env(const char*, int dflt) { return dflt; }
+#define QIE_DBG(expr) false
+#endif
 
 // ------------------------------------------------------------- bf16 helpers
 __device__ __forceinline__ float bf2f(uint32_t h16) { return __uint_as_float(h16 << 16); }

@@ -143,7 +143,7 @@ class OrderSet:
         return out
 
 
-def forced_decisions(oracle, hw, batch, prompt, n, seed=77, nthreads=0):
+def forced_decisions(oracle, hw, batch, prompt, n, seed=77, nthreads=0, progress=False):
     """Runs the protocol above on slot 0 of `batch` (an engine over the same weights as
     `hw`).  Returns the report dict; report["ok"] applies the rule:
       * every step's engine logits within max(1e-3, 2 x the run's max order-0 vs order-2
@@ -166,6 +166,8 @@ def forced_decisions(oracle, hw, batch, prompt, n, seed=77, nthreads=0):
                           rel01=norm_rel(lg[1], lg[0]), rel02=norm_rel(lg[2], lg[0]),
                           abs_spread=float(max(np.abs(f[1] - f[0]).max(), np.abs(f[2] - f[0]).max())),
                           lg0=lg[0], ulps=2 * 2.0 ** -7 * float(np.abs(f[0]).max())))
+        if progress and (i % 16 == 0 or i + 1 == n):
+            print(f"  forced decision {i + 1}/{n}: rel {steps[-1]['rel']:.2e}", flush=True)
         if i + 1 < n:
             batch.set_position(0, P + i, forced[i])
             t_e = batch.decode_step()[0]
@@ -174,12 +176,14 @@ def forced_decisions(oracle, hw, batch, prompt, n, seed=77, nthreads=0):
     abs_spread = max(s["abs_spread"] for s in steps)
     bar = max(NORM_REL, SPREAD_FACTOR * rel02)
     flips = hard = agreed_flips = 0
+    flip_gaps = []
     for s in steps:
         o0 = s["ids"][0]
         if s["gpu"] == o0:
             continue
         lg0 = s["lg0"]
         gap = abs(float(G.bf(lg0[o0])) - float(G.bf(lg0[s["gpu"]])))
+        flip_gaps.append(round(gap, 5))
         if gap <= max(s["ulps"], abs_spread):
             flips += 1
             if s["ids"][1] == o0 and s["ids"][2] == o0:
@@ -195,7 +199,9 @@ def forced_decisions(oracle, hw, batch, prompt, n, seed=77, nthreads=0):
         "hard_mismatches": hard, "max_flips": max_flips(n),
         "max_norm_rel": round(max(s["rel"] for s in steps), 6),
         "oracle_o1_spread": round(rel01, 6), "oracle_o2_spread": round(rel02, 6), "bar": round(bar, 6),
-        "max_abs_spread": round(abs_spread, 5),
+        "max_abs_spread": round(abs_spread, 5), "gpu_flip_top2_gaps": flip_gaps,
+        "median_top2_gap": round(float(np.median([abs(np.diff(np.sort(G.bf(s["lg0"]).astype(np.float64))[-2:]))[0]
+                                                  for s in steps])), 5),
     }
     rep["ok"] = bool(max(s["rel"] for s in steps) <= bar and hard == 0 and flips <= max_flips(n))
     return rep

@@ -200,6 +200,23 @@ def test_qwen2_0_5b_config1_greedy_matches_oracle(oracle):
     assert flips <= 2
 
 
+def test_qwen2_0_5b_config2_p128_g128_forced_decisions(oracle):
+    """BASELINE config 2 end to end: the full Qwen2-0.5B (24 layers, tied head) with a
+    128-token prompt (M = 128 prefill dispatch) and 127 hipGraph decode steps at ctx
+    129..255 (the one-split decode attention), 128 greedy decisions on a forced
+    continuation against or_forward in summation orders 0 / 1 / 2 (tests/parity.py
+    forced_decisions; peaked head = boosted rows of the tied embedding)."""
+    from parity import PEAKED, forced_decisions
+    spec = S.QWEN2_0_5B
+    syn = W.SynthParams(seed=0, **PEAKED)
+    eng = Q.Engine(spec, max_ctx=272).init_synthetic(syn)
+    b = eng.batch(1, 272)
+    prompt = [int(t) for t in rng(128).integers(0, spec.vocab, 128)]
+    rep = forced_decisions(oracle, W.HostWeights.synthetic(spec, syn), b, prompt, 128, progress=True)
+    print("config 2 forced decisions:", rep)
+    assert rep["ok"], rep
+
+
 @pytest.mark.slow
 def test_qwen2_7b_widths_two_layers_match_oracle(oracle):
     """Full Qwen2-7B widths (H 3584, I 18944, 28/4 heads, V 152064), 2 layers: any

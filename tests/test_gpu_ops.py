@@ -48,7 +48,7 @@ def test_rmsnorm(oracle, qlib, rows, H, num):
 
 
 # --------------------------------------------------------------------------- linear
-def _linear(qlib, x, segs, biases, M, K, N, y, epi, norm_w=None, eps=1e-4, num=0, keys=None, ldy=None):
+def _linear(qlib, x, segs, biases, M, K, N, y, epi, norm_w=None, eps=1e-4, num=0, keys=None, ldy=None, flags=0):
     a = LinearArgsC()
     a.x, a.ldx = G.p(x), K
     for i, s in enumerate(segs):
@@ -62,6 +62,7 @@ def _linear(qlib, x, segs, biases, M, K, N, y, epi, norm_w=None, eps=1e-4, num=0
     a.norm_w = G.p(norm_w) if norm_w is not None else None
     a.norm_eps, a.numerics = eps, num
     a.argmax_keys = G.p(keys) if keys is not None else None
+    a.flags = flags
     G.check(qlib.qie_linear(C.byref(a), None), "qie_linear")
 
 
@@ -134,11 +135,11 @@ def test_linear_swiglu(oracle, qlib, M, K, I):
 @pytest.mark.parametrize("M,K", [(256, 896), (300, 96), (520, 32), (257, 3584)])
 @pytest.mark.parametrize("epi", ["store3", "residual", "swiglu", "f32"])
 @pytest.mark.parametrize("tile", ["1", "2"])
-def test_linear_big_gemm(oracle, qlib, M, K, epi, tile, monkeypatch):
-    """The LDS-DMA prefill GEMM, 256x256 (QIE_GEMM_BIG=1) and 256x128 (=2) tiles, forced at
-    test sizes (the engine picks them by tile count): every epilogue, ragged M and N
-    (clamped rows never stored), K of 1, 3 and 28+ k-tiles (ring prologue / drain)."""
-    monkeypatch.setenv("QIE_GEMM_BIG", tile)
+def test_linear_big_gemm(oracle, qlib, M, K, epi, tile):
+    """The LDS-DMA prefill GEMM, 256x256 (QIE_LINEAR_TILE256) and 256x128 (QIE_LINEAR_TILE128)
+    tiles, forced at test sizes (the engine picks them by tile count): every epilogue, ragged
+    M and N (clamped rows never stored), K of 1, 3 and 28+ k-tiles (ring prologue / drain)."""
+    fl = _lib.QIE_LINEAR_TILE256 if tile == "1" else _lib.QIE_LINEAR_TILE128
     x = rand_bf16(oracle, (M, K), seed=M + K)
     if epi == "store3":
         n = (200, 72, 40)
@@ -148,7 +149,7 @@ def test_linear_big_gemm(oracle, qlib, M, K, epi, tile, monkeypatch):
         want = np.concatenate([oracle.matmul(x, w, b) for w, b in zip(ws, bs)], axis=1)
         y = G.zeros_bf16(M, N)
         _linear(qlib, G.dev(x), [(G.dev(w), r) for w, r in zip(ws, n)], [G.dev(b) for b in bs], M, K, N, y,
-                _lib.QIE_EPI_STORE)
+                _lib.QIE_EPI_STORE, flags=fl)
         scale = np.concatenate([_abs_scale(oracle, x, w) for w in ws], axis=1)
         G.assert_sum_close(G.host_bf16(y), want, scale, what=f"big store M={M} K={K}")
     elif epi == "residual":
@@ -157,7 +158,7 @@ def test_linear_big_gemm(oracle, qlib, M, K, epi, tile, monkeypatch):
         res = rand_bf16(oracle, (M, N), seed=5)
         want = oracle.resadd(res, oracle.matmul(x, w))
         y = G.dev(res)
-        _linear(qlib, G.dev(x), [(G.dev(w), N)], [], M, K, N, y, _lib.QIE_EPI_RESIDUAL)
+        _linear(qlib, G.dev(x), [(G.dev(w), N)], [], M, K, N, y, _lib.QIE_EPI_RESIDUAL, flags=fl)
         acc = G.bf(oracle.matmul(x, w)).astype(np.float64)
         tol = 2.0 ** -7 * (np.abs(acc) + np.abs(G.bf(want))) + 1e-5 * _abs_scale(oracle, x, w)
         assert (np.abs(G.bf(G.host_bf16(y)).astype(np.float64) - G.bf(want)) <= tol).all()
@@ -167,7 +168,7 @@ def test_linear_big_gemm(oracle, qlib, M, K, epi, tile, monkeypatch):
         wu = rand_bf16(oracle, (I, K), 0.08, seed=8)
         want = oracle.silu_mul(oracle.matmul(x, wg), oracle.matmul(x, wu))
         y = G.zeros_bf16(M, I)
-        _linear(qlib, G.dev(x), [(G.dev(wg), I), (G.dev(wu), I)], [], M, K, I, y, _lib.QIE_EPI_SWIGLU)
+        _linear(qlib, G.dev(x), [(G.dev(wg), I), (G.dev(wu), I)], [], M, K, I, y, _lib.QIE_EPI_SWIGLU, flags=fl)
         got = G.host_bf16(y)
         d = G.ulp_diff(got, want)
         gs = G.bf(oracle.matmul(x, wg)).astype(np.float64)
@@ -178,7 +179,7 @@ def test_linear_big_gemm(oracle, qlib, M, K, epi, tile, monkeypatch):
         N = 264
         w = rand_bf16(oracle, (N, K), 0.05, seed=9)
         y = G.zeros((M, N), np.float32)
-        _linear(qlib, G.dev(x), [(G.dev(w), N)], [], M, K, N, y, _lib.QIE_EPI_F32)
+        _linear(qlib, G.dev(x), [(G.dev(w), N)], [], M, K, N, y, _lib.QIE_EPI_F32, flags=fl)
         want = oracle.bf16_to_f32(x).astype(np.float64) @ oracle.bf16_to_f32(w).astype(np.float64).T
         assert np.abs(G.host(y) - want).max() <= 1e-5 * _abs_scale(oracle, x, w).max() + 1e-6
 

@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Kernel A/B micro-benchmarks on the real Qwen2-7B decode state (one process, interleaved
-rounds, cdna_hip_programming.md §5.4 rule 24).  Prints one JSON line per measurement."""
+rounds, cdna_hip_programming.md §5.4 rule 24).  Prints one JSON line per measurement.
+The knobs exist only in the development build: run with
+QIE_LIB=qwen_inference_engine_amd/lib/dev/libqie.so (make -C ... DEV=1)."""
 import json
 import os
 import sys
@@ -25,6 +27,9 @@ def main():
     b.decode(256, want_ids=False)          # ctx ~2300
     sets = os.environ.get("UB_SET", "attn,gemv").split(",")
     variants = []
+    if os.environ.get("UB_VARIANTS"):   # JSON list of [kernel name, which, {env}]
+        variants += [tuple(v) for v in json.loads(os.environ["UB_VARIANTS"])]
+        sets = []
     if "attn" in sets:
         variants += [("attn", 5, {})]
         for sp in ("8", "16", "24", "48"):

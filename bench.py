@@ -55,6 +55,9 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-prompt", type=int, default=16)
     ap.add_argument("--cpu-decode", type=int, default=8)
+    ap.add_argument("--cpu-full", action="store_true",
+                    help="CPU baseline at BASELINE.md §3's sizes instead of the bounded sample: the headline "
+                         "model's full prompt (--prompt) prefill + --cpu-decode steps, median of 3 (minutes)")
     ap.add_argument("--parity-decisions", type=int, default=64,
                     help="full-depth greedy decisions of the GPU-vs-oracle parity sample (cpu_baseline leg)")
     ap.add_argument("--fp8", action="store_true",
@@ -317,19 +320,23 @@ def cpu_baseline(spec, a, batch, eng):
     t0 = time.perf_counter()
     hw = W.HostWeights.synthetic(spec, W.SynthParams(seed=0))
     t_gen = time.perf_counter() - t0
-    prompt = [int(x) for x in np.random.default_rng(5).integers(0, spec.vocab, a.cpu_prompt)]
-    m0 = O.Model(hw, a.cpu_prompt + a.cpu_decode + 4, nthreads=threads)
-    t0 = time.perf_counter()
-    lg0 = m0.forward(prompt, 0)
-    t_pf = time.perf_counter() - t0
-    ids = [O.argmax(lg0)]
-    lgs = [lg0]
-    t0 = time.perf_counter()
-    for _ in range(a.cpu_decode):
-        lgs.append(m0.forward([ids[-1]]))
-        ids.append(O.argmax(lgs[-1]))
-    t_dec = time.perf_counter() - t0
-    del m0
+    n_pf = a.prompt if a.cpu_full else a.cpu_prompt
+    full_prompt = [int(x) for x in np.random.default_rng(5).integers(0, spec.vocab, n_pf)]
+    prompt = full_prompt[:a.cpu_prompt]
+    runs = []
+    for _ in range(3 if a.cpu_full else 1):   # median of 3 at full size
+        m0 = O.Model(hw, n_pf + a.cpu_decode + 4, nthreads=threads)
+        t0 = time.perf_counter()
+        lg0 = m0.forward(full_prompt, 0)
+        t_pf = time.perf_counter() - t0
+        ids = [O.argmax(lg0)]
+        t0 = time.perf_counter()
+        for _ in range(a.cpu_decode):
+            ids.append(O.argmax(m0.forward([ids[-1]])))
+        runs.append((t_pf, time.perf_counter() - t0))
+        del m0
+    t_pf = float(np.median([r[0] for r in runs]))
+    t_dec = float(np.median([r[1] for r in runs]))
     # ---- full-depth greedy parity (tests/parity.py forced_decisions): the engine's
     # lm_head and the host copy get the same exact peaked-head boost (parity.PEAKED), then
     # a 16-token prompt + a seeded random continuation, a.parity_decisions decisions,
@@ -347,10 +354,10 @@ def cpu_baseline(spec, a, batch, eng):
     del hw
     return {"value": round(a.cpu_decode / t_dec, 4), "unit": "tokens/s", "cores": threads, "kind": "port",
             "host_nproc": os.cpu_count(),
-            "sample": f"{spec.name}: {a.cpu_prompt}-token prefill ({t_pf:.2f} s, "
-                      f"{a.cpu_prompt / t_pf:.2f} tok/s) + {a.cpu_decode} greedy decode steps "
-                      f"({t_dec:.2f} s); weights generated in {t_gen:.1f} s",
-            "prefill_tok_s": round(a.cpu_prompt / t_pf, 3),
+            "sample": f"{spec.name}: {n_pf}-token prefill ({t_pf:.2f} s, "
+                      f"{n_pf / t_pf:.2f} tok/s) + {a.cpu_decode} greedy decode steps at ctx {n_pf + 1}.. "
+                      f"({t_dec:.2f} s){', median of 3' if a.cpu_full else ''}; weights generated in {t_gen:.1f} s",
+            "prefill_tok_s": round(n_pf / t_pf, 3),
             "config1": {"workload": "Qwen2-0.5B, prompt=16, gen=16, greedy (BASELINE config 1), timed in full",
                         "seconds": round(t_c1, 3), "tokens_s": round(16 / t_c1, 2), "ids_head": ids05[:4],
                         "cores": threads},

@@ -151,10 +151,15 @@ int qie_attention(const void* q, int64_t M, const int32_t* pos, int32_t rows_per
 /* Decode attention with the q/k post-projection fused in (one launch per layer):
  * qkv rows [B][(nq + 2 nkv) hd] straight from the QKV projection; applies qk-norm
  * (q_norm/k_norm non-NULL) and RoPE at pos[m] to q and to the new k, appends the
- * new K/V row of sequence m at pos[m], and attends over [0, pos[m]].  Splits of 64
+ * new K/V row of sequence m at pos[m], and attends over [0, pos[m]].  Splits of 128
  * keys are combined in-launch by the last-arriving workgroup.  ws must hold
  * qie_attention_decode_workspace_bytes() and be ZEROED once before first use (it
- * is left zeroed by every call). */
+ * is left zeroed by every call).
+ * numerics may carry QIE_ATTN_PREROPED (REF numerics, no qk-norm only): q and the new
+ * k in qkv are already rotated (the engine's decode QKV projection applies RoPE in its
+ * epilogue), so only the K/V append and the attention run here. */
+#define QIE_NUMERICS_MASK 0xff
+#define QIE_ATTN_PREROPED 0x100
 int64_t qie_attention_decode_workspace_bytes(int64_t B, int32_t n_heads, int32_t n_kv_heads,
                                              int32_t head_dim, int32_t max_ctx);
 int qie_attention_decode(const void* qkv, int64_t B, const int32_t* pos, const void* q_norm,
@@ -246,6 +251,8 @@ int qie_quantize_fp8_host(const void* w_bf16, int64_t rows, int64_t cols, void* 
 int qie_dequantize_fp8(const void* w_fp8, int64_t rows, int64_t cols, void* out_bf16, void* stream);
 /* Test probe: out_dev[i] = the device decode of e4m3 code i (i < 256). */
 int qie_debug_fp8_decode(float* out_dev);
+/* Test probe: out_dev[i] = the bf16 bits the fp8 MFMA GEMV decodes e4m3 code i to (i < 256). */
+int qie_debug_fp8_decode_bf16(uint16_t* out_dev);
 
 /* Tensor-parallel shard of the same synthetic tensor: dev[i][j] = element
  * (row0 + i) * full_cols + col0 + j of the full tensor, rows x cols, row-major. */

@@ -26,6 +26,8 @@
 
 namespace qie {
 int gemv(const qie_linear_args* a, hipStream_t st);
+int gemv_rope(const qie_linear_args* a, const int32_t* pos, const float* cs, const float* sn, int hd, int64_t rows,
+              hipStream_t st);
 int gemm(const qie_linear_args* a, hipStream_t st);
 }  // namespace qie
 
@@ -410,6 +412,14 @@ static int prenorm(qie_batch* b, qie_linear_args& a, int64_t M) {
     return 0;
 }
 
+// batch 1, REF numerics, no qk-norm (Qwen2): the decode QKV projection's epilogue rotates q
+// and k (gemv_rope), so the attention's critical path loses the position -> RoPE-table round
+// trip (QIE_ATTN_PREROPED)
+static bool rope_in_projection(const qie_batch* b) {
+    const qie_model_spec& s = b->e->spec;
+    return b->B == 1 && !s.qk_norm && s.numerics == QIE_NUMERICS_REF && dev_env("QIE_ROPE_IN_PROJ", 0) != 0;
+}
+
 static int enqueue_layer_decode(qie_batch* b, int l) {
     qie_engine* e = b->e;
     const qie_model_spec& s = e->spec;
@@ -429,10 +439,13 @@ static int enqueue_layer_decode(qie_batch* b, int l) {
     a.epilogue = QIE_EPI_STORE;
     a.norm_w = L.attn_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
     QIE_TRY(prenorm(b, a, B));
-    QIE_TRY(gemv(&a, st));
+    const bool rope_in_proj = rope_in_projection(b);
+    if (rope_in_proj) QIE_TRY(gemv_rope(&a, b->d_pos, e->rope_cos, e->rope_sin, (int)hd, QD + KD, st));
+    else QIE_TRY(gemv(&a, st));
 
     QIE_TRY(qie_attention_decode(b->qkv, B, b->d_pos, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, e->sh.nq,
-                                 &cache, l, s.rms_eps, s.numerics, b->att, b->dec_ws, st));
+                                 &cache, l, s.rms_eps, s.numerics | (rope_in_proj ? QIE_ATTN_PREROPED : 0), b->att,
+                                 b->dec_ws, st));
     a = lin_base(e);
     a.x = b->att; a.ldx = QD;
     a.w[0] = L.wo; a.seg_rows[0] = H;
@@ -1403,11 +1416,15 @@ int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* av
     auto run = [&](int i) -> int {
         const int l = layer_of(i);
         const qie_layer_weights& L = e->layers[l];
+        const bool rp = rope_in_projection(b);
         if (which == 5)
             return qie_attention_decode(b->qkv, B, b->d_pos, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, sh.nq,
-                                        &cache, l, s.rms_eps, s.numerics, scratch, b->dec_ws, e->stream);
+                                        &cache, l, s.rms_eps, s.numerics | (rp ? QIE_ATTN_PREROPED : 0), scratch,
+                                        b->dec_ws, e->stream);
         double lb = 0;
         qie_linear_args a = args_for(l, &lb);
+        if (which == 2 && rp)   // as the step runs it
+            return gemv_rope(&a, b->d_pos, e->rope_cos, e->rope_sin, (int)s.head_dim, QD + KD, e->stream);
         return qie_linear(&a, e->stream);
     };
     if (which != 5) args_for(0, &by);

@@ -220,6 +220,8 @@ struct DecodeAttnParams {
     int dbg;                  // timing experiments only (QIE_DEC_DBG): 1 no combine,
                               // 8/16 stop after prologue / P.V, 64 exit at once
     int sc1;                  // combine reads the partials with sc1 loads instead of an acquire
+    int pre_roped;            // q and the new k arrive rotated by the QKV projection's epilogue
+                              // (REF numerics, no qk-norm): the prologue only moves them
     float eps;
     int numerics;
     float* part_o;            // [B][nq][nsplit_max][HD]
@@ -551,7 +553,7 @@ struct DecPro {
     bool is_q, is_k, is_v, pro, nrm, hf;
 };
 
-template <int HD>
+template <int HD, bool PR>
 __device__ __forceinline__ DecPro dec_pro_issue(const DecodeAttnParams& a, const uint16_t* row, int g, int G, int grp,
                                                 int dl, int p, bool has_new) {
     DecPro d;
@@ -564,6 +566,10 @@ __device__ __forceinline__ DecPro dec_pro_issue(const DecodeAttnParams& a, const
                                  : (d.is_k ? row + a.nq * HD + g * HD : row + (a.nq + a.nkv) * HD + g * HD);
     if (!(d.is_q || d.is_k || d.is_v)) src = row;
     d.raw = *reinterpret_cast<const uint4*>(src + dl * 8);
+    if constexpr (PR) {   // rotated upstream, no qk-norm: nothing else to load
+        d.nrm = false;
+        return d;
+    }
     const uint16_t* nwp = d.is_q ? a.q_norm : a.k_norm;
     d.nrm = nwp != nullptr && !d.is_v;
     d.nraw = *reinterpret_cast<const uint4*>((nwp ? nwp : row) + dl * 8);
@@ -580,41 +586,65 @@ __device__ __forceinline__ DecPro dec_pro_issue(const DecodeAttnParams& a, const
 
 // qk-norm + RoPE of the q heads and the new k, then q -> LDS (bf16), new k/v -> cache
 // and LDS.  Branch-free (only the stores are predicated), stores predicated, loads unconditional).
-template <int HD>
+template <int HD, bool PR>
 __device__ __forceinline__ void dec_pro_finish(const DecodeAttnParams& a, DecPro& d, int dl, int grp, int64_t poff,
                                                uint16_t* kb, uint16_t* vb, uint16_t (*q_s)[HD],
                                                uint16_t (*kv_new)[HD]) {
 #pragma clang fp contract(off)
     constexpr int LPT = HD / 8;
+    if constexpr (PR) {   // q / new k already rotated: move them
+        pin4(d.raw);
+        if (d.is_q) {
+            *reinterpret_cast<uint4*>(&q_s[grp][dl * 8]) = d.raw;
+        } else if (d.pro) {
+            *reinterpret_cast<uint4*>((d.is_k ? kb : vb) + poff + dl * 8) = d.raw;
+            *reinterpret_cast<uint4*>(&kv_new[d.is_k ? 0 : 1][dl * 8]) = d.raw;
+        }
+        return;
+    }
     pin4(d.raw); pin4(d.nraw); pin4(d.c0); pin4(d.s0); pin4(d.c1); pin4(d.s1);
     float x[8], wv[8];
     unpack_bf8(d.raw, x);
     unpack_bf8(d.nraw, wv);
-    float ss = 0.f;
+    // qk-norm (Qwen3) and HF numerics are launch-uniform: branch around them instead of
+    // computing both forms per element (Qwen2, REF: neither — 8 divisions and the HF RoPE
+    // products per lane were dead work on the critical path)
+    if (a.q_norm != nullptr) {
+        float ss = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; j++) ss += x[j] * x[j];
-    ss = group_sum<LPT>(ss);
-    const float rms = sqrtf((ss / (float)HD) + a.eps);
+        for (int j = 0; j < 8; j++) ss += x[j] * x[j];
+        ss = group_sum<LPT>(ss);
+        const float rms = sqrtf((ss / (float)HD) + a.eps);
+        if (d.hf) {
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-        const float xn = d.hf ? rbf(wv[j] * rbf(x[j] * (1.0f / rms))) : rbf((x[j] / rms) * wv[j]);
-        x[j] = d.nrm ? xn : x[j];
+            for (int j = 0; j < 8; j++) {
+                const float xn = rbf(wv[j] * rbf(x[j] * (1.0f / rms)));
+                x[j] = d.nrm ? xn : x[j];
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const float xn = rbf((x[j] / rms) * wv[j]);
+                x[j] = d.nrm ? xn : x[j];
+            }
+        }
     }
     const float cv[8] = {d.c0.x, d.c0.y, d.c0.z, d.c0.w, d.c1.x, d.c1.y, d.c1.z, d.c1.w};
     const float sv[8] = {d.s0.x, d.s0.y, d.s0.z, d.s0.w, d.s1.x, d.s1.y, d.s1.z, d.s1.w};
-    float o[8], y[8];
+    float y[8];
+    if (d.hf) {
+        float o[8];
 #pragma unroll
-    for (int j = 0; j < 8; j++) o[j] = __shfl_xor(x[j], LPT / 2, 64);
-    const bool first = dl < LPT / 2;
+        for (int j = 0; j < 8; j++) o[j] = __shfl_xor(x[j], LPT / 2, 64);
+        const float sg = dl < LPT / 2 ? -1.f : 1.f;   // rotate_half: first half takes -x[j + hd/2]
 #pragma unroll
-    for (int j = 0; j < 8; j += 2) {
-        const float ya = rbf(x[j] * cv[j / 2] - x[j + 1] * sv[j / 2]);
-        const float yb = rbf(x[j + 1] * cv[j / 2] + x[j] * sv[j / 2]);
-        const float ha = first ? rbf(rbf(x[j] * cv[j]) + rbf(-o[j] * sv[j])) : rbf(rbf(x[j] * cv[j]) + rbf(o[j] * sv[j]));
-        const float hb = first ? rbf(rbf(x[j + 1] * cv[j + 1]) + rbf(-o[j + 1] * sv[j + 1]))
-                               : rbf(rbf(x[j + 1] * cv[j + 1]) + rbf(o[j + 1] * sv[j + 1]));
-        y[j] = d.hf ? ha : ya;
-        y[j + 1] = d.hf ? hb : yb;
+        for (int j = 0; j < 8; j++) y[j] = rbf(rbf(x[j] * cv[j]) + rbf((sg * o[j]) * sv[j]));
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+            y[j] = rbf(x[j] * cv[j / 2] - x[j + 1] * sv[j / 2]);
+            y[j + 1] = rbf(x[j + 1] * cv[j / 2] + x[j] * sv[j / 2]);
+        }
     }
 #pragma unroll
     for (int j = 0; j < 8; j++) x[j] = d.is_v ? x[j] : y[j];
@@ -630,32 +660,28 @@ __device__ __forceinline__ void dec_pro_finish(const DecodeAttnParams& a, DecPro
 
 // Body of the decode attention for workgroup (bx, by); true when this workgroup wrote a
 // combined (row, kv head) output (its stores are write-through, sc1).
-template <int HD, bool PG>
+template <int HD, bool PG, int NWA, bool PR>
 __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a, const int bx, const int by) {
 #pragma clang fp contract(off)
     constexpr int LPT = HD / 8;          // prologue: lanes per head row
     constexpr int KSTEPS = HD / 32;      // MFMA k-steps over d for S
     constexpr int CPR = HD / 8;          // 16-byte chunks per K row
-    constexpr int DW = HD / 4;           // output dims per wave
-    constexpr int DTW = DW / 16;         // output d tiles per wave (2 at hd 128, 1 at 64)
+    constexpr int DW = HD / NWA;         // output dims per wave
+    constexpr int DTW = DW / 16;         // output d tiles per wave (2 at hd 128 x 4 waves, else 1)
     constexpr int CPW = DW / 8;          // 16-byte chunks of a V row per wave
     constexpr int VCH = kDecMStep * CPW / 64;   // V chunks per lane per step
+    constexpr int TPW = kDecMStep / (16 * NWA);  // 16-key S tiles per wave per step
+    constexpr int NT = 64 * NWA;         // threads
+    static_assert(DTW >= 1 && TPW >= 1, "attn_decode: NWA too large for HD");
     __shared__ __attribute__((aligned(16))) uint16_t q_s[16][HD];
     __shared__ __attribute__((aligned(16))) uint16_t kv_new[2][HD];
-    __shared__ __attribute__((aligned(16))) uint16_t v_s[4][kDecMStep * DW];
+    __shared__ __attribute__((aligned(16))) uint16_t v_s[NWA][kDecMStep * DW];
     __shared__ __attribute__((aligned(16))) float s_s[16][kDecMStep + 4];
     __shared__ int last_flag;
 
     const int64_t m = by;
     const int g = bx / a.nsplit_max, s = bx % a.nsplit_max;
     const int G = a.nq / a.nkv;
-    const int p = a.pos[m], ctx = p + 1;
-    const int chunk = decm_chunk(ctx, a.splits_target);
-    const int nsplit = (ctx + chunk - 1) / chunk;
-    if (s >= nsplit || QIE_DBG(a.dbg & 64)) return false;
-    const int t0 = s * chunk, t1 = min(ctx, t0 + chunk);
-    const int nstep = (t1 - t0 + kDecMStep - 1) / kDecMStep;
-    const bool has_new = (t1 == ctx);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int fr = lane & 15, gq = lane >> 4;
     const int grp = tid / LPT, dl = tid % LPT;
@@ -664,18 +690,14 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
     const int64_t head_off = kv_run_off(a.km, (int64_t)a.layer * a.nkv + g, HD);
     uint16_t* kb = a.kc + head_off;
     uint16_t* vb = a.vc + head_off;
-
-    // ---------------- loads: prologue operands, then step 0's K tiles and V slice
-    DecPro pr = dec_pro_issue<HD>(a, row, g, G, grp, dl, p, has_new);
-    __builtin_amdgcn_sched_barrier(0);
-    uint4 kf[2][KSTEPS], vr[VCH];
-    auto load_step = [&](int st) {
-        const int kb0 = t0 + st * kDecMStep;
+    uint4 kf[TPW][KSTEPS], vr[VCH];
+    // step loads of keys [kb0, kb0 + 128), rows past `last` re-read row `last`
+    auto load_step_at = [&](int kb0, int last) {
         // a 128-key step never straddles a page (chunks and pages are multiples of 128)
         const int64_t so = kv_tok<PG>(a.km, m, kb0, HD);
 #pragma unroll
-        for (int t = 0; t < 2; t++) {
-            const int key = min(kb0 + 32 * wave + 16 * t + fr, t1 - 1);
+        for (int t = 0; t < TPW; t++) {
+            const int key = min(kb0 + 16 * TPW * wave + 16 * t + fr, last);
 #pragma unroll
             for (int ks = 0; ks < KSTEPS; ks++)
                 kf[t][ks] = *reinterpret_cast<const uint4*>(kb + so + (int64_t)(key - kb0) * HD + 32 * ks + 8 * gq);
@@ -683,17 +705,51 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
 #pragma unroll
         for (int i = 0; i < VCH; i++) {
             const int c = lane + 64 * i;
-            const int key = min(kb0 + c / CPW, t1 - 1);
+            const int key = min(kb0 + c / CPW, last);
             vr[i] = *reinterpret_cast<const uint4*>(vb + so + (int64_t)(key - kb0) * HD + wave * DW + (c % CPW) * 8);
         }
     };
-    load_step(0);
-    dec_pro_finish<HD>(a, pr, dl, grp, kv_tok<PG>(a.km, m, p, HD), kb, vb, q_s, kv_new);
-    for (int idx = tid; idx < (16 - G) * CPR; idx += 256)   // padded q rows
+    // Speculative step (pre-rotated, contiguous): the split of every context of 257 ..
+    // 128 * splits keys is keys [128 s, 128 s + 128) (decm_chunk's one-step rule), so its
+    // K / V loads go out with the position load instead of one HBM round trip behind it.
+    // The rotated q / k / v row goes out first (position-independent): vmcnt retires in
+    // order, and the prologue that waits for it must not wait behind the whole K / V step.
+    constexpr bool SPEC = PR && !PG;
+    const int p = a.pos[m];
+    DecPro pr;
+    if constexpr (SPEC) {
+        pr = dec_pro_issue<HD, PR>(a, row, g, G, grp, dl, 0, false);
+        __builtin_amdgcn_sched_barrier(0);
+        load_step_at(kDecMStep * s, a.max_ctx - 1);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    const int ctx = p + 1;
+    const int chunk = decm_chunk(ctx, a.splits_target);
+    const int nsplit = (ctx + chunk - 1) / chunk;
+    if (s >= nsplit || QIE_DBG(a.dbg & 64)) return false;
+    const int t0 = s * chunk, t1 = min(ctx, t0 + chunk);
+    const int nstep = (t1 - t0 + kDecMStep - 1) / kDecMStep;
+    const bool has_new = (t1 == ctx);
+    auto load_step = [&](int st) { load_step_at(t0 + st * kDecMStep, t1 - 1); };
+
+    // ---------------- loads: prologue operands, then step 0's K tiles and V slice
+    if constexpr (SPEC) pr.pro = pr.is_q || ((pr.is_k || pr.is_v) && has_new);
+    else pr = dec_pro_issue<HD, PR>(a, row, g, G, grp, dl, p, has_new);
+    __builtin_amdgcn_sched_barrier(0);
+    if (!SPEC || chunk != kDecMStep) load_step(0);   // (uniform) the speculative step was not this split's
+    if constexpr (SPEC) {
+        // rows past the context hold whatever the cache has there: their scores are masked
+        // to -inf (P = 0), and their V rows are zeroed so that 0 * V stays 0 for any bits
+#pragma unroll
+        for (int i = 0; i < VCH; i++)
+            if (t0 + (lane + 64 * i) / CPW >= t1) vr[i] = make_uint4(0, 0, 0, 0);
+    }
+    dec_pro_finish<HD, PR>(a, pr, dl, grp, kv_tok<PG>(a.km, m, p, HD), kb, vb, q_s, kv_new);
+    for (int idx = tid; idx < (16 - G) * CPR; idx += NT)   // padded q rows
         *reinterpret_cast<uint4*>(&q_s[G + idx / CPR][(idx % CPR) * 8]) = make_uint4(0, 0, 0, 0);
     __syncthreads();
     if (QIE_DBG(a.dbg & 8)) {
-        if (tid == 0) a.out[m] = (uint16_t)(kf[0][0].x + vr[VCH - 1].y + kf[1][KSTEPS - 1].z);
+        if (tid == 0) a.out[m] = (uint16_t)(kf[0][0].x + vr[VCH - 1].y + kf[TPW - 1][KSTEPS - 1].z);
         return false;
     }
 
@@ -716,16 +772,16 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
         const int kb0 = t0 + st * kDecMStep;
         // ---- S^T for this wave's 32 keys -> LDS (raw dots)
 #pragma unroll
-        for (int t = 0; t < 2; t++) {
+        for (int t = 0; t < TPW; t++) {
             f32x4_t sacc = f32x4_t{0.f, 0.f, 0.f, 0.f};
-            const bool nw = kb0 + 32 * wave + 16 * t + fr == p;
+            const bool nw = kb0 + 16 * TPW * wave + 16 * t + fr == p;
 #pragma unroll
             for (int ks = 0; ks < KSTEPS; ks++)
                 sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                     __builtin_bit_cast(bf16x8_t, sel4(nw, knew[ks], kf[t][ks])), qb[ks], sacc, 0, 0, 0);
             // C map: col = head fr, rows = keys 4 gq + r of the tile; scores s = dot / sqrt(hd)
             // (self_attension.cu) divided once here, not by every wave that reads them
-            *reinterpret_cast<float4*>(&s_s[fr][32 * wave + 16 * t + 4 * gq]) =
+            *reinterpret_cast<float4*>(&s_s[fr][16 * TPW * wave + 16 * t + 4 * gq]) =
                 make_float4(sacc[0] / scale, sacc[1] / scale, sacc[2] / scale, sacc[3] / scale);
         }
         // ---- this wave's V slice -> LDS (the new token's row from kv_new)
@@ -857,9 +913,10 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
     }
     __syncthreads();
     if (!last_flag) return false;
-    // acquire, then plain loads.  Measured alternatives without the fence (sc1 loads of
-    // the write-through partials, MI355X_MICROARCH.md hand-off row 1): 8-B agent-scope
-    // atomic loads 11.4 vs 10.7 us per launch; 16-B sc1 raw buffer loads 73 us.
+    // Default: 16-B sc1 buffer loads on a uniform (SGPR) resource instead of the acquire
+    // (MI355X_MICROARCH.md hand-off row 1): 9.79 -> 9.56 us per launch.  (Round 2 measured
+    // 8-B agent-scope atomic loads at 11.4 vs 10.7 us, and 16-B sc1 loads at 73 us — that
+    // form put the resource in VGPRs, a waterfall loop per load.)
     if (!a.sc1) {
         if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -934,9 +991,9 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
     return true;
 }
 
-template <int HD, bool PG>
-__global__ __launch_bounds__(256) void attn_decode_mfma2_kernel(DecodeAttnParams a) {
-    attn_decode_mfma2_body<HD, PG>(a, blockIdx.x, blockIdx.y);
+template <int HD, bool PG, int NWA, bool PR>
+__global__ __launch_bounds__(64 * NWA) void attn_decode_mfma2_kernel(DecodeAttnParams a) {
+    attn_decode_mfma2_body<HD, PG, NWA, PR>(a, blockIdx.x, blockIdx.y);
 }
 
 
@@ -979,11 +1036,14 @@ static int fill_dec_params(DecodeAttnParams& a, const void* qkv, int64_t B, cons
     const int senv = std::min(dev_env("QIE_DEC_SPLITS", 0), kDecMaxSplits);
     a.splits_target = senv > 0 ? senv : kDecMSplits;
     a.dbg = dev_env("QIE_DEC_DBG", 0);
-    a.sc1 = dev_env("QIE_DEC_SC1", 0);
+    a.sc1 = dev_env("QIE_DEC_SC1", 1);   // 9.79 -> 9.56 us per launch (ctx 2.3k, Qwen2-7B)
     a.nsplit_max = std::min(a.splits_target, (cache->max_ctx + kDecMStep - 1) / kDecMStep);
     QIE_REQUIRE(a.nsplit_max <= kDecMaxSplits, "qie_attention_decode: max_ctx %d too long", cache->max_ctx);
     a.eps = eps;
-    a.numerics = numerics;
+    a.numerics = numerics & QIE_NUMERICS_MASK;
+    a.pre_roped = (numerics & QIE_ATTN_PREROPED) != 0;
+    QIE_REQUIRE(!a.pre_roped || (q_norm == nullptr && k_norm == nullptr && a.numerics == QIE_NUMERICS_REF),
+                "qie_attention_decode: QIE_ATTN_PREROPED needs REF numerics without qk-norm");
     const int64_t cnt = ((B * a.nkv * 4 + 255) / 256) * 256;
     a.counters = (unsigned*)ws;
     a.part_o = (float*)((char*)ws + cnt);
@@ -1103,8 +1163,16 @@ int qie_attention_decode(const void* qkv, int64_t B, const int32_t* pos, const v
                             out, ws));
     dim3 grid((unsigned)(a.nkv * a.nsplit_max), (unsigned)B);
     const bool pg = a.km.table != nullptr;
-    auto k2 = cache->head_dim == 128 ? (pg ? attn_decode_mfma2_kernel<128, true> : attn_decode_mfma2_kernel<128, false>)
-                                     : (pg ? attn_decode_mfma2_kernel<64, true> : attn_decode_mfma2_kernel<64, false>);
+    // hd 128: 8 waves per workgroup (one 16-key S tile and a 16-dim P.V slice per wave);
+    // hd 64 keeps 4 (a 16-dim slice per wave is the MFMA tile's minimum)
+    // 4 waves per workgroup (8 at hd 128, one 16-key tile and a 16-dim P.V slice per wave,
+    // measured slower: 12.9 vs 9.8 us per launch at ctx 2.3k)
+    const bool pr = a.pre_roped != 0;
+    auto k2 = cache->head_dim == 128
+                  ? (pr ? (pg ? attn_decode_mfma2_kernel<128, true, 4, true> : attn_decode_mfma2_kernel<128, false, 4, true>)
+                        : (pg ? attn_decode_mfma2_kernel<128, true, 4, false> : attn_decode_mfma2_kernel<128, false, 4, false>))
+                  : (pr ? (pg ? attn_decode_mfma2_kernel<64, true, 4, true> : attn_decode_mfma2_kernel<64, false, 4, true>)
+                        : (pg ? attn_decode_mfma2_kernel<64, true, 4, false> : attn_decode_mfma2_kernel<64, false, 4, false>));
     hipLaunchKernelGGL(k2, grid, dim3(256), 0, (hipStream_t)stream, a);
     QIE_LAUNCH_CHECK();
     return 0;

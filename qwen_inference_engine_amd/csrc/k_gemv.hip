@@ -48,7 +48,22 @@ struct GemvParams {
     int64_t n_tasks;
     int dbg;           // skinny kernel timing experiments (QIE_SKINNY_DBG): 1 plain x copy instead of the
                        // fused norm, 2 stop after the prologue, 4 no prologue at all
+    // interleaved RoPE in the STORE epilogue (decode QKV, M = 1, REF numerics, no qk-norm):
+    // output rows [0, rope_rows) are (q | k) head rows of rope_hd; pair (2j, 2j + 1) of a
+    // head is rotated by the fp32 table row of position rope_pos[0] (RoPE.cu:6-22)
+    const int32_t* rope_pos;
+    const float* rope_cs;
+    const float* rope_sn;
+    int rope_hd;
+    int64_t rope_rows;
 };
+
+// uniform loads through the scalar cache (constant address space): the RoPE coefficients
+// wait on lgkmcnt, not behind the weight stream's in-order vmcnt
+template <class T>
+__device__ __forceinline__ T sload(const T* p, int64_t i) {
+    return ((const __attribute__((address_space(4))) T*)p)[i];
+}
 
 __device__ __forceinline__ void fma8(float& acc, const float* xf, u32x4 w) {
     acc = fmaf(xf[0], bf_lo(w.x), acc);
@@ -80,13 +95,22 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint16_t* xs = reinterpret_cast<uint16_t*>(smem);
     float* red = reinterpret_cast<float*>(smem + (p.xlds ? (size_t)MT * p.K * 2 : 0));
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // wave index made provably wave-uniform: every task / row pointer below derives from
+    // it, so the weight rows' buffer resources stay in SGPRs
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int NWv = blockDim.x >> 6;         // waves per block: 4, or 5..9 for the one-block-per-CU grid
     const int64_t TS = (int64_t)blockDim.x * 8;   // x elements per block-wide 16-byte pass
     const int64_t K = p.K;
     constexpr int EB = WT ? 1 : 2;     // bytes per weight
     constexpr int EL = 16 / EB;        // weights per 16-byte lane load
     constexpr int WS = 64 * EL;        // weights per wave-load
+    // Weight rows and x are read with buffer loads: one VGPR offset per lane plus a constant
+    // per chunk (no 64-bit address per chunk), and a chunk past the row end (K not a multiple
+    // of a wave-load) reads zeros from the hardware range check instead of a clamped re-read.
+    auto rsrc = [](const void* base, int64_t bytes) {
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+    };
+    constexpr int kNT = 2;   // buffer-load cache policy: nt (weights stream once)
 
     // ---------------- task -> weight rows / output columns
     auto task_ptrs = [&](int64_t task, const u32x4* (&wr)[RPW]) {
@@ -145,14 +169,23 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
     // weight chunk multiplies together with that chunk (L1/L2 hits: every wave of the
     // block reads the same row), so no prologue or barrier precedes the weight stream.
     uint4 xg[XCH == 1 ? U : 1];
+    // XCH == 3 (MT = 1, fused RMSNorm, K <= 512 U): the 64 lanes of a wave load all of x
+    // between them (U 16-B chunks per lane), so every wave reduces the sum of squares itself
+    // (wave_sum, no cross-wave exchange); wave w then normalises chunks w, w + NW, ... into
+    // LDS — one barrier in all, instead of the x-first prologue's two around a block reduction.
+    uint4 xr[XCH == 3 ? U : 1];
     auto load_chunk = [&](const u32x4* const (&wr)[RPW], int64_t k0, u32x4 (&wv)[U][RPW]) {
+        const int voff = (int)(k0 * EB);   // this lane's byte offset in the row (< 2^31)
+        const auto rx = rsrc(p.x, K * 2);
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const int64_t k = k0 + u * WS;
-            if constexpr (XCH == 1) xg[u] = *reinterpret_cast<const uint4*>(p.x + (k < K ? k : K - EL));
+            if constexpr (XCH == 1) {
+                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(k0 * 2), u * WS * 2, 0);
+                xg[u] = make_uint4(v.x, v.y, v.z, v.w);
+            }
 #pragma unroll
-            for (int i = 0; i < RPW; i++)   // unconditional (clamped) loads: see below
-                wv[u][i] = __builtin_nontemporal_load(wr[i] + ((k < K ? k : K - EL) / EL));
+            for (int i = 0; i < RPW; i++)   // unconditional loads (a chunk past K reads zeros)
+                wv[u][i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc(wr[i], K * EB), voff, u * WS * EB, kNT);
         }
     };
     auto x_at = [&](int m, int64_t k) -> uint4 {
@@ -201,6 +234,11 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
 
     const int64_t tstride = (int64_t)gridDim.x * NWv;
     const int64_t task0 = (int64_t)blockIdx.x * NWv + wave;
+    // RoPE epilogue: the position goes out first (one scalar load), its table row for the
+    // first task after the prologue, so neither round trip lands after the weight stream
+    constexpr bool ROPE = EPI == QIE_EPI_STORE && RPW % 2 == 0 && MT == 1;
+    const bool rope = ROPE && p.rope_rows > 0;
+    int32_t rpos = 0;   // loaded right after the first weight issue (an lgkmcnt wait before it would hold the issue)
     const u32x4* wr[RPW];
     u32x4 wv[U][RPW];
     constexpr bool PF = XCH > 0;
@@ -208,6 +246,72 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
     if constexpr (XCH == 1) {
         task_ptrs(task0 < p.n_tasks ? task0 : p.n_tasks - 1, wr);
         load_chunk(wr, (int64_t)lane * EL, wv);
+    } else if constexpr (XCH == 3) {
+        // x chunks first, then the wave's first weight chunks, THEN the norm arithmetic
+        // (vmcnt retires in order: the x loads must be the older ones)
+        const auto rx = rsrc(p.x, K * 2), rn = rsrc(p.norm_w, K * 2);
+#pragma unroll
+        for (int u = 0; u < U; u++) {   // a chunk past K reads zeros (range check)
+            const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rx, lane * 16, u * 1024, 0);
+            xr[u] = make_uint4(a.x, a.y, a.z, a.w);
+        }
+        // the norm weights of the (at most NWC) chunks this wave normalises, also before the
+        // weight stream: a load issued after it could only be waited for behind all of it
+        constexpr int NWC = (U + 3) / 4;   // chunks per wave at >= 4 waves per block
+        u32x4 nvw[NWC];
+#pragma unroll
+        for (int c = 0; c < NWC; c++) {
+            const int u = wave + c * NWv;   // wave-uniform; past U: a harmless in-range re-read
+            nvw[c] = __builtin_amdgcn_raw_buffer_load_b128(rn, lane * 16, (u < U ? u : 0) * 1024, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        task_ptrs(task0 < p.n_tasks ? task0 : p.n_tasks - 1, wr);
+        load_chunk(wr, (int64_t)lane * EL, wv);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < U; u++)   // opaque: the x math cannot be hoisted above the weight issue
+            asm volatile("" : "+v"(xr[u].x), "+v"(xr[u].y), "+v"(xr[u].z), "+v"(xr[u].w));
+#pragma unroll
+        for (int c = 0; c < NWC; c++) asm volatile("" : "+v"(nvw[c]));
+        float ss = 0.f;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            float f[8];
+            unpack8(u32x4{xr[u].x, xr[u].y, xr[u].z, xr[u].w}, f);
+#pragma unroll
+            for (int j = 0; j < 8; j++) ss += f[j] * f[j];
+        }
+        ss = wave_sum(ss);
+        const float rms = sqrtf((ss / (float)K) + p.eps);
+        const float inv = 1.0f / rms;
+        const bool hf = p.numerics == QIE_NUMERICS_HF;
+        const int nch = (int)((K + WS - 1) / WS);
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int c = 0; c < NWC; c++) {   // static indices into xr / nvw: no scratch
+#pragma clang fp contract(off)
+            if (u != wave + c * NWv || u >= nch) continue;   // wave-uniform
+            float f[8], wf[8];
+            unpack8(u32x4{xr[u].x, xr[u].y, xr[u].z, xr[u].w}, f);
+            unpack8(nvw[c], wf);
+            uint32_t o[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                float y0, y1;
+                if (hf) {
+                    y0 = wf[2 * j] * rbf(f[2 * j] * inv);
+                    y1 = wf[2 * j + 1] * rbf(f[2 * j + 1] * inv);
+                } else {
+                    y0 = (f[2 * j] / rms) * wf[2 * j];
+                    y1 = (f[2 * j + 1] / rms) * wf[2 * j + 1];
+                }
+                o[j] = pack2(y0, y1);
+            }
+            const int64_t k = (int64_t)lane * EL + u * WS;
+            if (k < K) *reinterpret_cast<uint4*>(xs + k) = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+        __syncthreads();
     } else if constexpr (XCH > 0) {
         // ---------------- x-first prologue (MT = 1, x staged in LDS, K <= 2048 * XCH; the
         // host guarantees it).  Order of issue: this thread's x chunks (+ norm weights),
@@ -229,6 +333,8 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
         // branch makes the vmcnt bookkeeping at the join wait for everything
         task_ptrs(task0 < p.n_tasks ? task0 : p.n_tasks - 1, wr);
         load_chunk(wr, (int64_t)lane * EL, wv);
+        __builtin_amdgcn_sched_barrier(0);
+        if (rope) rpos = sload(p.rope_pos, 0);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int c = 0; c < XCH; c++) {   // opaque: x math cannot be hoisted above the weight issue
@@ -344,6 +450,20 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
         }
         __syncthreads();
     }
+    if constexpr (XCH == 0 || XCH == 1 || XCH == 3)   // prologues without the early position load
+        if (rope) rpos = sload(p.rope_pos, 0);
+    float rc[ROPE ? RPW / 2 : 1], rs[ROPE ? RPW / 2 : 1];
+    auto rope_coef = [&](int64_t task, float* c_out, float* s_out) {
+#pragma unroll
+        for (int i = 0; i < (ROPE ? RPW / 2 : 0); i++) {
+            const int64_t c = task * RPW + 2 * i;   // STORE: rows of a task are consecutive
+            const int64_t j = (int64_t)rpos * (p.rope_hd / 2) + (c % p.rope_hd) / 2;
+            const bool ok = c + 1 < p.rope_rows;
+            c_out[i] = ok ? sload(p.rope_cs, j) : 1.f;
+            s_out[i] = ok ? sload(p.rope_sn, j) : 0.f;
+        }
+    };
+    if (rope) rope_coef(task0 < p.n_tasks ? task0 : 0, rc, rs);
 
     // Running arg-max key per row (lane 0 of each wave); reduced over the block and
     // published with ONE atomicMax per block after the task loop — an atomic per task
@@ -422,17 +542,39 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
                     }
                 } else {
                     unsigned long long best = kbest[m];
+                    float vv[RPW];
 #pragma unroll
                     for (int i = 0; i < RPW; i++) {
-                        const int64_t c = col[i];
-                        if (c >= p.N) continue;
+                        const int64_t c = col[i] < p.N ? col[i] : p.N - 1;
                         float v = acc[m][i];
                         const uint16_t* b = c < p.n0 ? p.b0 : (c < p.n01 ? p.b1 : p.b2);
                         if (b) {
                             int64_t bi = c < p.n0 ? c : (c < p.n01 ? c - p.n0 : c - p.n01);
                             v = v + bf2f(b[bi]);
                         }
-                        uint16_t o = f2bf(v);
+                        vv[i] = rbf(v);   // the projection's bf16 output
+                    }
+                    if constexpr (ROPE) {
+                        if (rope) {   // uniform: (2j, 2j + 1) pairs of q / k head rows
+                            float tc[RPW / 2], ts[RPW / 2];
+                            if (task != task0) rope_coef(task, tc, ts);
+#pragma unroll
+                            for (int i = 0; i < RPW / 2; i++) {
+                                const int64_t c = col[2 * i];
+                                if (c + 1 >= p.rope_rows || c + 1 >= p.N) continue;
+                                const float cs = task == task0 ? rc[i] : tc[i];
+                                const float sn = task == task0 ? rs[i] : ts[i];
+                                const float x0 = vv[2 * i], x1 = vv[2 * i + 1];
+                                vv[2 * i] = x0 * cs - x1 * sn;
+                                vv[2 * i + 1] = x1 * cs + x0 * sn;
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int i = 0; i < RPW; i++) {
+                        const int64_t c = col[i];
+                        if (c >= p.N) continue;
+                        uint16_t o = f2bf(vv[i]);
                         yr[c] = o;
                         if (p.keys) {
                             unsigned long long kk = sel_key(bf2f(o), (uint32_t)(c + p.key_col0));
@@ -492,7 +634,7 @@ __global__ __launch_bounds__(NW * 64) void skinny_mfma_kernel(GemvParams p) {
     // distinct LDS banks (an unpadded 7168-B row stride maps every row to one bank)
     const int64_t KP = K + 8;
     uint16_t* xs = reinterpret_cast<uint16_t*>(smem);
-    float* red = reinterpret_cast<float*>(smem + (XL ? (size_t)M * KP * 2 : 0));            // [NW][NB][256]
+    float* red = reinterpret_cast<float*>(smem + (XL ? (size_t)M * KP * 2 : 0));            // [NW - 1][NB][256]
     __shared__ unsigned long long kb_s[16];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int fr = lane & 15, g = lane >> 4;
@@ -653,11 +795,13 @@ __global__ __launch_bounds__(NW * 64) void skinny_mfma_kernel(GemvParams p) {
     // epilogue by wave 0.  The barriers wait on LDS only (no vmcnt), so the prefetched
     // next step stays in flight.
     auto tile_end = [&](const Step& st) {
+        // waves 1.. publish (wave 0 keeps its partial in registers: NW - 1 tiles of LDS,
+        // which keeps config 4's staged gate/up launch within 64 KiB of dynamic LDS)
+        if (wave > 0) {
 #pragma unroll
-        for (int b = 0; b < NB; b++) {
-            *reinterpret_cast<float4*>(&red[(wave * NB + b) * 256 + lane * 4]) =
-                make_float4(acc[b][0], acc[b][1], acc[b][2], acc[b][3]);
-            acc[b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+            for (int b = 0; b < NB; b++)
+                *reinterpret_cast<float4*>(&red[((wave - 1) * NB + b) * 256 + lane * 4]) =
+                    make_float4(acc[b][0], acc[b][1], acc[b][2], acc[b][3]);
         }
         __syncthreads();
         if (wave == 0) {
@@ -668,9 +812,9 @@ __global__ __launch_bounds__(NW * 64) void skinny_mfma_kernel(GemvParams p) {
 #pragma unroll
                 for (int r = 0; r < 4; r++)
                 {
-                    float t = red[b * 256 + lane * 4 + r];
+                    float t = acc[b][r];   // same order as before: wave 0, then 1 .. NW - 1
 #pragma unroll
-                    for (int w = 1; w < NW; w++) t += red[(w * NB + b) * 256 + lane * 4 + r];
+                    for (int w = 1; w < NW; w++) t += red[((w - 1) * NB + b) * 256 + lane * 4 + r];
                     c[b][r] = t;
                 }
             if constexpr (WT != 0) {
@@ -705,6 +849,8 @@ __global__ __launch_bounds__(NW * 64) void skinny_mfma_kernel(GemvParams p) {
                 }
             }
         }
+#pragma unroll
+        for (int b = 0; b < NB; b++) acc[b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
         __syncthreads();   // red[] reused by the next tile
     };
 
@@ -889,8 +1035,10 @@ static int launch_gemv_t(const GemvParams& p, hipStream_t st, int blocks_per_cu)
     // CU streams the same rows.  (SwiGLU and lm_head have > 9 tasks per CU: grid-stride.)
     int threads = 256;
     const int64_t cus = device_cu_count();
+    // one row per wave: up to 16 waves per block (Qwen2-7B O / down: 14 one-row waves per CU)
+    constexpr int LBB = RPW == 1 ? 1024 : kGemvBalancedThreads;
     if (MT == 1 && WT == 0 && EPI != QIE_EPI_SWIGLU && blocks_per_cu < 0 && p.n_tasks > 4 * cus &&
-        p.n_tasks <= (kGemvBalancedThreads / 64) * cus &&
+        p.n_tasks <= (LBB / 64) * cus &&
         env_int_gemv("QIE_GEMV_BALANCED", 1) != 0) {
         const int64_t nw = (p.n_tasks + cus - 1) / cus;
         threads = (int)(64 * nw);
@@ -899,7 +1047,7 @@ static int launch_gemv_t(const GemvParams& p, hipStream_t st, int blocks_per_cu)
     const unsigned grid = (unsigned)grid64;
     if (threads > 256) {
         if constexpr (MT == 1 && WT == 0 && EPI != QIE_EPI_SWIGLU) {
-            const void* fb = (const void*)gemv_kernel<MT, RPW, EPI, U, XCH, WT, kGemvBalancedThreads>;
+            const void* fb = (const void*)gemv_kernel<MT, RPW, EPI, U, XCH, WT, LBB>;
             if (shm > 65536) {
                 static bool raised_b = false;
                 if (!raised_b) {
@@ -907,8 +1055,7 @@ static int launch_gemv_t(const GemvParams& p, hipStream_t st, int blocks_per_cu)
                     raised_b = true;
                 }
             }
-            hipLaunchKernelGGL((gemv_kernel<MT, RPW, EPI, U, XCH, WT, kGemvBalancedThreads>), dim3(grid), dim3(threads),
-                               shm, st, p);
+            hipLaunchKernelGGL((gemv_kernel<MT, RPW, EPI, U, XCH, WT, LBB>), dim3(grid), dim3(threads), shm, st, p);
             QIE_LAUNCH_CHECK();
             return 0;
         }
@@ -920,6 +1067,10 @@ static int launch_gemv_t(const GemvParams& p, hipStream_t st, int blocks_per_cu)
 
 template <int MT, int XCH, int WT = 0, int UO = 0>
 static int launch_gemv_m(const GemvParams& p, int rpw, int epi, hipStream_t st, int bpc) {
+    if constexpr (MT == 1 && XCH == 1 && WT == 0) {   // one row per wave (O / down, x beside the weights)
+        if (rpw == 1 && epi == QIE_EPI_RESIDUAL) return launch_gemv_t<1, 1, QIE_EPI_RESIDUAL, 1, 0, UO>(p, st, bpc);
+        if (rpw == 1 && epi == QIE_EPI_STORE) return launch_gemv_t<1, 1, QIE_EPI_STORE, 1, 0, UO>(p, st, bpc);
+    }
     if (epi == QIE_EPI_SWIGLU) {
         return rpw >= 4 ? launch_gemv_t<MT, 4, QIE_EPI_SWIGLU, XCH, WT, UO>(p, st, bpc)
                         : launch_gemv_t<MT, 2, QIE_EPI_SWIGLU, XCH, WT, UO>(p, st, bpc);
@@ -945,6 +1096,11 @@ static int launch_gemv_1(const GemvParams& p, int rpw, int epi, hipStream_t st, 
     const int64_t n = (p.K + 511) / 512;   // bf16 wave-loads per row
     const bool vocab = p.n_tasks * rpw >= 65536;
     const int64_t ub = (n + (n + 7) / 8 - 1) / ((n + 7) / 8);   // balanced slots per pass (<= 8)
+    if (xch == 3) {   // fused norm, x in registers: one batch of wave-loads covers a row
+        if (n <= 2) return launch_gemv_m<1, 3, 0, 2>(p, rpw, epi, st, bpc);
+        if (n == 7 && !vocab) return launch_gemv_m<1, 3, 0, 7>(p, rpw, epi, st, bpc);
+        return launch_gemv_m<1, 3, 0, 8>(p, rpw, epi, st, bpc);
+    }
     if (xch == 2 && n <= 2) return launch_gemv_m<1, 2, 0, 2>(p, rpw, epi, st, bpc);
     if (xch == 2 && n == 7 && !vocab) return launch_gemv_m<1, 2, 0, 7>(p, rpw, epi, st, bpc);
     if (xch == 5 && (n == 9 || n == 10) && !vocab) return launch_gemv_m<1, 5, 0, 5>(p, rpw, epi, st, bpc);
@@ -970,7 +1126,8 @@ template <int EPI, int WT, int XL, int NW, int UO = 0>
 static int launch_skinny_x(const GemvParams& p, hipStream_t st) {
     constexpr int NB = EPI == QIE_EPI_SWIGLU ? 2 : 1;
     const void* fn = (const void*)skinny_mfma_kernel<EPI, WT, XL, NW, UO>;
-    const size_t shm = (p.xlds ? (size_t)p.M * (p.K + 8) * 2 : 0) + (size_t)NW * NB * 256 * 4;
+    // reduction tiles: NW - 1 partial C tiles per B tile (>= 64 floats for the norm prologue)
+    const size_t shm = (p.xlds ? (size_t)p.M * (p.K + 8) * 2 : 0) + (size_t)std::max(NW - 1, 1) * NB * 256 * 4;
     if (shm > 65536) {
         static bool raised = false;
         if (!raised) {
@@ -1023,6 +1180,32 @@ static int launch_skinny(const GemvParams& p, int epi, bool fp8w, hipStream_t st
 }
 static bool K_fits(int64_t K, int xch) { return K <= 2048 * (int64_t)xch && K % 8 == 0; }
 
+// RoPE for the next gemv() call only (gemv_rope); thread-local: engines on other host
+// threads (tensor-parallel ranks) enqueue concurrently
+struct RopeArgs {
+    const int32_t* pos = nullptr;
+    const float* cs = nullptr;
+    const float* sn = nullptr;
+    int hd = 0;
+    int64_t rows = 0;
+};
+static thread_local RopeArgs g_rope;
+
+int gemv(const qie_linear_args* a, hipStream_t st);
+
+// Decode QKV projection (M = 1, REF numerics, no qk-norm) with the interleaved RoPE of its q
+// and k rows fused into the STORE epilogue (RoPE.cu:6-22 on the projection's bf16 output):
+// the decode attention then takes q / k as they are (qie_attention_decode, QIE_ATTN_PREROPED).
+int gemv_rope(const qie_linear_args* a, const int32_t* pos, const float* cs, const float* sn, int hd,
+              int64_t rows, hipStream_t st) {
+    QIE_REQUIRE(a->M == 1 && a->epilogue == QIE_EPI_STORE && rows % 2 == 0 && hd % 2 == 0 && pos && cs && sn,
+                "gemv_rope: M = 1 STORE projections only");
+    g_rope = RopeArgs{pos, cs, sn, hd, rows};
+    const int rc = gemv(a, st);
+    g_rope = RopeArgs{};
+    return rc;
+}
+
 int gemv(const qie_linear_args* a, hipStream_t st) {
     GemvParams p;
     p.x = (const uint16_t*)a->x;
@@ -1046,6 +1229,11 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
     p.keys = (unsigned long long*)a->argmax_keys;
     p.key_col0 = a->key_col0;
     p.dbg = 0;
+    p.rope_pos = g_rope.pos;
+    p.rope_cs = g_rope.cs;
+    p.rope_sn = g_rope.sn;
+    p.rope_hd = g_rope.hd;
+    p.rope_rows = g_rope.rows;
     if (a->M >= 2 && a->M <= 16 && env_int("QIE_SKINNY_MFMA", 1) != 0) {
         const bool fp8w = (a->flags & QIE_LINEAR_FP8) != 0;
         const int kstep = 64;
@@ -1059,6 +1247,13 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
             // fp8: O 9.7 -> 7.8 us, down 26.4 -> 24.6; bf16 O 11.6 -> 10.1, QKV 16.5 -> 15.3)
             const int64_t n_tiles = (a->N + 15) / 16;
             p.xlds = lds_ok && (a->norm_w || n_tiles > 2 * (int64_t)device_cu_count()) ? 1 : 0;
+            // Without a fused norm the staged copy is only an optimisation: keep the launch's
+            // dynamic LDS within the default 64 KiB (no raised kernel attribute).  r02's config-4
+            // gate/up node (8 rows x 3,592 + two 4-KiB reduction tiles per wave = 65,664 B) was
+            // the one decode-graph node above it, and rocprofv3's kernel trace crashed on that
+            // graph only; with NW - 1 reduction tiles it is 63,616 B and stays staged.
+            const size_t staged = (size_t)a->M * (a->K + 8) * 2 + (a->epilogue == QIE_EPI_SWIGLU ? 2 : 1) * 3072;
+            if (p.xlds && !a->norm_w && staged > 65536 && env_int("QIE_SKINNY_LDS64", 1) != 0) p.xlds = 0;
             const int fx = env_int("QIE_SKINNY_XL", -1);
             if (fx >= 0) p.xlds = fx && lds_ok ? 1 : 0;
             p.dbg = env_int("QIE_SKINNY_DBG", 0);
@@ -1105,6 +1300,17 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
         if (p.norm_w) xch = K_fits(a->K, 2) ? 2 : (K_fits(a->K, 5) ? 5 : 0);
         else xch = K_fits(a->K, 2) ? 2 : (K_fits(a->K, 10) ? 10 : 0);
     }
+    // Fused norm with a per-wave sum of squares (XCH 3) where one batch of <= 8 wave-loads
+    // covers a row (K <= 4,096, K % 8 == 0: Qwen2-7B QKV / gate/up / lm_head at K = 3,584,
+    // Qwen2-0.5B at 896): no block reduction, one barrier before the weight stream.
+    // Measured (tools/ubench.py, Qwen2-7B): lm_head 175.3 -> 167.4 us; QKV (9.14 vs 9.67) and
+    // gate/up (42.7 vs 43.8) are faster with the x-first prologue's one-chunk-per-thread x
+    // loads, so only the vocabulary projection takes it.
+    const bool vocab_rows = rows >= 65536;
+    if (MT == 1 && p.M == 1 && p.norm_w && a->K % 8 == 0 && a->K <= 4096 &&
+        env_int("QIE_GEMV_XREG", vocab_rows ? 1 : 0) != 0) {
+        xch = 3;
+    }
     // Batch-1 GEMVs without a fused norm on the one-block-per-CU grid (one row task per
     // wave: Qwen2-7B O, down) read x from L2 beside each weight chunk (XCH = 1) instead of
     // staging it in LDS behind a barrier: Qwen2-7B decode 355 -> 358 tok/s (two A/B rounds),
@@ -1117,6 +1323,14 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
         p.n_tasks <= (kGemvBalancedThreads / 64) * (int64_t)cus && env_int_gemv("QIE_GEMV_BALANCED", 1) != 0) {
         xch = 1;
         p.xlds = 0;
+        // one row per wave, up to 16 waves per CU, where x is short (each wave re-reads all of x
+        // from L2): Qwen2-7B O 6.68 -> 6.45 us; down (x 37.9 KB, K = 18,944) doubled its L2
+        // traffic for x that way (23.3 -> 25.1 us), so it keeps two rows per wave
+        if ((a->epilogue == QIE_EPI_RESIDUAL || a->epilogue == QIE_EPI_STORE) && rows <= 16 * (int64_t)cus &&
+            a->K <= 4096 && env_int("QIE_GEMV_RPW1", 1) != 0) {
+            rpw = 1;
+            p.n_tasks = rows;
+        }
     }
     QIE_REQUIRE(!(xch == 10 && p.norm_w), "qie_linear: internal: fused norm routed to a variant without one");
     switch (MT) {

@@ -125,6 +125,44 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const uint4* __restrict__ 
     for (int64_t i = threadIdx.x; i < H8; i += 256) yr[i] = rms_apply8(xr[i], w[i], rms, inv, numerics);
 }
 
+// H <= 2048 V: the row and the norm weights stay in registers, both loaded up front (one
+// round trip instead of the loop form's two; the batched decode runs it twice per layer)
+template <int V>
+__global__ __launch_bounds__(256) void rmsnorm_reg_kernel(const uint4* __restrict__ x, const uint4* __restrict__ w,
+                                                          uint4* __restrict__ y, int64_t H, float eps, int numerics) {
+    __shared__ float red[4];
+    const int64_t H8 = H / 8;
+    const uint4* xr = x + blockIdx.x * H8;
+    uint4* yr = y + blockIdx.x * H8;
+    uint4 xv[V], wv[V];
+#pragma unroll
+    for (int c = 0; c < V; c++) {
+        const int64_t i = threadIdx.x + 256 * c;
+        const int64_t ic = i < H8 ? i : H8 - 1;   // clamped: loads stay unconditional
+        xv[c] = xr[ic];
+        wv[c] = w[ic];
+    }
+    float ss = 0.f;
+#pragma unroll
+    for (int c = 0; c < V; c++) {
+        if (threadIdx.x + 256 * c >= H8) continue;
+        const uint32_t a[4] = {xv[c].x, xv[c].y, xv[c].z, xv[c].w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            float l = bf_lo(a[j]), h = bf_hi(a[j]);
+            ss += l * l + h * h;
+        }
+    }
+    ss = block_sum_256(ss, red);
+    const float rms = sqrtf((ss / (float)H) + eps);
+    const float inv = 1.0f / rms;
+#pragma unroll
+    for (int c = 0; c < V; c++) {
+        const int64_t i = threadIdx.x + 256 * c;
+        if (i < H8) yr[i] = rms_apply8(xv[c], wv[c], rms, inv, numerics);
+    }
+}
+
 // ------------------------------------------- q/k post-projection + KV append
 // Block per row, one wave per head.  Each lane owns one RoPE pair:
 //   REF: (2*lane, 2*lane+1) interleaved (RoPE.cu:12-18)
@@ -445,6 +483,15 @@ __global__ void fp8_decode_probe_kernel(float* out) {
     for (int j = 0; j < 4; j++) out[4 * b + j] = f[j];
 }
 
+__global__ void fp8_decode_bf16_probe_kernel(uint16_t* out) {
+    const uint32_t b = threadIdx.x;   // 64 threads x 4 codes, through the MFMA GEMV's decode
+    const uint2 v = fp8x4_to_bf16x4((4 * b) | ((4 * b + 1) << 8) | ((4 * b + 2) << 16) | ((4 * b + 3) << 24));
+    out[4 * b] = (uint16_t)(v.x & 0xffff);
+    out[4 * b + 1] = (uint16_t)(v.x >> 16);
+    out[4 * b + 2] = (uint16_t)(v.y & 0xffff);
+    out[4 * b + 3] = (uint16_t)(v.y >> 16);
+}
+
 __global__ __launch_bounds__(256) void synth_slice_kernel(uint16_t* __restrict__ out, int64_t rows, int64_t cols,
                                                           int64_t full_cols, int64_t row0, int64_t col0,
                                                           uint64_t base, float scale, float offset) {
@@ -600,8 +647,11 @@ int qie_rmsnorm(const void* x, const void* w, void* y, int64_t rows, int64_t H, 
     QIE_REQUIRE(x && w && y && rows >= 0 && H > 0 && H % 8 == 0 && x != y,
                 "qie_rmsnorm: bad arguments");
     if (rows == 0) return 0;
-    hipLaunchKernelGGL(rmsnorm_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream,
-                       (const uint4*)x, (const uint4*)w, (uint4*)y, H, eps, numerics);
+    const int64_t v = (H / 8 + 255) / 256;   // 16-B vectors per thread
+    auto fn = v <= 1 ? rmsnorm_reg_kernel<1> : v <= 2 ? rmsnorm_reg_kernel<2> : v <= 4 ? rmsnorm_reg_kernel<4>
+                                                                                     : rmsnorm_kernel;
+    hipLaunchKernelGGL(fn, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, (const uint4*)x, (const uint4*)w,
+                       (uint4*)y, H, eps, numerics);
     QIE_LAUNCH_CHECK();
     return 0;
 }
@@ -820,6 +870,14 @@ int qie_quantize_fp8_host(const void* w_bf16, int64_t rows, int64_t cols, void* 
 int qie_debug_fp8_decode(float* out_dev) {
     QIE_REQUIRE(out_dev, "qie_debug_fp8_decode: null output");
     hipLaunchKernelGGL(fp8_decode_probe_kernel, dim3(1), dim3(64), 0, (hipStream_t)0, out_dev);
+    QIE_LAUNCH_CHECK();
+    QIE_HIP(hipDeviceSynchronize());
+    return 0;
+}
+
+int qie_debug_fp8_decode_bf16(uint16_t* out_dev) {
+    QIE_REQUIRE(out_dev, "qie_debug_fp8_decode_bf16: null output");
+    hipLaunchKernelGGL(fp8_decode_bf16_probe_kernel, dim3(1), dim3(64), 0, (hipStream_t)0, out_dev);
     QIE_LAUNCH_CHECK();
     QIE_HIP(hipDeviceSynchronize());
     return 0;

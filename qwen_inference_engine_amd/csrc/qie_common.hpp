@@ -136,10 +136,13 @@ __device__ __forceinline__ void fp8x4_to_f32(uint32_t w, float* f) {
 // the exact fp32 conversion, then one v_cvt_pk_bf16_f32 per pair.  (The one-step
 // v_cvt_scalef32_pk_bf16_fp8 does not reproduce the subnormal codes: the fp8 engine test
 // against the dequantised oracle model fails with it.)
+// Two codes -> two bf16 per instruction (gfx950 v_cvt_scalef32_pk_bf16_fp8, scale 1.0):
+// every e4m3 value is a bf16, so the convert is exact (all 256 codes are checked against
+// the e4m3fn table by qie_debug_fp8_decode_bf16); half the VALU of fp8 -> f32 -> bf16.
 __device__ __forceinline__ uint2 fp8x4_to_bf16x4(uint32_t w) {
-    const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8((int)w, false);
-    const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8((int)w, true);
-    return make_uint2(pack2(lo[0], lo[1]), pack2(hi[0], hi[1]));
+    const auto lo = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)w, 1.0f, false);
+    const auto hi = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)w, 1.0f, true);
+    return make_uint2(__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi));
 }
 
 // A uniform pointer as an opaque register value: per-lane selects between

@@ -33,6 +33,19 @@ def test_fp8_decode_all_codes(qlib):
     assert np.isnan(got[~ok]).all()
 
 
+def test_fp8_decode_bf16_all_codes(qlib):
+    """The MFMA GEMV's one-instruction decode (v_cvt_scalef32_pk_bf16_fp8, scale 1.0) gives
+    the bf16 of every finite e4m3fn code bit-exactly (each is exactly a bf16), NaN for NaN."""
+    out = G.zeros((256,), np.uint16)
+    G.check(qlib.qie_debug_fp8_decode_bf16(G.p(out)))
+    got, want = G.host(out), W.e4m3_table()
+    ok = ~np.isnan(want)
+    assert np.array_equal(got[ok], (want[ok].view(np.uint32) >> 16).astype(np.uint16))
+    assert (want[ok].view(np.uint32) & 0xffff == 0).all()
+    nan = got[~ok]
+    assert ((nan & 0x7f80) == 0x7f80).all() and ((nan & 0x7f) != 0).all()
+
+
 @pytest.mark.parametrize("rows,cols", [(7, 64), (33, 896), (5, 18944)])
 def test_quantize_device_equals_host(oracle, qlib, rows, cols):
     w = rand_bf16(oracle, (rows, cols), 0.05, seed=rows)

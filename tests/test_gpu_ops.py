@@ -423,3 +423,44 @@ def test_attention_decode_fused(oracle, qlib, hd, qkn, num, nq, nkv):
             d = np.abs(G.bf(got[b]) - G.bf(want[0]))
             assert d.max() <= 2 ** -7 * max(1.0, np.abs(G.bf(want[0])).max()) * 2, f"ctx {ctxs[b]}: {d.max()}"
     assert not G.host(ws)[:B * nkv * 4].any()
+
+
+@pytest.mark.parametrize("hd", [64, 128])
+def test_attention_decode_pre_roped(oracle, qlib, hd):
+    """QIE_ATTN_PREROPED: q / new k arrive rotated (the QKV projection's RoPE epilogue);
+    the kernel only appends and attends.  Same cache rows and outputs as the fused form."""
+    nq, nkv, L, layer, maxc = 28, 4, 2, 0, 700
+    ctxs = [1, 129, 300, 700]
+    B = len(ctxs)
+    QD, KD = nq * hd, nkv * hd
+    kc_h = rand_bf16(oracle, (B, L, nkv, maxc, hd), seed=hd + 3)
+    vc_h = rand_bf16(oracle, (B, L, nkv, maxc, hd), seed=hd + 4)
+    qkv = rand_bf16(oracle, (B, QD + 2 * KD), seed=6)
+    pos = np.array(ctxs, np.int32) - 1
+    cs, sn = oracle.rope_table(maxc, hd, 1e6, "ref")
+    q = oracle.rope(qkv[:, :QD].copy(), cs, sn, pos, nq, hd, "ref")
+    k = oracle.rope(qkv[:, QD:QD + KD].copy(), cs, sn, pos, nkv, hd, "ref")
+    v = qkv[:, QD + KD:].copy()
+    pre = np.concatenate([q, k, v], axis=1)
+    ws = G.zeros_bytes(qlib.qie_attention_decode_workspace_bytes(B, nq, nkv, hd, maxc))
+    kc, vc = G.dev(kc_h), G.dev(vc_h)
+    out = G.zeros_bf16(B, QD)
+    c = _cache(kc, vc, L, nkv, hd, maxc, L * nkv * maxc * hd)
+    dcs, dsn, dqkv, dpos = G.dev(cs), G.dev(sn), G.dev(pre), G.dev(pos)
+    G.check(qlib.qie_attention_decode(G.p(dqkv), B, G.p(dpos), None, None, G.p(dcs), G.p(dsn), nq, C.byref(c),
+                                      layer, 1e-6, _lib.QIE_ATTN_PREROPED, G.p(out), G.p(ws), None))
+    got = G.host_bf16(out)
+    hk = G.host_bf16(kc).reshape(B, L, nkv, maxc, hd)
+    hv = G.host_bf16(vc).reshape(B, L, nkv, maxc, hd)
+    for b in range(B):
+        p = pos[b]
+        assert np.array_equal(hk[b, layer, :, p], k[b].reshape(nkv, hd))
+        assert np.array_equal(hv[b, layer, :, p], v[b].reshape(nkv, hd))
+        kk = kc_h[b, layer, :, :p + 1].copy()
+        vv = vc_h[b, layer, :, :p + 1].copy()
+        kk[:, p] = k[b].reshape(nkv, hd)
+        vv[:, p] = v[b].reshape(nkv, hd)
+        want = oracle.attention(q[b:b + 1], kk, vv, nq, nkv, hd, False, 0)
+        d = np.abs(G.bf(got[b]) - G.bf(want[0]))
+        assert d.max() <= 2 ** -7 * max(1.0, np.abs(G.bf(want[0])).max()) * 2, f"ctx {ctxs[b]}: {d.max()}"
+    assert not G.host(ws)[:B * nkv * 4].any()

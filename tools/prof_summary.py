@@ -17,7 +17,13 @@ ROLE = {
     "gemv_kernel<1, 2, 0, 7, 2, 0, 576> [g 256 x 576]": "decode QKV GEMV (+RMSNorm, bias), one block per CU",
     "gemv_kernel<1, 2, 1, 7, 1, 0, 576> [g 256 x 448]": "decode O-proj GEMV (+residual, x from L2), one block per CU",
     "gemv_kernel<1, 2, 0, 8, 2, 0, 256> [g 761 x 256]": "lm_head GEMV (+final RMSNorm, arg-max keys)",
+    "gemv_kernel<1, 2, 0, 8, 3, 0, 256> [g 761 x 256]": "lm_head GEMV (+final RMSNorm per wave, arg-max keys)",
+    "gemv_kernel<1, 1, 1, 7, 1, 0, 1024> [g 256 x 896]": "decode O-proj GEMV (+residual), one row per wave, one block per CU",
+    "gemv_kernel<1, 1, 0, 7, 1, 0, 1024> [g 256 x 896]": "bench live timing of O-proj (store epilogue)",
     "attn_decode_mfma2_kernel<128, false>": "decode attention (fused qk-norm/RoPE/KV append, split-K, in-launch combine)",
+    "attn_decode_mfma2_kernel<128, false, 4, false>": "decode attention (fused RoPE/KV append, split-K, in-launch combine)",
+    "rmsnorm_kernel": "prefill RMSNorm",
+    "qkv_post_kernel<false>": "prefill RoPE + KV-cache write",
     "attn_prefill_mfma2_kernel<128, false>": "prefill flash attention (MFMA, 32 rows/wave)",
     "gemm_big_kernel<2, 256>": "prefill gate/up GEMM (256x256 LDS-DMA, SwiGLU)",
     "gemm_big_kernel<1, 128>": "prefill O / down GEMM (256x128 LDS-DMA, +residual)",
@@ -81,7 +87,12 @@ def in_graph_decode(trace):
     return out
 
 
-def main(tag="r01", src="gpurun_out/prof"):
+HEADLINE = ("`rocprofv3 --kernel-trace --stats --output-format csv -- python3 bench.py --steps 64 --warmup 4 "
+            "--prefill-iters 1 --no-cpu-baseline` (Qwen2-7B bf16, batch 1, prompt 2048; prefill x2 + 4 warm-up + "
+            "64 timed hipGraph decode steps + bench's live kernel timings).")
+
+
+def main(tag="r01", src="gpurun_out/prof", desc=HEADLINE, how="tools/gpu_check.sh PROFILE=1"):
     src = os.path.join(ROOT, src)
     trace = list(csv.DictReader(open(os.path.join(src, "run_kernel_trace.csv"))))
     groups = collections.defaultdict(list)
@@ -94,10 +105,7 @@ def main(tag="r01", src="gpurun_out/prof"):
         groups[key].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     total = sum(sum(v) for v in groups.values())
     lines = [f"# rocprofv3 kernel summary ({tag})", "",
-             "Command (tools/gpu_check.sh PROFILE=1, one MI355X):",
-             "`rocprofv3 --kernel-trace --stats --output-format csv -- python3 bench.py --steps 64 --warmup 4 "
-             "--prefill-iters 1 --no-cpu-baseline` (Qwen2-7B bf16, batch 1, prompt 2048; prefill x2 + 4 warm-up + "
-             "64 timed hipGraph decode steps + bench's live kernel timings).", "",
+             f"Command ({how}, one MI355X):", desc, "",
              "| kernel | role | calls | avg us | median us | total ms | % |", "|---|---|---|---|---|---|---|"]
     for name, v in sorted(groups.items(), key=lambda kv: -sum(kv[1])):
         lines.append(f"| `{name}` | {ROLE.get(name, '')} | {len(v)} | {statistics.mean(v):.2f} | "

@@ -29,6 +29,7 @@ int gemv(const qie_linear_args* a, hipStream_t st);
 int gemv_rope(const qie_linear_args* a, const int32_t* pos, const float* cs, const float* sn, int hd, int64_t rows,
               hipStream_t st);
 int gemm(const qie_linear_args* a, hipStream_t st);
+bool dec8_applies(const qie_linear_args* a);
 }  // namespace qie
 
 
@@ -405,6 +406,7 @@ static int row_parallel(qie_batch* b, qie_linear_args& a, uint16_t* x, float* pa
 static int prenorm(qie_batch* b, qie_linear_args& a, int64_t M) {
     static const int on = dev_env("QIE_PRENORM", 1);
     if (!on || M < 2 || M > 16 || !a.norm_w) return 0;
+    if (dec8_applies(&a) && dev_env("QIE_DEC8_PRENORM", 0) == 0) return 0;   // the fp8 batched-decode kernel fuses the norm
     QIE_TRY(qie_rmsnorm(a.x, a.norm_w, b->xn, M, a.K, a.norm_eps, a.numerics, b->e->stream));
     a.x = b->xn;
     a.ldx = a.K;

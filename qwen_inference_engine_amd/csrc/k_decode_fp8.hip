@@ -1,0 +1,566 @@
+// k_decode_fp8.hip — batched decode projections on fp8 weights (2 <= M <= 16 rows).
+//
+// Replaces matrix_mul (layers/src/matrix_mul.cu:165-288) for the batched decode step of
+// BASELINE config 4 (Qwen2-7B, e4m3 weights with a power-of-two row scale, batch 8), plus
+// the launch_rms that precedes the QKV and gate/up projections (normalization.cu:5-25).
+//
+// The general skinny kernel (k_gemv.hip skinny_mfma_kernel) re-reads its A fragments (the
+// M activation rows) from LDS or L2 for every 64-k unit of every column tile and merges
+// its waves' partial tiles behind two barriers per tile; at config 4 it was issue-bound
+// (16 VALU per MFMA, 47 % of wave-cycles waiting for issue, profiles/r02_pmc_skinny_b8.txt).
+// Here the work is laid out so that the loop is only loads, conversions and MFMAs:
+//   * a block of KS waves owns whole 16-column tiles; wave w owns the SAME K slice
+//     [w·KU·64, (w+1)·KU·64) of every tile, so its A fragments (16 rows × its K slice,
+//     KU·2 16-B vectors per lane) are loaded ONCE per launch and stay in registers;
+//   * the RMSNorm is fused: the block's waves together hold every row's whole K range, so
+//     the sum of squares is one wave reduction + one LDS exchange, and each wave
+//     normalises its own fragments in registers (no qie_rmsnorm launch in front);
+//   * weights: one 16-B buffer load per lane per 64-k unit (16 e4m3 codes of one row;
+//     lanes 16g..16g+15 = rows, g = k quarter), issued one tile ahead (two register sets),
+//     non-temporal; one v_cvt_scalef32_pk_bf16_fp8 per code pair, two
+//     v_mfma_f32_16x16x32_bf16 per unit (rows ≥ M are padding, never stored);
+//   * the KS partial C tiles meet in a double-buffered LDS area: ONE barrier per tile,
+//     the epilogue (row scale, bias / residual / SwiGLU / fp32 / arg-max keys) by a wave
+//     that rotates with the tile so no wave carries every epilogue.
+// Numerics: the dequantised products (e4m3 × 2^k is exact in bf16) accumulate in fp32 per
+// wave over its K slice, the KS slices are added in wave order, times the row scale; the
+// epilogues round exactly as the reference's separate kernels (bf16 after each op).
+#include "qie_common.hpp"
+#include "../../include/qie/qie_ops.h"
+
+#include <algorithm>
+#include <type_traits>
+
+namespace qie {
+
+typedef unsigned int d8_u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 d8_bf16x8 __attribute__((ext_vector_type(8)));
+typedef float d8_f32x4 __attribute__((ext_vector_type(4)));
+
+struct Dec8Params {
+    const uint16_t* x;         // [M][ldx] bf16 activation rows
+    int64_t ldx;
+    const uint16_t* norm_w;    // fused RMSNorm weights (null: rows used as they are)
+    float eps;
+    int numerics;
+    const uint8_t* w[3];       // segment bases: [rows][K] e4m3 codes, then rows fp32 scales
+    const uint16_t* bias[3];   // per segment, may be null
+    int32_t seg_rows[3];
+    int32_t t01[2];            // tiles in segment 0, in segments 0 + 1
+    int32_t K, N, M;
+    int32_t n_tiles;
+    uint16_t* y;               // [M][ldy] (fp32 for QIE_EPI_F32)
+    int64_t ldy;
+    unsigned long long* keys;  // arg-max keys per row (STORE), may be null
+    int64_t key_col0;
+    int dbg;                   // development build only (QIE_DEC8_DBG): 2 skips the fused norm
+};
+
+// One bf16 pair of qie_rmsnorm's rms_apply8 (k_misc.hip, normalization.cu:18-23).
+// REF: x / rms as q = x * (1 / rms) plus one FMA residual step (Markstein) — the correctly
+// rounded quotient whenever nothing underflows, i.e. for every |x / rms| above 2^-100
+// (smaller non-zero activations may land 1 fp32 ulp off before the bf16 rounding); three
+// VALU ops instead of the ~10 of the IEEE division sequence, which made the fused prologue
+// VALU-bound (13 µs per launch at config 4).  rms = +inf enters as rr = 0, inv = 0, so the
+// quotient is 0 for finite x and NaN for infinite x, as the division gives.
+// HF: w * bf16(x * (1 / rms)).
+template <bool HF>
+__device__ __forceinline__ uint32_t d8_rms_pair(uint32_t xv, uint32_t wv, float rr, float inv) {
+#pragma clang fp contract(off)
+    const float a[2] = {bf_lo(xv), bf_hi(xv)}, w[2] = {bf_lo(wv), bf_hi(wv)};
+    float y[2];
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const float q = a[j] * inv;
+        y[j] = HF ? w[j] * rbf(q) : fmaf(fmaf(-q, rr, a[j]), inv, q) * w[j];
+    }
+    return pack2(y[0], y[1]);
+}
+
+template <int EPI, int KU, int KS>
+__global__ __launch_bounds__(KS * 64) void dec8_kernel(Dec8Params p) {
+#pragma clang fp contract(off)
+    constexpr int NB = EPI == QIE_EPI_SWIGLU ? 2 : 1;   // B tiles per column tile (gate, up)
+    constexpr int kNT = 2;                               // buffer-load policy: nt (streamed once)
+    __shared__ __attribute__((aligned(16))) float red[2][KS][NB][256];
+    __shared__ float ssq[KS][16];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int fr = lane & 15, g = lane >> 4;
+    const int M = p.M, K = p.K, T = p.n_tiles;
+    if ((int)blockIdx.x >= T) return;   // block-uniform, before any barrier
+    const int my = (T - 1 - (int)blockIdx.x) / (int)gridDim.x + 1;
+    const int arow = fr < M ? fr : M - 1;
+    const int kw = wave * (KU * 64);
+
+    // ---- A fragments of this wave's K slice: row arow, k = kw + 64 u + 16 g + [0, 16)
+    d8_u32x4 av[KU][2];
+    {
+        const d8_u32x4* xp = reinterpret_cast<const d8_u32x4*>(p.x + (int64_t)arow * p.ldx + kw + 16 * g);
+#pragma unroll
+        for (int u = 0; u < KU; u++) {
+            av[u][0] = xp[8 * u];
+            av[u][1] = xp[8 * u + 1];
+        }
+    }
+    // this wave's slice of the norm weights: one 16-B load per lane (k = kw + 8 lane), staged
+    // in LDS for the apply below (a register copy per fragment doubled the prologue's
+    // footprint and spilled)
+    __shared__ __attribute__((aligned(16))) d8_u32x4 nw_s[KS][KU * 8];
+    const bool nrm = p.norm_w != nullptr && !QIE_DBG(p.dbg & 2);   // launch-uniform
+    const d8_u32x4 nwv = *reinterpret_cast<const d8_u32x4*>((nrm ? p.norm_w : p.x) + kw + 8 * (lane < KU * 8 ? lane : 0));
+
+    // A step = half a tile's units (KH per B tile) of one column tile; two steps are in
+    // flight (double-buffered registers), i.e. one tile of weights per wave ahead
+    constexpr int KH = KU / 2;
+    struct Step {
+        d8_u32x4 wv[NB][KH];
+        float sc[NB];
+        float ep[4];   // residual values (rows 4 g + r) or the bias (ep[0])
+    };
+    // loads of step s: every load unconditional (clamped), so none sits under a branch
+    // (a load under a branch costs a vmcnt(0) at the join)
+    // hf (which half of the tile) is a constant at every call site: the epilogue operands
+    // ride with the second half only
+    auto issue = [&](Step& t, int it, int hf) {
+        const int tile = (int)blockIdx.x + it * (int)gridDim.x;
+        const int sg = NB == 2 ? 0 : (tile < p.t01[0] ? 0 : (tile < p.t01[1] ? 1 : 2));
+        const int tb0 = sg == 0 ? 0 : (sg == 1 ? p.t01[0] : p.t01[1]);
+        const int rows = p.seg_rows[sg];
+        int r = (tile - tb0) * 16 + fr;
+        r = r < rows ? r : rows - 1;
+        const int voff = r * K + kw + 16 * g + hf * (KH * 64);
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+            const uint8_t* base = p.w[NB == 2 ? b : sg];
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), (short)0,
+                                                              (int)((int64_t)rows * (K + 4)), 0x00020000);
+#pragma unroll
+            for (int u = 0; u < KH; u++) t.wv[b][u] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, u * 64, kNT);
+            if (hf) t.sc[b] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, rows * K + r * 4, 0, 0));
+        }
+        if (!hf) return;
+        const int n = tile * 16 + fr;
+        const int nc = n < p.N ? n : p.N - 1;
+        if constexpr (EPI == QIE_EPI_RESIDUAL) {
+#pragma unroll
+            for (int rr = 0; rr < 4; rr++) {
+                const int i = 4 * g + rr < M ? 4 * g + rr : M - 1;
+                t.ep[rr] = bf2f(p.y[(int64_t)i * p.ldy + nc]);
+            }
+        } else if constexpr (EPI == QIE_EPI_STORE) {
+            const uint16_t* bp = p.bias[sg];
+            const float v = bf2f((bp ? bp : p.x)[bp ? r : 0]);
+            t.ep[0] = bp ? v : 0.f;
+        }
+    };
+
+    Step sa, sb;
+    issue(sa, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+
+    // ---- fused RMSNorm: row arow's sum of squares over the whole K (this wave's slice,
+    // the 4 k quarters by lane exchange, the KS slices through LDS), then the fragments are
+    // normalised in place (qie_rmsnorm's arithmetic)
+    if (nrm) {
+        float ss = 0.f;
+#pragma unroll
+        for (int u = 0; u < KU; u++)
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const uint32_t e4[4] = {av[u][h].x, av[u][h].y, av[u][h].z, av[u][h].w};
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const float l = bf_lo(e4[j]), hh = bf_hi(e4[j]);
+                    ss += l * l + hh * hh;
+                }
+            }
+        ss = xor32_sum(xor16_sum(ss));
+        if (g == 0) ssq[wave][fr] = ss;
+        if (lane < KU * 8) nw_s[wave][lane] = nwv;
+        __syncthreads();
+        float tot = 0.f;
+#pragma unroll
+        for (int w = 0; w < KS; w++) tot += ssq[w][fr];
+        const float rms = sqrtf((tot / (float)K) + p.eps);
+        const float inv = 1.0f / rms;
+        const float rr = rms < INFINITY ? rms : 0.f;
+        // the numerics are launch-uniform: one unrolled copy per mode, only one runs
+        auto apply = [&](auto hf) {
+            constexpr bool HF = decltype(hf)::value;
+#pragma unroll
+            for (int u = 0; u < KU; u++)
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const d8_u32x4 nv = nw_s[wave][8 * u + 2 * g + h];   // k = kw + 64 u + 16 g + 8 h
+                    av[u][h].x = d8_rms_pair<HF>(av[u][h].x, nv.x, rr, inv);
+                    av[u][h].y = d8_rms_pair<HF>(av[u][h].y, nv.y, rr, inv);
+                    av[u][h].z = d8_rms_pair<HF>(av[u][h].z, nv.z, rr, inv);
+                    av[u][h].w = d8_rms_pair<HF>(av[u][h].w, nv.w, rr, inv);
+                    // one fragment at a time: left alone the scheduler hoists every
+                    // product of the prologue first and spills
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+        };
+        __builtin_amdgcn_sched_barrier(0);
+        if (p.numerics == QIE_NUMERICS_HF) apply(std::true_type{});
+        else apply(std::false_type{});
+        __builtin_amdgcn_sched_barrier(0);
+    }
+
+    unsigned long long kbest[4] = {0ull, 0ull, 0ull, 0ull};
+    d8_f32x4 acc[NB];
+    auto mma = [&](const Step& t, int hf) {
+        if (hf == 0) {
+#pragma unroll
+            for (int b = 0; b < NB; b++) acc[b] = d8_f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int u = 0; u < KH; u++) {
+            const int ua = hf * KH + u;   // (hf is a compile-time constant at every call)
+            const d8_bf16x8 a0 = __builtin_bit_cast(d8_bf16x8, av[ua][0]);
+            const d8_bf16x8 a1 = __builtin_bit_cast(d8_bf16x8, av[ua][1]);
+#pragma unroll
+            for (int b = 0; b < NB; b++) {
+                const uint2 c0 = fp8x4_to_bf16x4(t.wv[b][u].x), c1 = fp8x4_to_bf16x4(t.wv[b][u].y);
+                const uint2 c2 = fp8x4_to_bf16x4(t.wv[b][u].z), c3 = fp8x4_to_bf16x4(t.wv[b][u].w);
+                const d8_u32x4 lo = d8_u32x4{c0.x, c0.y, c1.x, c1.y};
+                const d8_u32x4 hi = d8_u32x4{c2.x, c2.y, c3.x, c3.y};
+                acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, __builtin_bit_cast(d8_bf16x8, lo), acc[b], 0, 0, 0);
+                acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, __builtin_bit_cast(d8_bf16x8, hi), acc[b], 0, 0, 0);
+            }
+        }
+    };
+    // tile end (after its second step): partial tiles -> LDS, one barrier, epilogue
+    auto finish = [&](const Step& t, int it) {
+        const int buf = it & 1;
+#pragma unroll
+        for (int b = 0; b < NB; b++)
+            *reinterpret_cast<float4*>(&red[buf][wave][b][lane * 4]) = make_float4(acc[b][0], acc[b][1], acc[b][2], acc[b][3]);
+        // one barrier per tile: the next write of red[buf] is two tiles away, behind the
+        // next tile's barrier, which the epilogue wave reaches only after its reads
+        __syncthreads();
+        if (wave != it % KS) return;   // wave-uniform
+        const int tile = (int)blockIdx.x + it * (int)gridDim.x;
+        const int n = tile * 16 + fr;
+        float c[NB][4];
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+            float4 s = *reinterpret_cast<const float4*>(&red[buf][0][b][lane * 4]);
+#pragma unroll
+            for (int w = 1; w < KS; w++) {
+                const float4 v = *reinterpret_cast<const float4*>(&red[buf][w][b][lane * 4]);
+                s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+            }
+            c[b][0] = s.x * t.sc[b];
+            c[b][1] = s.y * t.sc[b];
+            c[b][2] = s.z * t.sc[b];
+            c[b][3] = s.w * t.sc[b];
+        }
+        if (n >= p.N) return;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int i = 4 * g + r;
+            if (i >= M) continue;
+            uint16_t* yr = p.y + (int64_t)i * p.ldy;
+            if constexpr (EPI == QIE_EPI_SWIGLU) {
+                const float gg = rbf(c[0][r]);
+                const float uu = rbf(c[1][r]);
+                const float a = rbf(gg * (1.0f / (1.0f + expf(-gg))));
+                yr[n] = f2bf(uu * a);
+            } else if constexpr (EPI == QIE_EPI_RESIDUAL) {
+                yr[n] = f2bf(t.ep[r] + rbf(c[0][r]));
+            } else if constexpr (EPI == QIE_EPI_F32) {
+                reinterpret_cast<float*>(p.y)[(int64_t)i * p.ldy + n] = c[0][r];
+            } else {
+                const uint16_t o = f2bf(c[0][r] + t.ep[0]);
+                yr[n] = o;
+                if (p.keys) {
+                    const unsigned long long kk = sel_key(bf2f(o), (uint32_t)(n + p.key_col0));
+                    kbest[r] = kk > kbest[r] ? kk : kbest[r];
+                }
+            }
+        }
+    };
+
+    // steps alternate sa (first half of a tile) / sb (second half); the next step is
+    // always issued before this one is computed
+    __builtin_amdgcn_sched_barrier(0);
+    int it = 0;
+    for (; it + 1 < my; it++) {
+        issue(sb, it, 1);
+        mma(sa, 0);
+        issue(sa, it + 1, 0);
+        mma(sb, 1);
+        finish(sb, it);
+    }
+    issue(sb, it, 1);
+    mma(sa, 0);
+    mma(sb, 1);
+    finish(sb, it);
+    if constexpr (EPI == QIE_EPI_STORE) {
+        if (p.keys) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                unsigned long long v = kbest[r];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {   // max over the 16 columns of row 4 g + r
+                    const unsigned long long s = __shfl_xor(v, o, 64);
+                    v = s > v ? s : v;
+                }
+                if (fr == 0 && 4 * g + r < M && v) atomicMax(p.keys + 4 * g + r, v);
+            }
+        }
+    }
+}
+
+// Long-K form (Qwen2-7B down, K = 18,944: the M rows are 303 KB, too many to keep in
+// registers or LDS): the same tile / wave-slice layout, but each 64-k unit's A fragments
+// are loaded from L2 beside its weight vector (the rows were just written by the gate/up
+// launch), in steps of KH units, two steps in flight.  A wave's slice is K / 64 / KS units
+// (37 at 18,944 with 8 waves); the last step of a slice clamps its dead units to the slice's
+// last unit (an L1/L2 re-read, no HBM bytes) and multiplies them by a zero A fragment.
+// No fused norm (the engine's down / O projections have none); RESIDUAL and F32 epilogues.
+template <int EPI, int KH, int KS>
+__global__ __launch_bounds__(KS * 64) void dec8g_kernel(Dec8Params p) {
+#pragma clang fp contract(off)
+    constexpr int kNT = 2;
+    __shared__ __attribute__((aligned(16))) float red[2][KS][256];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int fr = lane & 15, g = lane >> 4;
+    const int M = p.M, K = p.K, T = p.n_tiles;
+    if ((int)blockIdx.x >= T) return;   // block-uniform, before any barrier
+    const int my = (T - 1 - (int)blockIdx.x) / (int)gridDim.x + 1;
+    const int arow = fr < M ? fr : M - 1;
+    const int units = K / 64;
+    const int ub = wave * units / KS, ue = (wave + 1) * units / KS;   // this wave's slice [ub, ue)
+    const int NS = (ue - ub + KH - 1) / KH;                          // steps per tile (wave-uniform)
+    const int S = my * NS;
+    const int rows = p.seg_rows[0];
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p.w[0]), (short)0,
+                                                      (int)((int64_t)rows * (K + 4)), 0x00020000);
+    const uint16_t* xrow = p.x + (int64_t)arow * p.ldx + 16 * g;
+
+    struct Step {
+        d8_u32x4 wv[KH];
+        d8_u32x4 xa[KH][2];
+        float sc;
+        float ep[4];
+    };
+    auto issue = [&](Step& t, int s) {
+        s = s < S ? s : S - 1;
+        const int it = s / NS, j = s - it * NS;
+        const int tile = (int)blockIdx.x + it * (int)gridDim.x;
+        int r = tile * 16 + fr;
+        r = r < rows ? r : rows - 1;
+#pragma unroll
+        for (int u = 0; u < KH; u++) {
+            int uu = ub + j * KH + u;
+            uu = uu < ue ? uu : ue - 1;
+            t.wv[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, r * K + uu * 64 + 16 * g, 0, kNT);
+            const d8_u32x4* xp = reinterpret_cast<const d8_u32x4*>(xrow + uu * 64);
+            t.xa[u][0] = xp[0];
+            t.xa[u][1] = xp[1];
+        }
+        t.sc = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, rows * K + r * 4, 0, 0));
+        if constexpr (EPI == QIE_EPI_RESIDUAL) {
+#pragma unroll
+            for (int rr = 0; rr < 4; rr++) {
+                const int i = 4 * g + rr < M ? 4 * g + rr : M - 1;
+                t.ep[rr] = bf2f(p.y[(int64_t)i * p.ldy + r]);
+            }
+        }
+    };
+    d8_f32x4 acc = d8_f32x4{0.f, 0.f, 0.f, 0.f};
+    // the steps of a tile are j = 0 .. NS - 1; only the last may hold dead units
+    auto mma = [&](const Step& t, int j, bool full) {
+#pragma unroll
+        for (int u = 0; u < KH; u++) {
+            const bool live = full || ub + j * KH + u < ue;
+            const d8_u32x4 z = d8_u32x4{0u, 0u, 0u, 0u};
+            const d8_bf16x8 a0 = __builtin_bit_cast(d8_bf16x8, live ? t.xa[u][0] : z);
+            const d8_bf16x8 a1 = __builtin_bit_cast(d8_bf16x8, live ? t.xa[u][1] : z);
+            const uint2 c0 = fp8x4_to_bf16x4(t.wv[u].x), c1 = fp8x4_to_bf16x4(t.wv[u].y);
+            const uint2 c2 = fp8x4_to_bf16x4(t.wv[u].z), c3 = fp8x4_to_bf16x4(t.wv[u].w);
+            const d8_u32x4 lo = d8_u32x4{c0.x, c0.y, c1.x, c1.y};
+            const d8_u32x4 hi = d8_u32x4{c2.x, c2.y, c3.x, c3.y};
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, __builtin_bit_cast(d8_bf16x8, lo), acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, __builtin_bit_cast(d8_bf16x8, hi), acc, 0, 0, 0);
+        }
+    };
+    auto finish = [&](const Step& t, int it) {
+        const int buf = it & 1;
+        *reinterpret_cast<float4*>(&red[buf][wave][lane * 4]) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        acc = d8_f32x4{0.f, 0.f, 0.f, 0.f};
+        __syncthreads();   // one barrier per tile (double-buffered red, as dec8_kernel)
+        if (wave != it % KS) return;
+        const int n = ((int)blockIdx.x + it * (int)gridDim.x) * 16 + fr;
+        float4 sm = *reinterpret_cast<const float4*>(&red[buf][0][lane * 4]);
+#pragma unroll
+        for (int w = 1; w < KS; w++) {
+            const float4 v = *reinterpret_cast<const float4*>(&red[buf][w][lane * 4]);
+            sm.x += v.x; sm.y += v.y; sm.z += v.z; sm.w += v.w;
+        }
+        const float c[4] = {sm.x * t.sc, sm.y * t.sc, sm.z * t.sc, sm.w * t.sc};
+        if (n >= p.N) return;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int i = 4 * g + r;
+            if (i >= M) continue;
+            if constexpr (EPI == QIE_EPI_RESIDUAL) p.y[(int64_t)i * p.ldy + n] = f2bf(t.ep[r] + rbf(c[r]));
+            else reinterpret_cast<float*>(p.y)[(int64_t)i * p.ldy + n] = c[r];
+        }
+    };
+    auto step = [&](const Step& t, int s) {
+        const int it = s / NS, j = s - it * NS;
+        if (j + 1 < NS) mma(t, j, true);   // wave-uniform
+        else {
+            mma(t, j, false);
+            finish(t, it);
+        }
+    };
+    Step sa, sb;
+    issue(sa, 0);
+    int s = 0;
+    for (; s + 2 < S; s += 2) {
+        issue(sb, s + 1);
+        step(sa, s);
+        issue(sa, s + 2);
+        step(sb, s + 1);
+    }
+    if (S - s == 2) {
+        issue(sb, s + 1);
+        step(sa, s);
+        step(sb, s + 1);
+    } else {
+        step(sa, s);
+    }
+}
+
+template <int EPI, int KH, int KS>
+static int dec8g_launch(const Dec8Params& p, hipStream_t st) {
+    const void* fn = (const void*)dec8g_kernel<EPI, KH, KS>;
+    static int per_cu = 0;
+    if (per_cu == 0) {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, KS * 64, 0) != hipSuccess || nb < 1) nb = 1;
+        per_cu = nb;
+    }
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(p.n_tiles, (int64_t)device_cu_count() * per_cu));
+    hipLaunchKernelGGL((dec8g_kernel<EPI, KH, KS>), dim3(grid), dim3(KS * 64), 0, st, p);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+
+template <int EPI, int KU, int KS>
+static int dec8_launch(const Dec8Params& p, hipStream_t st) {
+    const void* fn = (const void*)dec8_kernel<EPI, KU, KS>;
+    static int per_cu = 0;   // resident blocks per CU (one per instantiation, cached)
+    if (per_cu == 0) {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, KS * 64, 0) != hipSuccess || nb < 1) nb = 1;
+        per_cu = nb;
+    }
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(p.n_tiles, (int64_t)device_cu_count() * per_cu));
+    hipLaunchKernelGGL((dec8_kernel<EPI, KU, KS>), dim3(grid), dim3(KS * 64), 0, st, p);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+
+template <int KU, int KS>
+static int dec8_epi(const Dec8Params& p, int epi, hipStream_t st) {
+    switch (epi) {
+        case QIE_EPI_SWIGLU: return dec8_launch<QIE_EPI_SWIGLU, KU, KS>(p, st);
+        case QIE_EPI_RESIDUAL: return dec8_launch<QIE_EPI_RESIDUAL, KU, KS>(p, st);
+        case QIE_EPI_F32: return dec8_launch<QIE_EPI_F32, KU, KS>(p, st);
+        default: return dec8_launch<QIE_EPI_STORE, KU, KS>(p, st);
+    }
+}
+
+// K slice shapes: (units per wave KU, waves KS) with KU * KS * 64 = K
+static bool dec8_shape(int64_t K, int* ku, int* ks) {
+    if (K % 64 != 0) return false;
+    const int64_t units = K / 64;
+    static const int shapes[][2] = {{8, 7}, {8, 8}, {2, 7}, {4, 8}, {8, 4}};
+    for (const auto& s : shapes)
+        if ((int64_t)s[0] * s[1] == units) {
+            *ku = s[0];
+            *ks = s[1];
+            return true;
+        }
+    return false;
+}
+
+// true when dec8_linear takes this projection (the engine then skips its separate norm)
+bool dec8_applies(const qie_linear_args* a) {
+    if (!(a->flags & QIE_LINEAR_FP8) || a->M < 2 || a->M > 16) return false;
+    if (dev_env("QIE_DEC8", 1) == 0) return false;
+    int ku, ks;
+    // long K without a norm (down): the A-from-L2 form; otherwise a register-slice shape
+    const bool long_k = a->K % 64 == 0 && a->K >= 8 * 64 * 8 && !a->norm_w &&
+                        (a->epilogue == QIE_EPI_RESIDUAL || a->epilogue == QIE_EPI_F32) && a->seg_rows[1] <= 0;
+    if (!dec8_shape(a->K, &ku, &ks) && !long_k) return false;
+    // vocabulary-sized projections (tens of tiles per block) keep the general skinny kernel:
+    // its 16 waves per CU keep more bytes in flight than one 7-wave block (lm_head 119 vs 194 µs)
+    if (a->N <= 0 || a->N > 32768 || a->ldx % 8 != 0 || a->K >= (1 << 20)) return false;
+    if (a->epilogue != QIE_EPI_SWIGLU) {
+        // column tiles must not straddle segments
+        if (a->seg_rows[0] % 16 != 0 || (a->seg_rows[1] > 0 && (a->seg_rows[0] + a->seg_rows[1]) % 16 != 0))
+            return false;
+    }
+    // every segment's codes + scales must fit a 32-bit buffer range
+    for (int s = 0; s < 3; s++)
+        if ((int64_t)(a->epilogue == QIE_EPI_SWIGLU ? a->N : a->seg_rows[s]) * (a->K + 4) >= (int64_t)1 << 31)
+            return false;
+    return true;
+}
+
+int dec8_linear(const qie_linear_args* a, hipStream_t st) {
+    QIE_REQUIRE(dec8_applies(a), "qie_linear: internal: fp8 batched-decode path does not apply");
+    Dec8Params p;
+    p.x = (const uint16_t*)a->x;
+    p.ldx = a->ldx;
+    p.norm_w = (const uint16_t*)a->norm_w;
+    p.eps = a->norm_eps;
+    p.numerics = a->numerics;
+    p.K = (int32_t)a->K;
+    p.N = (int32_t)a->N;
+    p.M = (int32_t)a->M;
+    p.y = (uint16_t*)a->y;
+    p.ldy = a->ldy;
+    p.keys = (unsigned long long*)a->argmax_keys;
+    p.key_col0 = a->key_col0;
+    p.dbg = dev_env("QIE_DEC8_DBG", 0);
+    p.n_tiles = (int32_t)((a->N + 15) / 16);
+    for (int s = 0; s < 3; s++) {
+        p.w[s] = (const uint8_t*)a->w[s];
+        p.bias[s] = (const uint16_t*)a->bias[s];
+    }
+    if (a->epilogue == QIE_EPI_SWIGLU) {
+        p.seg_rows[0] = p.seg_rows[1] = p.seg_rows[2] = (int32_t)a->N;
+        p.t01[0] = p.t01[1] = p.n_tiles;
+    } else {
+        const int64_t r0 = a->seg_rows[0] > 0 ? a->seg_rows[0] : a->N;
+        const int64_t r1 = a->seg_rows[1];
+        p.seg_rows[0] = (int32_t)r0;
+        p.seg_rows[1] = (int32_t)(r1 > 0 ? r1 : 1);
+        p.seg_rows[2] = (int32_t)std::max<int64_t>(1, a->N - r0 - r1);
+        p.t01[0] = (int32_t)(r0 / 16);
+        p.t01[1] = (int32_t)((r0 + r1) / 16);
+        QIE_REQUIRE(r0 + r1 <= a->N && (r1 == 0 || a->w[1]) && (r0 + r1 == a->N || a->w[2]) && a->w[0],
+                    "qie_linear: segment rows do not match the weights");
+    }
+    int ku = 0, ks = 0;
+    if (!dec8_shape(a->K, &ku, &ks)) {   // long K (dec8_applies checked the form)
+        if (a->epilogue == QIE_EPI_F32) return dec8g_launch<QIE_EPI_F32, 4, 8>(p, st);
+        return dec8g_launch<QIE_EPI_RESIDUAL, 4, 8>(p, st);
+    }
+    if (ku == 8 && ks == 7) return dec8_epi<8, 7>(p, a->epilogue, st);
+    if (ku == 8 && ks == 8) return dec8_epi<8, 8>(p, a->epilogue, st);
+    if (ku == 2 && ks == 7) return dec8_epi<2, 7>(p, a->epilogue, st);
+    if (ku == 4 && ks == 8) return dec8_epi<4, 8>(p, a->epilogue, st);
+    return dec8_epi<8, 4>(p, a->epilogue, st);
+}
+
+}  // namespace qie

@@ -183,3 +183,96 @@ def test_fp8_batch8_equals_single(oracle):
                 assert gap <= logit_tol(s_lgs[i][t])
                 flips += 1
     assert flips <= 3
+
+
+@pytest.mark.parametrize("M", [2, 8, 16])
+@pytest.mark.parametrize("K", [896, 3584])
+@pytest.mark.parametrize("num", ["ref", "hf"])
+def test_fp8_batched_decode_kernel(oracle, qlib, M, K, num):
+    """k_decode_fp8.hip (fp8 weights, 2..16 rows, K = 7 wave slices): the fused RMSNorm with
+    the 3-segment QKV-shaped STORE (+bias, arg-max keys), SwiGLU with the norm, the residual
+    and the fp32 epilogue, each against the oracle on the dequantised weights (the bar of
+    test_linear_fused_norm_and_argmax / test_linear_swiglu / test_linear_residual)."""
+    eps = 1e-4 if num == "ref" else 1e-6
+    nf = 0 if num == "ref" else 1
+    x = rand_bf16(oracle, (M, K), seed=M + K)
+    nw = oracle.f32_to_bf16((1 + 0.2 * rng(12).standard_normal(K)).astype(np.float32))
+    # the fused norm itself: identity weights make the STORE output the kernel's normalised
+    # rows; they may round an element 1 ulp away from the oracle's (sum order of the squares,
+    # test_rmsnorm's bar) — the projections below are then checked on the kernel's own rows
+    eye = oracle.f32_to_bf16(np.eye(K, dtype=np.float32))
+    de, _ = _fp8_dev(qlib, eye)
+    ye = G.zeros_bf16(M, K)
+    _linear(qlib, G.dev(x), [(de, K)], [], M, K, K, ye, _lib.QIE_EPI_STORE, norm_w=G.dev(nw), eps=eps, num=nf,
+            flags=_lib.QIE_LINEAR_FP8)
+    xn = G.host_bf16(ye)
+    G.assert_bf16_close(xn, oracle.rmsnorm(x, nw, eps, num), max_ulp=1 if num == "ref" else 2, min_exact=0.98,
+                        what="fused norm")
+    # QKV-shaped: 3 segments with biases, norm fused, arg-max keys
+    n = (512, 128, 128)
+    q = [_fp8_dev(qlib, rand_bf16(oracle, (r, K), 0.05, seed=30 + i)) for i, r in enumerate(n)]
+    bs = [rand_bf16(oracle, (r,), 0.1, seed=40 + i) for i, r in enumerate(n)]
+    N = sum(n)
+    want = np.concatenate([oracle.matmul(xn, dq, b) for (_, dq), b in zip(q, bs)], axis=1)
+    y = G.zeros_bf16(M, N)
+    keys = G.dev(np.zeros(M, np.uint64))
+    _linear(qlib, G.dev(x), [(d, r) for (d, _), r in zip(q, n)], [G.dev(b) for b in bs], M, K, N, y,
+            _lib.QIE_EPI_STORE, norm_w=G.dev(nw), eps=eps, num=nf, keys=keys, flags=_lib.QIE_LINEAR_FP8)
+    got = G.host_bf16(y)
+    scale = np.concatenate([_abs_scale(oracle, xn, dq) for _, dq in q], axis=1)
+    G.assert_sum_close(got, want, scale, what=f"fp8 dec8 store M={M}")
+    ids = G.zeros((M,), np.int32)
+    G.check(qlib.qie_keys_to_ids(G.p(keys), M, G.p(ids), None))
+    for m in range(M):
+        assert G.host(ids)[m] == oracle.argmax(got[m])
+    # SwiGLU with the fused norm
+    I = 640
+    (dg, qg), (du, qu) = _fp8_dev(qlib, rand_bf16(oracle, (I, K), 0.08, seed=7)), \
+        _fp8_dev(qlib, rand_bf16(oracle, (I, K), 0.08, seed=8))
+    want = oracle.silu_mul(oracle.matmul(xn, qg), oracle.matmul(xn, qu))
+    y = G.zeros_bf16(M, I)
+    _linear(qlib, G.dev(x), [(dg, I), (du, I)], [], M, K, I, y, _lib.QIE_EPI_SWIGLU, norm_w=G.dev(nw), eps=eps,
+            num=nf, flags=_lib.QIE_LINEAR_FP8)
+    d = G.ulp_diff(G.host_bf16(y), want)
+    assert (d == 0).mean() > 0.97
+    gs = G.bf(oracle.matmul(xn, qg)).astype(np.float64)
+    u = np.abs(G.bf(oracle.matmul(xn, qu)).astype(np.float64))
+    ill = (np.abs(gs) < 1e-2 * _abs_scale(oracle, xn, qg)) | (u < 1e-2 * _abs_scale(oracle, xn, qu)) | (gs < -4)
+    assert not ((d > 2) & ~ill).any()
+    # residual (O-shaped: N = K) and fp32 partial sums, no norm
+    h = rand_bf16(oracle, (M, K), seed=3)
+    dw, qw = _fp8_dev(qlib, rand_bf16(oracle, (K, K), 0.02, seed=4))
+    res = rand_bf16(oracle, (M, K), seed=5)
+    want = oracle.resadd(res, oracle.matmul(h, qw))
+    yr = G.dev(res)
+    _linear(qlib, G.dev(h), [(dw, K)], [], M, K, K, yr, _lib.QIE_EPI_RESIDUAL, flags=_lib.QIE_LINEAR_FP8)
+    acc = G.bf(oracle.matmul(h, qw)).astype(np.float64)
+    tol = 2.0 ** -7 * (np.abs(acc) + np.abs(G.bf(want))) + 1e-5 * _abs_scale(oracle, h, qw)
+    assert (np.abs(G.bf(G.host_bf16(yr)).astype(np.float64) - G.bf(want)) <= tol).all()
+    yf = G.zeros((M, K), np.float32)
+    _linear(qlib, G.dev(h), [(dw, K)], [], M, K, K, yf, _lib.QIE_EPI_F32, flags=_lib.QIE_LINEAR_FP8)
+    want = oracle.bf16_to_f32(h).astype(np.float64) @ oracle.bf16_to_f32(qw).astype(np.float64).T
+    assert np.abs(G.host(yf) - want).max() <= 1e-5 * _abs_scale(oracle, h, qw).max() + 1e-6
+
+
+@pytest.mark.parametrize("M", [2, 8, 16])
+@pytest.mark.parametrize("K,N", [(4864, 896), (18944, 3584)])
+def test_fp8_batched_decode_long_k(oracle, qlib, M, K, N):
+    """k_decode_fp8.hip dec8g_kernel (fp8, 2..16 rows, long K without a norm: the down
+    projection; K = 4,864 splits unevenly over the 8 wave slices): residual and fp32."""
+    h = rand_bf16(oracle, (M, K), seed=K + M)
+    dw, qw = _fp8_dev(qlib, rand_bf16(oracle, (N, K), 0.02, seed=4))
+    res = rand_bf16(oracle, (M, N), seed=5)
+    want = oracle.resadd(res, oracle.matmul(h, qw))
+    yr = G.dev(res)
+    _linear(qlib, G.dev(h), [(dw, N)], [], M, K, N, yr, _lib.QIE_EPI_RESIDUAL, flags=_lib.QIE_LINEAR_FP8)
+    acc = G.bf(oracle.matmul(h, qw)).astype(np.float64)
+    tol = 2.0 ** -7 * (np.abs(acc) + np.abs(G.bf(want))) + 1e-5 * _abs_scale(oracle, h, qw)
+    got = G.host_bf16(yr)
+    assert (np.abs(G.bf(got).astype(np.float64) - G.bf(want)) <= tol).all()
+    assert (G.ulp_diff(got, want) == 0).mean() > 0.99
+    if M == 8:
+        yf = G.zeros((M, N), np.float32)
+        _linear(qlib, G.dev(h), [(dw, N)], [], M, K, N, yf, _lib.QIE_EPI_F32, flags=_lib.QIE_LINEAR_FP8)
+        want = oracle.bf16_to_f32(h).astype(np.float64) @ oracle.bf16_to_f32(qw).astype(np.float64).T
+        assert np.abs(G.host(yf) - want).max() <= 1e-5 * _abs_scale(oracle, h, qw).max() + 1e-6

@@ -320,7 +320,8 @@ __global__ __launch_bounds__(KS * 64) void dec8_kernel(Dec8Params p) {
 // launch), in steps of KH units, two steps in flight.  A wave's slice is K / 64 / KS units
 // (37 at 18,944 with 8 waves); the last step of a slice clamps its dead units to the slice's
 // last unit (an L1/L2 re-read, no HBM bytes) and multiplies them by a zero A fragment.
-// No fused norm (the engine's down / O projections have none); RESIDUAL and F32 epilogues.
+// No fused norm (the engine's down / O projections have none); RESIDUAL, F32 and STORE
+// (+bias, one segment, no arg-max keys) epilogues.
 template <int EPI, int KH, int KS>
 __global__ __launch_bounds__(KS * 64) void dec8g_kernel(Dec8Params p) {
 #pragma clang fp contract(off)
@@ -370,6 +371,10 @@ __global__ __launch_bounds__(KS * 64) void dec8g_kernel(Dec8Params p) {
                 const int i = 4 * g + rr < M ? 4 * g + rr : M - 1;
                 t.ep[rr] = bf2f(p.y[(int64_t)i * p.ldy + r]);
             }
+        } else if constexpr (EPI == QIE_EPI_STORE) {
+            const uint16_t* bp = p.bias[0];
+            const float v = bf2f((bp ? bp : p.x)[bp ? r : 0]);
+            t.ep[0] = bp ? v : 0.f;
         }
     };
     d8_f32x4 acc = d8_f32x4{0.f, 0.f, 0.f, 0.f};
@@ -409,6 +414,7 @@ __global__ __launch_bounds__(KS * 64) void dec8g_kernel(Dec8Params p) {
             const int i = 4 * g + r;
             if (i >= M) continue;
             if constexpr (EPI == QIE_EPI_RESIDUAL) p.y[(int64_t)i * p.ldy + n] = f2bf(t.ep[r] + rbf(c[r]));
+            else if constexpr (EPI == QIE_EPI_STORE) p.y[(int64_t)i * p.ldy + n] = f2bf(c[r] + t.ep[0]);
             else reinterpret_cast<float*>(p.y)[(int64_t)i * p.ldy + n] = c[r];
         }
     };
@@ -499,7 +505,7 @@ bool dec8_applies(const qie_linear_args* a) {
     int ku, ks;
     // long K without a norm (down): the A-from-L2 form; otherwise a register-slice shape
     const bool long_k = a->K % 64 == 0 && a->K >= 8 * 64 * 8 && !a->norm_w &&
-                        (a->epilogue == QIE_EPI_RESIDUAL || a->epilogue == QIE_EPI_F32) && a->seg_rows[1] <= 0;
+                        a->epilogue != QIE_EPI_SWIGLU && !a->argmax_keys && a->seg_rows[1] <= 0;
     if (!dec8_shape(a->K, &ku, &ks) && !long_k) return false;
     // vocabulary-sized projections (tens of tiles per block) keep the general skinny kernel:
     // its 16 waves per CU keep more bytes in flight than one 7-wave block (lm_head 119 vs 194 µs)
@@ -554,6 +560,7 @@ int dec8_linear(const qie_linear_args* a, hipStream_t st) {
     int ku = 0, ks = 0;
     if (!dec8_shape(a->K, &ku, &ks)) {   // long K (dec8_applies checked the form)
         if (a->epilogue == QIE_EPI_F32) return dec8g_launch<QIE_EPI_F32, 4, 8>(p, st);
+        if (a->epilogue == QIE_EPI_STORE) return dec8g_launch<QIE_EPI_STORE, 4, 8>(p, st);
         return dec8g_launch<QIE_EPI_RESIDUAL, 4, 8>(p, st);
     }
     if (ku == 8 && ks == 7) return dec8_epi<8, 7>(p, a->epilogue, st);

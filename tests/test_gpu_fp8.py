@@ -271,6 +271,11 @@ def test_fp8_batched_decode_long_k(oracle, qlib, M, K, N):
     got = G.host_bf16(yr)
     assert (np.abs(G.bf(got).astype(np.float64) - G.bf(want)) <= tol).all()
     assert (G.ulp_diff(got, want) == 0).mean() > 0.99
+    # STORE + bias (the bench's live timing of this launch uses it)
+    b = rand_bf16(oracle, (N,), 0.1, seed=6)
+    ys = G.zeros_bf16(M, N)
+    _linear(qlib, G.dev(h), [(dw, N)], [G.dev(b)], M, K, N, ys, _lib.QIE_EPI_STORE, flags=_lib.QIE_LINEAR_FP8)
+    G.assert_sum_close(G.host_bf16(ys), oracle.matmul(h, qw, b), _abs_scale(oracle, h, qw), what="long-K store")
     if M == 8:
         yf = G.zeros((M, N), np.float32)
         _linear(qlib, G.dev(h), [(dw, N)], [], M, K, N, yf, _lib.QIE_EPI_F32, flags=_lib.QIE_LINEAR_FP8)

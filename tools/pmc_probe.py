@@ -21,10 +21,15 @@ ORDER = [(0, "gate_up"), (1, "down"), (2, "qkv"), (3, "o"), (4, "lm_head"), (5, 
 
 def main():
     spec = S.PRESETS["Qwen2-7B"]
-    P = 2048
-    eng = Q.Engine(spec, max_ctx=P + 64).init_synthetic(W.SynthParams(seed=0))
-    b = eng.batch(1, P + 64)
-    b.prefill(0, np.random.default_rng(1).integers(0, spec.vocab, P))
+    fp8b8 = os.environ.get("PMC_CONFIG") == "fp8b8"   # BASELINE config 4: fp8 weights, batch 8, prompt 1024
+    P, B = (1024, 8) if fp8b8 else (2048, 1)
+    eng = Q.Engine(spec, max_ctx=P + 64, weight_fp8=fp8b8).init_synthetic(W.SynthParams(seed=0))
+    b = eng.batch(B, P + 64)
+    prompts = np.random.default_rng(1).integers(0, spec.vocab, (B, P))
+    if B > 1:
+        b.prefill_batch(0, prompts)
+    else:
+        b.prefill(0, prompts[0])
     meta = []
     for which, name in ORDER:
         us, by = b.time_kernel(which, ITERS)   # min(L, 4) warm-up + ITERS launches (qie_batch_time_kernel)

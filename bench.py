@@ -216,8 +216,10 @@ def run(a):
         us, by = batch.time_kernel(which, 54)
         kern[name] = {"avg_us": round(us, 3), "bytes": by, "GBps": round(by / us / 1e3, 1)}
     dom = kern["gate_up_gemv"]
-    traffic, traffic_src = (pmc_traffic("gate_up") if spec.name == "Qwen2-7B" and B == 1 and not a.fp8 and tp == 1
-                            else (None, None))
+    # PMC summaries exist for the headline (bf16, B = 1) and config 4 (fp8, B = 8) shapes
+    pmc_tag = ("" if B == 1 and not a.fp8 else "fp8_b8_" if B == 8 and a.fp8 else None) \
+        if spec.name == "Qwen2-7B" and tp == 1 else None
+    traffic, traffic_src = pmc_traffic("gate_up", pmc_tag) if pmc_tag is not None else (None, None)
     avg_ctx = P + (a.steps + 1) / 2.0
     step_bytes = spec.decode_weight_bytes(fp8=a.fp8) + B * spec.kv_bytes_per_position() * avg_ctx
     step_gbs = step_bytes / (ms_step * 1e-3) / 1e9 / tp   # per GPU (TP: each streams ~1/tp of the weights)
@@ -267,13 +269,14 @@ def run(a):
     return 0
 
 
-def pmc_traffic(kernel="gate_up"):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary
-    (profiles/rNN_pmc_traffic.json: rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes over
-    tools/pmc_probe.py, same model / layer / shapes; gfx950 FETCH_SIZE correction applied
+def pmc_traffic(kernel="gate_up", tag=""):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary of this
+    configuration (profiles/rNN_<tag>pmc_traffic.json: rocprofv3 --pmc FETCH_SIZE and
+    WRITE_SIZE passes over tools/pmc_probe.py, same model / layer / shapes — tag "" the
+    headline, "fp8_b8_" config 4 (PMC_CONFIG=fp8b8); gfx950 FETCH_SIZE correction applied
     by tools/pmc_summary.py).  Counters cannot be read from inside this process."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r[0-9][0-9]_{tag}pmc_traffic.json")))
     if not files:
         return None, None
     doc = json.load(open(files[-1]))

@@ -314,151 +314,6 @@ __global__ __launch_bounds__(KS * 64) void dec8_kernel(Dec8Params p) {
     }
 }
 
-// Long-K form (Qwen2-7B down, K = 18,944: the M rows are 303 KB, too many to keep in
-// registers or LDS): the same tile / wave-slice layout, but each 64-k unit's A fragments
-// are loaded from L2 beside its weight vector (the rows were just written by the gate/up
-// launch), in steps of KH units, two steps in flight.  A wave's slice is K / 64 / KS units
-// (37 at 18,944 with 8 waves); the last step of a slice clamps its dead units to the slice's
-// last unit (an L1/L2 re-read, no HBM bytes) and multiplies them by a zero A fragment.
-// No fused norm (the engine's down / O projections have none); RESIDUAL, F32 and STORE
-// (+bias, one segment, no arg-max keys) epilogues.
-template <int EPI, int KH, int KS>
-__global__ __launch_bounds__(KS * 64) void dec8g_kernel(Dec8Params p) {
-#pragma clang fp contract(off)
-    constexpr int kNT = 2;
-    __shared__ __attribute__((aligned(16))) float red[2][KS][256];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int fr = lane & 15, g = lane >> 4;
-    const int M = p.M, K = p.K, T = p.n_tiles;
-    if ((int)blockIdx.x >= T) return;   // block-uniform, before any barrier
-    const int my = (T - 1 - (int)blockIdx.x) / (int)gridDim.x + 1;
-    const int arow = fr < M ? fr : M - 1;
-    const int units = K / 64;
-    const int ub = wave * units / KS, ue = (wave + 1) * units / KS;   // this wave's slice [ub, ue)
-    const int NS = (ue - ub + KH - 1) / KH;                          // steps per tile (wave-uniform)
-    const int S = my * NS;
-    const int rows = p.seg_rows[0];
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p.w[0]), (short)0,
-                                                      (int)((int64_t)rows * (K + 4)), 0x00020000);
-    const uint16_t* xrow = p.x + (int64_t)arow * p.ldx + 16 * g;
-
-    struct Step {
-        d8_u32x4 wv[KH];
-        d8_u32x4 xa[KH][2];
-        float sc;
-        float ep[4];
-    };
-    auto issue = [&](Step& t, int s) {
-        s = s < S ? s : S - 1;
-        const int it = s / NS, j = s - it * NS;
-        const int tile = (int)blockIdx.x + it * (int)gridDim.x;
-        int r = tile * 16 + fr;
-        r = r < rows ? r : rows - 1;
-#pragma unroll
-        for (int u = 0; u < KH; u++) {
-            int uu = ub + j * KH + u;
-            uu = uu < ue ? uu : ue - 1;
-            t.wv[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, r * K + uu * 64 + 16 * g, 0, kNT);
-            const d8_u32x4* xp = reinterpret_cast<const d8_u32x4*>(xrow + uu * 64);
-            t.xa[u][0] = xp[0];
-            t.xa[u][1] = xp[1];
-        }
-        t.sc = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, rows * K + r * 4, 0, 0));
-        if constexpr (EPI == QIE_EPI_RESIDUAL) {
-#pragma unroll
-            for (int rr = 0; rr < 4; rr++) {
-                const int i = 4 * g + rr < M ? 4 * g + rr : M - 1;
-                t.ep[rr] = bf2f(p.y[(int64_t)i * p.ldy + r]);
-            }
-        } else if constexpr (EPI == QIE_EPI_STORE) {
-            const uint16_t* bp = p.bias[0];
-            const float v = bf2f((bp ? bp : p.x)[bp ? r : 0]);
-            t.ep[0] = bp ? v : 0.f;
-        }
-    };
-    d8_f32x4 acc = d8_f32x4{0.f, 0.f, 0.f, 0.f};
-    // the steps of a tile are j = 0 .. NS - 1; only the last may hold dead units
-    auto mma = [&](const Step& t, int j, bool full) {
-#pragma unroll
-        for (int u = 0; u < KH; u++) {
-            const bool live = full || ub + j * KH + u < ue;
-            const d8_u32x4 z = d8_u32x4{0u, 0u, 0u, 0u};
-            const d8_bf16x8 a0 = __builtin_bit_cast(d8_bf16x8, live ? t.xa[u][0] : z);
-            const d8_bf16x8 a1 = __builtin_bit_cast(d8_bf16x8, live ? t.xa[u][1] : z);
-            const uint2 c0 = fp8x4_to_bf16x4(t.wv[u].x), c1 = fp8x4_to_bf16x4(t.wv[u].y);
-            const uint2 c2 = fp8x4_to_bf16x4(t.wv[u].z), c3 = fp8x4_to_bf16x4(t.wv[u].w);
-            const d8_u32x4 lo = d8_u32x4{c0.x, c0.y, c1.x, c1.y};
-            const d8_u32x4 hi = d8_u32x4{c2.x, c2.y, c3.x, c3.y};
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, __builtin_bit_cast(d8_bf16x8, lo), acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, __builtin_bit_cast(d8_bf16x8, hi), acc, 0, 0, 0);
-        }
-    };
-    auto finish = [&](const Step& t, int it) {
-        const int buf = it & 1;
-        *reinterpret_cast<float4*>(&red[buf][wave][lane * 4]) = make_float4(acc[0], acc[1], acc[2], acc[3]);
-        acc = d8_f32x4{0.f, 0.f, 0.f, 0.f};
-        __syncthreads();   // one barrier per tile (double-buffered red, as dec8_kernel)
-        if (wave != it % KS) return;
-        const int n = ((int)blockIdx.x + it * (int)gridDim.x) * 16 + fr;
-        float4 sm = *reinterpret_cast<const float4*>(&red[buf][0][lane * 4]);
-#pragma unroll
-        for (int w = 1; w < KS; w++) {
-            const float4 v = *reinterpret_cast<const float4*>(&red[buf][w][lane * 4]);
-            sm.x += v.x; sm.y += v.y; sm.z += v.z; sm.w += v.w;
-        }
-        const float c[4] = {sm.x * t.sc, sm.y * t.sc, sm.z * t.sc, sm.w * t.sc};
-        if (n >= p.N) return;
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int i = 4 * g + r;
-            if (i >= M) continue;
-            if constexpr (EPI == QIE_EPI_RESIDUAL) p.y[(int64_t)i * p.ldy + n] = f2bf(t.ep[r] + rbf(c[r]));
-            else if constexpr (EPI == QIE_EPI_STORE) p.y[(int64_t)i * p.ldy + n] = f2bf(c[r] + t.ep[0]);
-            else reinterpret_cast<float*>(p.y)[(int64_t)i * p.ldy + n] = c[r];
-        }
-    };
-    auto step = [&](const Step& t, int s) {
-        const int it = s / NS, j = s - it * NS;
-        if (j + 1 < NS) mma(t, j, true);   // wave-uniform
-        else {
-            mma(t, j, false);
-            finish(t, it);
-        }
-    };
-    Step sa, sb;
-    issue(sa, 0);
-    int s = 0;
-    for (; s + 2 < S; s += 2) {
-        issue(sb, s + 1);
-        step(sa, s);
-        issue(sa, s + 2);
-        step(sb, s + 1);
-    }
-    if (S - s == 2) {
-        issue(sb, s + 1);
-        step(sa, s);
-        step(sb, s + 1);
-    } else {
-        step(sa, s);
-    }
-}
-
-template <int EPI, int KH, int KS>
-static int dec8g_launch(const Dec8Params& p, hipStream_t st) {
-    const void* fn = (const void*)dec8g_kernel<EPI, KH, KS>;
-    static int per_cu = 0;
-    if (per_cu == 0) {
-        int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, KS * 64, 0) != hipSuccess || nb < 1) nb = 1;
-        per_cu = nb;
-    }
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(p.n_tiles, (int64_t)device_cu_count() * per_cu));
-    hipLaunchKernelGGL((dec8g_kernel<EPI, KH, KS>), dim3(grid), dim3(KS * 64), 0, st, p);
-    QIE_LAUNCH_CHECK();
-    return 0;
-}
-
 template <int EPI, int KU, int KS>
 static int dec8_launch(const Dec8Params& p, hipStream_t st) {
     const void* fn = (const void*)dec8_kernel<EPI, KU, KS>;
@@ -484,7 +339,8 @@ static int dec8_epi(const Dec8Params& p, int epi, hipStream_t st) {
     }
 }
 
-// K slice shapes: (units per wave KU, waves KS) with KU * KS * 64 = K
+// K slice shapes: (units per wave KU, waves KS) with KU * KS * 64 = K.  7 waves x 8 units at
+// K = 3,584 (14 x 4 measured the same for QKV and 0.45 µs slower for O at config 4).
 static bool dec8_shape(int64_t K, int* ku, int* ks) {
     if (K % 64 != 0) return false;
     const int64_t units = K / 64;
@@ -503,10 +359,7 @@ bool dec8_applies(const qie_linear_args* a) {
     if (!(a->flags & QIE_LINEAR_FP8) || a->M < 2 || a->M > 16) return false;
     if (dev_env("QIE_DEC8", 1) == 0) return false;
     int ku, ks;
-    // long K without a norm (down): the A-from-L2 form; otherwise a register-slice shape
-    const bool long_k = a->K % 64 == 0 && a->K >= 8 * 64 * 8 && !a->norm_w &&
-                        a->epilogue != QIE_EPI_SWIGLU && !a->argmax_keys && a->seg_rows[1] <= 0;
-    if (!dec8_shape(a->K, &ku, &ks) && !long_k) return false;
+    if (!dec8_shape(a->K, &ku, &ks)) return false;
     // vocabulary-sized projections (tens of tiles per block) keep the general skinny kernel:
     // its 16 waves per CU keep more bytes in flight than one 7-wave block (lm_head 119 vs 194 µs)
     if (a->N <= 0 || a->N > 32768 || a->ldx % 8 != 0 || a->K >= (1 << 20)) return false;
@@ -558,11 +411,7 @@ int dec8_linear(const qie_linear_args* a, hipStream_t st) {
                     "qie_linear: segment rows do not match the weights");
     }
     int ku = 0, ks = 0;
-    if (!dec8_shape(a->K, &ku, &ks)) {   // long K (dec8_applies checked the form)
-        if (a->epilogue == QIE_EPI_F32) return dec8g_launch<QIE_EPI_F32, 4, 8>(p, st);
-        if (a->epilogue == QIE_EPI_STORE) return dec8g_launch<QIE_EPI_STORE, 4, 8>(p, st);
-        return dec8g_launch<QIE_EPI_RESIDUAL, 4, 8>(p, st);
-    }
+    dec8_shape(a->K, &ku, &ks);
     if (ku == 8 && ks == 7) return dec8_epi<8, 7>(p, a->epilogue, st);
     if (ku == 8 && ks == 8) return dec8_epi<8, 8>(p, a->epilogue, st);
     if (ku == 2 && ks == 7) return dec8_epi<2, 7>(p, a->epilogue, st);

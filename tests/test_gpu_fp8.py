@@ -258,8 +258,9 @@ def test_fp8_batched_decode_kernel(oracle, qlib, M, K, num):
 @pytest.mark.parametrize("M", [2, 8, 16])
 @pytest.mark.parametrize("K,N", [(4864, 896), (18944, 3584)])
 def test_fp8_batched_decode_long_k(oracle, qlib, M, K, N):
-    """k_decode_fp8.hip dec8g_kernel (fp8, 2..16 rows, long K without a norm: the down
-    projection; K = 4,864 splits unevenly over the 8 wave slices): residual and fp32."""
+    """fp8, 2..16 rows, long K without a norm (the down projection; the skinny MFMA kernel,
+    k_gemv.hip — a long-K form of k_decode_fp8.hip measured no faster and was dropped):
+    residual, STORE + bias and fp32 against the oracle on the dequantised weights."""
     h = rand_bf16(oracle, (M, K), seed=K + M)
     dw, qw = _fp8_dev(qlib, rand_bf16(oracle, (N, K), 0.02, seed=4))
     res = rand_bf16(oracle, (M, N), seed=5)

@@ -54,10 +54,12 @@ def in_graph_decode(trace):
     steps = []
     for a, b in zip(fin, fin[1:]):
         seg = t[a + 1:b + 1]
-        if len(seg) < 7 or (len(seg) - 2) % 5:
-            continue
-        L = (len(seg) - 2) // 5
-        if short(seg[1]["Kernel_Name"]).startswith("attn_decode") is False:
+        # layers: groups of 5 launches whose second is the decode attention; what follows
+        # (optional final norm, lm_head, finalize) is the head
+        L = 0
+        while 5 * L + 1 < len(seg) and short(seg[5 * L + 1]["Kernel_Name"]).startswith("attn_decode"):
+            L += 1
+        if L < 2:
             continue
         steps.append((int(seg[-1]["End_Timestamp"]) - int(t[a]["End_Timestamp"])) / 1e3)
         for i, r in enumerate(seg):
@@ -67,8 +69,12 @@ def in_graph_decode(trace):
                 if i // 5 == 0:
                     continue
                 role = roles[i % 5]
+            elif i == len(seg) - 1:
+                role = "finalize"
+            elif short(r["Kernel_Name"]).startswith("rmsnorm"):
+                role = "final RMSNorm"
             else:
-                role = "lm_head GEMV" if i == 5 * L else "finalize"
+                role = "lm_head GEMV"
             dur[role].append((e0 - s0) / 1e3)
             gap[role].append((s0 - pe) / 1e3)
     if not steps:
@@ -77,8 +83,10 @@ def in_graph_decode(trace):
            "Kernel durations only: under --kernel-trace the profiler serialises graph nodes, so "
            "its inter-kernel gaps (and step spans) are profiler artefacts, not the bench's clock.", "",
            "| role | launches | avg us | median us |", "|---|---|---|---|"]
-    for role in roles + ["lm_head GEMV", "finalize"]:
+    for role in roles + ["final RMSNorm", "lm_head GEMV", "finalize"]:
         v = dur[role]
+        if not v:
+            continue
         out.append(f"| {role} | {len(v)} | {statistics.mean(v):.2f} | {statistics.median(v):.2f} |")
     per_layer = sum(statistics.mean(dur[r]) for r in roles)
     out.append("")

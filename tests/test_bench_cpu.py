@@ -78,3 +78,14 @@ def test_tp_shardable_presets():
     assert [S.shard_heads(28, 4, 8, r)[0] for r in range(8)] == [4, 3, 4, 3, 4, 3, 4, 3]
     assert S.shard_heads(28, 4, 32, 0) is None       # 8 ranks per kv head > its 7 q heads
     assert S.shard_heads(28, 4, 6, 0) is None        # 6 neither divides nor is a multiple of 4
+
+
+def test_pmc_traffic_is_read_from_the_benched_configuration():
+    """bench.py's roofline.traffic comes from the PMC summary of the configuration it ran:
+    the headline (bf16, B = 1) never picks up config 4's (fp8, B = 8) file and vice versa."""
+    sys.path.insert(0, ROOT)
+    import bench
+    head, src = bench.pmc_traffic("gate_up", "")
+    assert src is not None and "fp8" not in src and head > 2.5e8   # 271.6 MB algorithmic
+    fp8, src8 = bench.pmc_traffic("gate_up", "fp8_b8_")
+    assert src8 is not None and "fp8_b8" in src8 and 1.3e8 < fp8 < 1.5e8   # 136.2 MB algorithmic

@@ -32,6 +32,17 @@ ROLE = {
     "gemv_kernel<1, 2, 0, 8, 1, 0, 576> [g 256 x 448]": "bench live timing of down (store epilogue)",
     "gemv_kernel<1, 2, 0, 7, 1, 0, 576> [g 256 x 448]": "bench live timing of O-proj (store epilogue)",
     "synth_kernel": "synthetic weight fill (setup)",
+    # config 4 (fp8 weights, batch 8): k_decode_fp8.hip and the skinny MFMA kernel
+    "dec8_kernel<2, 8, 7>": "fp8 decode gate/up (+fused RMSNorm, SwiGLU)  [dominant]",
+    "dec8_kernel<0, 8, 7>": "fp8 decode QKV (+fused RMSNorm, bias); bench live timing of O (store)",
+    "dec8_kernel<1, 8, 7>": "fp8 decode O-proj (+residual)",
+    "skinny_mfma_kernel<1, 1, 0, 4, 0>": "fp8 decode down (+residual, x from L2)",
+    "skinny_mfma_kernel<0, 1, 0, 4, 0>": "bench live timing of down (store epilogue)",
+    "skinny_mfma_kernel<0, 1, 1, 4, 7>": "fp8 lm_head (rows staged, arg-max keys)",
+    "rmsnorm_reg_kernel<2>": "final RMSNorm (batch head) / prefill RMSNorm",
+    "gemm_kernel<1, 0>": "prefill O / down GEMM (128x128 tiles, +residual)",
+    "quantize_fp8_kernel": "fp8 weight quantisation (setup)",
+    "dequantize_fp8_kernel": "fp8 -> bf16 prefill copy (setup)",
 }
 
 

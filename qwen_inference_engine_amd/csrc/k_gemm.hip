@@ -488,7 +488,8 @@ int gemm(const qie_linear_args* a, hipStream_t st) {
     const unsigned gm = (unsigned)cdiv(a->M, BM);
     QIE_REQUIRE(a->K % 8 == 0, "qie_linear: GEMM needs K %% 8 == 0");
     if (!(a->flags & QIE_LINEAR_FP8) && a->K % big::BK == 0 && a->ldx % 8 == 0) {
-        // LDS-DMA kernel: 256x256 tiles when they fill the chip at least twice over, else
+        // LDS-DMA kernel: 256x256 tiles when they fill the chip at least once (config 4's
+        // O / down at 8,192 rows: 448 tiles; the generic 128x128 kernel took them before), else
         // 256x128 when those fill >= 3/4 of it in one round (Qwen2-7B O and down projections
         // at 2,048 rows: 112 vs 224 tiles on 256 CUs), else 256x256 in one round (below).
         // args.flags QIE_LINEAR_TILE256 / TILE128 force a tile (tests; dev builds also
@@ -499,7 +500,7 @@ int gemm(const qie_linear_args* a, hipStream_t st) {
         const int64_t cus = device_cu_count();
         const int force = (a->flags & QIE_LINEAR_TILE256) ? 1 : (a->flags & QIE_LINEAR_TILE128) ? 2
                                                                                             : dev_env("QIE_GEMM_BIG", -1);
-        if (force == 1 || (force < 0 && a->M >= big::BM && t256 >= 2 * cus))
+        if (force == 1 || (force < 0 && a->M >= big::BM && t256 >= cus))
             return launch_gemm_big<256>(a->epilogue, p, (int)n_mt, (int)t256, st);
         if (force == 2 || (force < 0 && a->M >= big::BM && t128 >= (3 * cus) / 4 && t128 <= cus))
             return launch_gemm_big<128>(a->epilogue, p, (int)n_mt, (int)t128, st);

@@ -304,12 +304,29 @@ def cpu_baseline(spec, a, batch, eng):
     Then the full-depth greedy parity sample (tests/parity.py forced_decisions): the GPU
     and oracle orders 0 / 1 / 2 over --parity-decisions teacher-forced decisions on a
     peaked-head copy of the same weights — a size-independent parity check at full depth."""
+    threads = cpu_threads()
+    # a progress line every minute on stderr: a GPU runner takes minutes of silence for a hang
+    # (the --cpu-full prefill of 2,048 tokens alone runs ~80 s per repetition)
+    import threading
+    t_start = time.perf_counter()
+    stop = threading.Event()
+
+    def beat():
+        while not stop.wait(60.0):
+            print(f"cpu_baseline: {time.perf_counter() - t_start:.0f} s", file=sys.stderr, flush=True)
+    threading.Thread(target=beat, daemon=True).start()
+    try:
+        return _cpu_baseline(spec, a, batch, eng, threads)
+    finally:
+        stop.set()
+
+
+def _cpu_baseline(spec, a, batch, eng, threads):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle as O
     from parity import PEAKED, forced_decisions
     from qwen_inference_engine_amd import spec as S, weights as W
-    threads = cpu_threads()
     # ---- BASELINE config 1: Qwen2-0.5B, P = 16, G = 16, greedy, timed in full
     s05 = S.QWEN2_0_5B
     hw05 = W.HostWeights.synthetic(s05, W.SynthParams(seed=0))

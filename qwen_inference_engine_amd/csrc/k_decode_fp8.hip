@@ -14,10 +14,11 @@
 //     KU·2 16-B vectors per lane) are loaded ONCE per launch and stay in registers;
 //   * the RMSNorm is fused: the block's waves together hold every row's whole K range, so
 //     the sum of squares is one wave reduction + one LDS exchange, and each wave
-//     normalises its own fragments in registers (no qie_rmsnorm launch in front);
+//     normalises its own fragments in registers (no qie_rmsnorm launch in front; the norm
+//     weights are staged in LDS, the quotient is a Markstein step, see d8_rms_pair);
 //   * weights: one 16-B buffer load per lane per 64-k unit (16 e4m3 codes of one row;
-//     lanes 16g..16g+15 = rows, g = k quarter), issued one tile ahead (two register sets),
-//     non-temporal; one v_cvt_scalef32_pk_bf16_fp8 per code pair, two
+//     lanes 16g..16g+15 = rows, g = k quarter), non-temporal, in half-tile steps with
+//     the next step always in flight (two register sets); one v_cvt_scalef32_pk_bf16_fp8 per code pair, two
 //     v_mfma_f32_16x16x32_bf16 per unit (rows ≥ M are padding, never stored);
 //   * the KS partial C tiles meet in a double-buffered LDS area: ONE barrier per tile,
 //     the epilogue (row scale, bias / residual / SwiGLU / fp32 / arg-max keys) by a wave

@@ -67,6 +67,8 @@ def parse(argv=None):
     ap.add_argument("--parallel", choices=["tp", "replicas"], default="tp",
                     help="N > 1: one tensor-parallel sequence (RCCL) or N independent replicas")
     ap.add_argument("--tp", action="store_true", help="(compat) same as --parallel tp")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the other single-GPU BASELINE configs (2 and 4) in the default line")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher only: print the child ranks' environments as JSON and exit (no GPU)")
     return ap.parse_args(argv)
@@ -215,6 +217,14 @@ def run(a):
                         (4, "lm_head_gemv"), (5, "attention")]:
         us, by = batch.time_kernel(which, 54)
         kern[name] = {"avg_us": round(us, 3), "bytes": by, "GBps": round(by / us / 1e3, 1)}
+    # in-graph durations: 8 greedy steps replayed from a capture of the step with an event pair
+    # around every launch (qie_batch_graph_kernel_times), from the prompt end again
+    for s_ in range(B):
+        batch.set_position(s_, P, first[s_])
+    try:
+        in_graph = batch.graph_kernel_times(8)
+    except Exception as ex:   # reported, never fatal for the headline line
+        in_graph = {"error": str(ex)[:200]}
     dom = kern["gate_up_gemv"]
     # PMC summaries exist for the headline (bf16, B = 1) and config 4 (fp8, B = 8) shapes
     pmc_tag = ("" if B == 1 and not a.fp8 else "fp8_b8_" if B == 8 and a.fp8 else None) \
@@ -250,15 +260,21 @@ def run(a):
         "roofline": {"bound": "hbm", "kernel": "gate_up_gemv (rms + gate/up GEMV + SwiGLU, layers 1..L-1)",
                      "achieved": dom["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(dom["GBps"] / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "algorithmic_bytes": dom["bytes"], "traffic_source": traffic_src},
+                     "algorithmic_bytes": dom["bytes"], "traffic_source": traffic_src,
+                     "in_graph": in_graph_frac(in_graph, "gate_up", dom["bytes"])},
         "step_roofline": {"bytes_per_step": step_bytes, "achieved_GBps_per_gpu": round(step_gbs, 1),
                           "frac": round(step_gbs / HBM_PEAK_GBS, 4),
                           "roofline_tok_s": round(HBM_PEAK_GBS * 1e9 * tp / step_bytes * B * (world // tp), 1)},
         "kernels": kern,
+        "kernels_in_graph_us": in_graph,
         "cpu_baseline": None,
     }
     if tp_note:
         out["note"] = tp_note
+    headline = (spec.name == "Qwen2-7B" and B == 1 and P == 2048 and not a.fp8 and not a.page_tokens
+                and world == 1 and not a.no_graph)
+    if rank == 0 and headline and not a.no_configs:
+        out["configs"] = other_configs(Q, S, W)
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.fp8 and B == 1:
         out["cpu_baseline"] = cpu_baseline(spec, a, batch, eng)
     if group:
@@ -267,6 +283,93 @@ def run(a):
     if rank == 0:
         print(json.dumps(out), flush=True)
     return 0
+
+
+def in_graph_frac(in_graph, role, bytes_):
+    """The dominant kernel's in-graph duration against the HBM peak."""
+    us = in_graph.get(role) if isinstance(in_graph, dict) else None
+    if not us or us <= 0:
+        return None
+    gbs = bytes_ / us / 1e3
+    return {"avg_us": us, "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+            "how": "qie_batch_graph_kernel_times: hipEvent pair around the launch inside the captured step, "
+                   "layers 1..L-1, 8 steps"}
+
+
+# BASELINE.json configs[1] and configs[3]: the other single-GPU configurations, timed by the
+# driver's own default bench run (one engine each, after the headline)
+OTHER_CONFIGS = [
+    {"key": "config2", "model": "Qwen2-0.5B", "batch": 1, "prompt": 128, "gen": 128, "fp8": False,
+     "workload": "Qwen2-0.5B bf16, batch=1, prompt=128, gen=128 (BASELINE configs[1])"},
+    {"key": "config4", "model": "Qwen2-7B", "batch": 8, "prompt": 1024, "gen": 256, "fp8": True,
+     "workload": "Qwen2-7B fp8 weights, batch=8, prompt=1024, gen=256 (BASELINE configs[3])"},
+]
+
+
+def other_configs(Q, S, W):
+    res = {}
+    for c in OTHER_CONFIGS:
+        t_cfg = time.perf_counter()
+        try:
+            res[c["key"]] = run_config(Q, S, W, c)
+        except Exception as ex:   # reported in the line, never silently dropped
+            res[c["key"]] = {"workload": c["workload"], "error": str(ex)[:300]}
+        res[c["key"]]["wall_s"] = round(time.perf_counter() - t_cfg, 1)
+    return res
+
+
+def run_config(Q, S, W, c):
+    spec = S.PRESETS[c["model"]]
+    B, P, G = c["batch"], c["prompt"], c["gen"]
+    steps = G - 1                         # the tokens after the prefill's first
+    max_ctx = P + G + 16
+    eng = Q.Engine(spec, max_ctx=max_ctx, weight_fp8=c["fp8"]).init_synthetic(W.SynthParams(seed=0))
+    b = None
+    try:
+        b = eng.batch(B, max_ctx)
+        prompts = np.random.default_rng(1).integers(0, spec.vocab, size=(B, P), dtype=np.int32)
+
+        def prefill():
+            return b.prefill_batch(0, prompts) if B > 1 else [b.prefill(0, prompts[0])]
+        first = prefill()
+        pts = []
+        for _ in range(2):
+            eng.sync()
+            t0 = time.perf_counter()
+            first = prefill()
+            eng.sync()
+            pts.append(time.perf_counter() - t0)
+        t_pf = float(np.median(pts))
+        b.decode(8, want_ids=False)
+        for s_ in range(B):
+            b.set_position(s_, P, first[s_])
+        eng.sync()
+        t0 = time.perf_counter()
+        b.decode(steps, want_ids=False)
+        eng.sync()
+        dt = time.perf_counter() - t0
+        ms = dt * 1e3 / steps
+        for s_ in range(B):
+            b.set_position(s_, P, first[s_])
+        in_graph = b.graph_kernel_times(8)
+        us_dom, by_dom = b.time_kernel(0, 54)
+        step_bytes = spec.decode_weight_bytes(fp8=c["fp8"]) + B * spec.kv_bytes_per_position() * (P + (steps + 1) / 2.0)
+        gbs = step_bytes / (ms * 1e-3) / 1e9
+        return {"workload": c["workload"], "value": round(B * steps / dt, 2), "unit": "tokens/s",
+                "ms_per_step": round(ms, 4), "steps": steps, "prefill_tok_s": round(B * P / t_pf, 1),
+                "prefill_ms": round(t_pf * 1e3, 3),
+                "step_roofline": {"bytes_per_step": step_bytes, "achieved_GBps": round(gbs, 1),
+                                  "frac": round(gbs / HBM_PEAK_GBS, 4),
+                                  "roofline_tok_s": round(HBM_PEAK_GBS * 1e9 / step_bytes * B, 1)},
+                "dominant_kernel": {"kernel": "gate_up (rms + gate/up + SwiGLU)", "live_us": round(us_dom, 3),
+                                    "algorithmic_bytes": by_dom,
+                                    "live_frac": round(by_dom / us_dom / 1e3 / HBM_PEAK_GBS, 4),
+                                    "in_graph": in_graph_frac(in_graph, "gate_up", by_dom)},
+                "kernels_in_graph_us": in_graph}
+    finally:
+        if b is not None:   # the batch before its engine
+            b.close()
+        eng.close()
 
 
 def pmc_traffic(kernel="gate_up", tag=""):

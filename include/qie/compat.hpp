@@ -73,6 +73,12 @@ inline Config& config() {
     static Config c;
     return c;
 }
+// the arena the last reference-form load_all_weights_to_gpu_chunked call filled (the
+// reference-form initialize_model_buffers binds the engine to it)
+inline bf16*& loaded_arena_() {
+    static bf16* p = nullptr;
+    return p;
+}
 inline void check_(int rc, const char* who) {
     if (rc != 0) {
         config().error = rc;
@@ -200,6 +206,7 @@ inline bool load_all_weights_to_gpu_chunked(const std::vector<tensor>& all_tenso
     }
     d_base_out = static_cast<bf16*>(d);
     total_bytes_out = off;
+    loaded_arena_() = d_base_out;
     return true;
 }
 
@@ -591,13 +598,17 @@ inline batch_metadata* new_sequence_(int sequence_id, const int* h_token_ids, in
     return s;
 }
 
+inline void initialize_model_buffers(ModelBuffers& buf, int* h_token_ids, TensorTable& tensors,
+                                     std::ifstream& weights, size_t sequence_len);
+
 // create_new_sequence, reference form (iengine.cu:25-47): the sequence's buffers (dims from
 // config().spec, the prompt); its KV slot is bound by its first llm() call.
 inline batch_metadata* create_new_sequence(int sequence_id, int* h_token_ids, int sequence_len, TensorTable tensors,
                                            std::ifstream& weights) {
-    (void)tensors;
-    (void)weights;
-    return new_sequence_(sequence_id, h_token_ids, sequence_len);
+    batch_metadata* s = new_sequence_(sequence_id, h_token_ids, sequence_len);
+    // as iengine.cu:25-47: the sequence's model buffers, once weights have been loaded
+    if (s && loaded_arena_()) initialize_model_buffers(*s->buffer, h_token_ids, tensors, weights, (size_t)sequence_len);
+    return s;
 }
 
 inline void destroy_sequence(batch_metadata* s) {
@@ -614,6 +625,7 @@ inline int llm_step_(batch_metadata* seq, const qie_sampling* sampling) {
         check_(rc ? rc : -22, who);
         return 0;
     };
+    config().error = 0;   // per call: an earlier failure must not mark this call failed
     if (!seq || !seq->batch || !seq->buffer) return bad(-22, "llm: sequence has no batch slot");
     int32_t tok = -1;
     if (seq->state == prefill) {
@@ -732,6 +744,23 @@ inline int bind_engine_(const TensorTable& tensors, bf16* base) {
     return 0;
 }
 
+// initialize_model_buffers, reference form (utils.hh:90-92, utills.cu:4-129): the sequence's
+// buffers over the engine bound to the arena that load_all_weights_to_gpu_chunked filled last
+// (the reference re-reads the embedding and norm tensors from `weights`; here they are in that
+// arena already).  Returns void as the reference does: failures set config().error.
+inline void initialize_model_buffers(ModelBuffers& buf, int* h_token_ids, TensorTable& tensors,
+                                     std::ifstream& weights, size_t sequence_len) {
+    (void)weights;
+    bf16* base = loaded_arena_();
+    if (!base) {
+        std::fprintf(stderr, "initialize_model_buffers: no weights loaded (load_all_weights_to_gpu_chunked first)\n");
+        config().error = -22;
+        return;
+    }
+    if (bind_engine_(tensors, base) != 0) return;   // reported by bind_engine_
+    if (!initialize_model_buffers(buf, h_token_ids, tensors, driver().engine, sequence_len)) config().error = -22;
+}
+
 // llm, reference form (iengine.cuh:51, qwen_main.cu:64-417): prefill when
 // seq->state == prefill, else ONE decode step fed seq->generated_token; the caller
 // advances step / generated_token / state (iengine.cu:419-421).  The first call binds the
@@ -741,6 +770,7 @@ inline int bind_engine_(const TensorTable& tensors, bf16* base) {
 inline int llm(batch_metadata* seq, TensorTable tensors, std::ifstream& weights, page_table* kv_cache_seq1,
                int page_size, bf16* g_gpu_weights_buffer) {
     (void)weights;
+    config().error = 0;   // per call (0 is also a token id: callers read config().error)
     if (!seq || !seq->buffer || !kv_cache_seq1 || page_size <= 0 || !g_gpu_weights_buffer) {
         check_(-22, "llm: bad arguments");
         return 0;

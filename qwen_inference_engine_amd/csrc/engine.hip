@@ -101,6 +101,7 @@ struct qie_batch {
     uint16_t* vc = nullptr;
     int64_t seq_stride = 0;
     int32_t* d_pos = nullptr;
+    float* d_rope_cur = nullptr;   // [B][rope_cur_stride(hd)]: RoPE row of each slot's current position
     int32_t* d_step = nullptr;
     int32_t* d_hist = nullptr;
     int32_t* d_ids = nullptr;
@@ -139,6 +140,10 @@ struct qie_batch {
     hipGraphExec_t gexec = nullptr;
     qie_sampling gs{};
     bool graph_ok = false;
+    // in-graph kernel probe (qie_batch_graph_kernel_times): while `probe` is set, the
+    // enqueue records an event pair around every launch role of layers 1..L-1 and the head
+    bool probe = false;
+    std::vector<hipEvent_t> pev;   // [(layer, role)][2], roles as qie_batch_time_kernel
 };
 
 namespace qie {
@@ -147,10 +152,31 @@ namespace qie {
 // Step finalisation: chosen id -> token history, position + 1, sample step + 1,
 // next step's input row x_res[m] = E[id] (embedding_matrix_func, decode branch
 // qwen_main.cu:259-268, without the host round trip).
+// The RoPE table row of a slot's current position, kept beside the position (tagged with it)
+// so that the decode attention's prologue loads need not wait for the position
+// (DecodeAttnParams::rc).  Every kernel that sets a position also writes the row.
+struct RopeCurArgs {
+    float* rc;
+    const float* cs;
+    const float* sn;
+    int hd, rows;
+};
+__device__ __forceinline__ void write_rope_cur(const RopeCurArgs& r, int m, int p) {
+    if (!r.rc) return;
+    float* o = r.rc + (int64_t)m * rope_cur_stride(r.hd);
+    const bool ok = p >= 0 && p < r.rows;
+    const int h2 = r.hd / 2;
+    for (int t = threadIdx.x; t < h2; t += blockDim.x) {
+        o[8 + t] = ok ? r.cs[(int64_t)p * h2 + t] : 0.f;
+        o[8 + h2 + t] = ok ? r.sn[(int64_t)p * h2 + t] : 0.f;
+    }
+    if (threadIdx.x == 0) o[0] = __int_as_float(ok ? p : -1);
+}
+
 __global__ __launch_bounds__(256) void finalize_kernel(int m0, unsigned long long* keys, const int32_t* ids_in,
                                                        int32_t* ids_out, int32_t* pos, int32_t* step,
                                                        int32_t* hist, int hist_stride, const uint4* E,
-                                                       uint4* x_res, int64_t H8, int32_t vocab) {
+                                                       uint4* x_res, int64_t H8, int32_t vocab, RopeCurArgs rca) {
     const int m = m0 + blockIdx.x;
     int32_t tok = keys ? key_idx(keys[m]) : ids_in[m];
     const int32_t p = pos[m];
@@ -163,6 +189,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(int m0, unsigned long lon
         step[m] = step[m] + 1;
         ids_out[m] = tok;
     }
+    write_rope_cur(rca, m, p + 1);
     const uint4* src = E + (int64_t)tok * H8;
     uint4* dst = x_res + (int64_t)m * H8;
     for (int64_t i = threadIdx.x; i < H8; i += 256) dst[i] = src[i];
@@ -170,7 +197,8 @@ __global__ __launch_bounds__(256) void finalize_kernel(int m0, unsigned long lon
 
 __global__ void set_state_kernel(int m, int32_t pos_v, int32_t step_v, int32_t tok, int32_t* pos,
                                  int32_t* step, int32_t* hist, int hist_stride, const uint4* E,
-                                 uint4* x_res, int64_t H8, int write_row) {
+                                 uint4* x_res, int64_t H8, int write_row, RopeCurArgs rca) {
+    write_rope_cur(rca, m, pos_v);
     if (threadIdx.x == 0) {
         pos[m] = pos_v;
         step[m] = step_v;
@@ -195,6 +223,11 @@ __global__ void copy_ids_kernel(const int32_t* src, int32_t* dst, int len, int64
 static int dmalloc(void** p, size_t bytes) {
     QIE_HIP(hipMalloc(p, bytes < 16 ? 16 : bytes));
     return 0;
+}
+
+static RopeCurArgs rope_cur_args(const qie_batch* b) {
+    const qie_engine* e = b->e;
+    return RopeCurArgs{b->d_rope_cur, e->rope_cos, e->rope_sin, (int)e->spec.head_dim, e->rope_rows};
 }
 
 // KV descriptor of the batch's sequences seq0.. (kernels see them as sequences 0..)
@@ -422,6 +455,13 @@ static bool rope_in_projection(const qie_batch* b) {
     return b->B == 1 && !s.qk_norm && s.numerics == QIE_NUMERICS_REF && dev_env("QIE_ROPE_IN_PROJ", 0) != 0;
 }
 
+// in-graph probe: event `edge` (0 before, 1 after) of launch role `role` of layer l (l = L: the head)
+static int probe_mark(qie_batch* b, int l, int role, int edge) {
+    if (!b->probe || l == 0) return 0;
+    QIE_HIP(hipEventRecord(b->pev[((size_t)l * 6 + role) * 2 + edge], b->e->stream));
+    return 0;
+}
+
 static int enqueue_layer_decode(qie_batch* b, int l) {
     qie_engine* e = b->e;
     const qie_model_spec& s = e->spec;
@@ -442,18 +482,27 @@ static int enqueue_layer_decode(qie_batch* b, int l) {
     a.norm_w = L.attn_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
     QIE_TRY(prenorm(b, a, B));
     const bool rope_in_proj = rope_in_projection(b);
+    QIE_TRY(probe_mark(b, l, 2, 0));
     if (rope_in_proj) QIE_TRY(gemv_rope(&a, b->d_pos, e->rope_cos, e->rope_sin, (int)hd, QD + KD, st));
     else QIE_TRY(gemv(&a, st));
+    QIE_TRY(probe_mark(b, l, 2, 1));
 
-    QIE_TRY(qie_attention_decode(b->qkv, B, b->d_pos, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, e->sh.nq,
-                                 &cache, l, s.rms_eps, s.numerics | (rope_in_proj ? QIE_ATTN_PREROPED : 0), b->att,
-                                 b->dec_ws, st));
+    set_decode_rope_cur(b->d_rope_cur);
+    QIE_TRY(probe_mark(b, l, 5, 0));
+    const int arc = qie_attention_decode(b->qkv, B, b->d_pos, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, e->sh.nq,
+                                         &cache, l, s.rms_eps, s.numerics | (rope_in_proj ? QIE_ATTN_PREROPED : 0),
+                                         b->att, b->dec_ws, st);
+    set_decode_rope_cur(nullptr);
+    QIE_TRY(arc);
+    QIE_TRY(probe_mark(b, l, 5, 1));
     a = lin_base(e);
     a.x = b->att; a.ldx = QD;
     a.w[0] = L.wo; a.seg_rows[0] = H;
     a.M = B; a.K = QD; a.N = H;
     a.ldy = H;
+    QIE_TRY(probe_mark(b, l, 3, 0));
     QIE_TRY(row_parallel(b, a, b->x_res, b->part, B));
+    QIE_TRY(probe_mark(b, l, 3, 1));
 
     a = lin_base(e);
     a.x = b->x_res; a.ldx = H;
@@ -463,14 +512,18 @@ static int enqueue_layer_decode(qie_batch* b, int l) {
     a.epilogue = QIE_EPI_SWIGLU;
     a.norm_w = L.ffn_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
     QIE_TRY(prenorm(b, a, B));
+    QIE_TRY(probe_mark(b, l, 0, 0));
     QIE_TRY(gemv(&a, st));
+    QIE_TRY(probe_mark(b, l, 0, 1));
 
     a = lin_base(e);
     a.x = b->h; a.ldx = I;
     a.w[0] = L.w_down; a.seg_rows[0] = H;
     a.M = B; a.K = I; a.N = H;
     a.ldy = H;
-    return row_parallel(b, a, b->x_res, b->part, B);
+    QIE_TRY(probe_mark(b, l, 1, 0));
+    QIE_TRY(row_parallel(b, a, b->x_res, b->part, B));
+    return probe_mark(b, l, 1, 1);
 }
 
 static bool is_greedy(const qie_sampling* s) { return !s || s->top_k <= 1 || !(s->temperature > 0.f); }
@@ -517,7 +570,9 @@ static int enqueue_head(qie_batch* b, const uint16_t* x, int64_t ldx, int m0, in
         a.argmax_keys = (uint64_t*)(b->d_keys + m0);
         a.key_col0 = e->sh.vocab0;   // keys carry global vocab ids
     }
+    QIE_TRY(probe_mark(b, s.n_layers, 4, 0));
     QIE_TRY(gemv(&a, st));
+    QIE_TRY(probe_mark(b, s.n_layers, 4, 1));
     if (greedy && use_comm(e)) QIE_TRY(e->comm->allreduce_max_u64((uint64_t*)(b->d_keys + m0), M, st));
     if (!greedy) {
         const uint16_t* lg = b->logits + (int64_t)m0 * Vl;
@@ -529,7 +584,7 @@ static int enqueue_head(qie_batch* b, const uint16_t* x, int64_t ldx, int m0, in
     }
     hipLaunchKernelGGL(finalize_kernel, dim3(M), dim3(256), 0, st, m0, greedy ? b->d_keys : nullptr,
                        b->d_ids, b->d_ids, b->d_pos, b->d_step, b->d_hist, b->max_ctx,
-                       (const uint4*)e->w.embed, (uint4*)b->x_res, (int64_t)s.hidden / 8, s.vocab);
+                       (const uint4*)e->w.embed, (uint4*)b->x_res, (int64_t)s.hidden / 8, s.vocab, rope_cur_args(b));
     QIE_LAUNCH_CHECK();
     return 0;
 }
@@ -965,6 +1020,7 @@ static int batch_create(qie_engine* e, int32_t batch, int32_t max_ctx, int32_t p
     A((void**)&b->vc, (size_t)n_runs * b->seq_stride * 2);
     if (page_tokens > 0) A((void**)&b->d_table, b->h_table.size() * 4);
     A((void**)&b->d_pos, batch * 4);
+    A((void**)&b->d_rope_cur, (size_t)batch * rope_cur_stride((int)hd) * 4);
     A((void**)&b->d_step, batch * 4);
     A((void**)&b->d_hist, (size_t)batch * max_ctx * 4);
     A((void**)&b->d_ids, batch * 4);
@@ -991,6 +1047,7 @@ static int batch_create(qie_engine* e, int32_t batch, int32_t max_ctx, int32_t p
         hipMemsetAsync(b->vc, 0, (size_t)n_runs * b->seq_stride * 2, e->stream);
         hipMemsetAsync(b->d_keys, 0, batch * 8, e->stream);
         hipMemsetAsync(b->d_pos, 0, batch * 4, e->stream);
+        hipMemsetAsync(b->d_rope_cur, 0xff, (size_t)batch * rope_cur_stride((int)hd) * 4, e->stream);   // tags -1
         hipMemsetAsync(b->d_step, 0, batch * 4, e->stream);
         hipMemsetAsync(b->d_ids, 0, batch * 4, e->stream);
         hipMemsetAsync(b->d_hist, 0, (size_t)batch * max_ctx * 4, e->stream);
@@ -1033,7 +1090,7 @@ int qie_batch_release(qie_batch* b, int32_t seq) {
     QIE_TRY(flush_table(b));
     qie_engine* e = b->e;
     hipLaunchKernelGGL(set_state_kernel, dim3(1), dim3(256), 0, e->stream, seq, 0, 0, 0, b->d_pos, b->d_step, b->d_hist,
-                       b->max_ctx, (const uint4*)e->w.embed, (uint4*)b->x_res, (int64_t)e->spec.hidden / 8, 1);
+                       b->max_ctx, (const uint4*)e->w.embed, (uint4*)b->x_res, (int64_t)e->spec.hidden / 8, 1, rope_cur_args(b));
     QIE_LAUNCH_CHECK();
     QIE_HIP(hipStreamSynchronize(e->stream));
     b->h_pos[seq] = 0;
@@ -1061,7 +1118,9 @@ void qie_batch_destroy(qie_batch* b) {
     if (!b) return;
     if (b->e && b->e->stream) hipStreamSynchronize(b->e->stream);
     if (b->gexec) hipGraphExecDestroy(b->gexec);
-    void* ps[] = {b->kc, b->vc, b->d_table, b->d_pos, b->d_step, b->d_hist, b->d_ids, b->d_keys, b->x_res, b->qkv, b->q,
+    for (hipEvent_t ev : b->pev)
+        if (ev) hipEventDestroy(ev);
+    void* ps[] = {b->kc, b->vc, b->d_table, b->d_pos, b->d_rope_cur, b->d_step, b->d_hist, b->d_ids, b->d_keys, b->x_res, b->qkv, b->q,
                   b->att, b->h, b->logits, b->attn_ws, b->dec_ws, b->samp_ws, b->pf_x, b->pf_hn, b->pf_qkv, b->pf_q,
                   b->pf_att, b->pf_h, b->pf_pos, b->pf_ids, b->pf_attn_ws, b->part, b->logits_full,
                   b->gather_tmp, b->pf_part, b->xn};
@@ -1150,7 +1209,7 @@ static int prefill_rows(qie_batch* b, int seq0, int n_seqs, const int32_t* ids, 
     for (int z = 0; z < n_seqs; z++) {
         hipLaunchKernelGGL(set_state_kernel, dim3(1), dim3(64), 0, st, seq0 + z, len - 1, 0,
                            ids[(int64_t)z * len + len - 1], b->d_pos, b->d_step, b->d_hist, b->max_ctx,
-                           (const uint4*)e->w.embed, (uint4*)b->x_res, (int64_t)H / 8, 0);
+                           (const uint4*)e->w.embed, (uint4*)b->x_res, (int64_t)H / 8, 0, rope_cur_args(b));
         QIE_LAUNCH_CHECK();
     }
     const uint16_t* last = b->pf_x + (int64_t)(len - 1) * H;
@@ -1234,7 +1293,7 @@ static int prepare_steps(qie_batch* b, int n_steps, const char* who) {
         if (b->idle[m] && b->h_pos[m] + n_steps >= b->max_ctx) {
             hipLaunchKernelGGL(set_state_kernel, dim3(1), dim3(256), 0, e->stream, m, 0, 0, 0, b->d_pos, b->d_step,
                                b->d_hist, b->max_ctx, (const uint4*)e->w.embed, (uint4*)b->x_res,
-                               (int64_t)e->spec.hidden / 8, 1);
+                               (int64_t)e->spec.hidden / 8, 1, rope_cur_args(b));
             QIE_LAUNCH_CHECK();
             b->h_pos[m] = 0;
         }
@@ -1306,7 +1365,7 @@ int qie_batch_set_position(qie_batch* b, int32_t seq, int32_t pos, int32_t token
     qie_engine* e = b->e;
     hipLaunchKernelGGL(set_state_kernel, dim3(1), dim3(256), 0, e->stream, seq, pos, pos, token, b->d_pos, b->d_step,
                        b->d_hist, b->max_ctx, (const uint4*)e->w.embed, (uint4*)b->x_res,
-                       (int64_t)e->spec.hidden / 8, 1);
+                       (int64_t)e->spec.hidden / 8, 1, rope_cur_args(b));
     QIE_LAUNCH_CHECK();
     QIE_HIP(hipStreamSynchronize(e->stream));
     b->h_pos[seq] = pos;
@@ -1398,7 +1457,9 @@ int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* av
             a.argmax_keys = (uint64_t*)(((uintptr_t)(scratch + B * V) + 7) & ~(uintptr_t)7);   // as the greedy step runs it
             *by = (double)V * H * wb + B * H * 2 + B * (double)V * 2;
         }
-        if (batched_norm && a.norm_w) {
+        // as prenorm() decides for the real step: the fp8 batched-decode kernel keeps its fused norm
+        const bool fused8 = dec8_applies(&a) && dev_env("QIE_DEC8_PRENORM", 0) == 0;
+        if (batched_norm && a.norm_w && !fused8) {
             a.x = b->xn;   // as the batched step runs it: rows normed once by prenorm(), plain GEMV
             a.ldx = a.K;
             a.norm_w = nullptr;
@@ -1419,10 +1480,14 @@ int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* av
         const int l = layer_of(i);
         const qie_layer_weights& L = e->layers[l];
         const bool rp = rope_in_projection(b);
-        if (which == 5)
-            return qie_attention_decode(b->qkv, B, b->d_pos, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, sh.nq,
-                                        &cache, l, s.rms_eps, s.numerics | (rp ? QIE_ATTN_PREROPED : 0), scratch,
-                                        b->dec_ws, e->stream);
+        if (which == 5) {
+            set_decode_rope_cur(b->d_rope_cur);
+            const int rc = qie_attention_decode(b->qkv, B, b->d_pos, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin,
+                                                sh.nq, &cache, l, s.rms_eps, s.numerics | (rp ? QIE_ATTN_PREROPED : 0),
+                                                scratch, b->dec_ws, e->stream);
+            set_decode_rope_cur(nullptr);
+            return rc;
+        }
         double lb = 0;
         qie_linear_args a = args_for(l, &lb);
         if (which == 2 && rp)   // as the step runs it
@@ -1446,6 +1511,62 @@ int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* av
     *avg_us = ms * 1000.0 / iters;
     *bytes = by;
     return 0;
+}
+
+int qie_batch_graph_kernel_times(qie_batch* b, int32_t n_steps, double* avg_us) {
+    QIE_REQUIRE(b && n_steps > 0 && avg_us, "qie_batch_graph_kernel_times: bad arguments");
+    qie_engine* e = b->e;
+    const int L = e->spec.n_layers;
+    QIE_REQUIRE(e->opts.use_graph && L >= 2, "qie_batch_graph_kernel_times: needs the graph path and >= 2 layers");
+    const size_t nev = (size_t)(L + 1) * 6 * 2;
+    if (b->pev.size() != nev) {
+        for (hipEvent_t ev : b->pev)
+            if (ev) hipEventDestroy(ev);
+        b->pev.assign(nev, nullptr);
+        for (auto& ev : b->pev) QIE_HIP(hipEventCreate(&ev));
+    }
+    QIE_TRY(prepare_steps(b, n_steps, "qie_batch_graph_kernel_times"));
+    // a separate capture of the greedy step with the event pairs in it (the cached graph is kept)
+    hipGraph_t g = nullptr;
+    hipGraphExec_t gx = nullptr;
+    QIE_HIP(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+    b->probe = true;
+    const int rc = enqueue_decode(b, nullptr);
+    b->probe = false;
+    hipError_t he = hipStreamEndCapture(e->stream, &g);
+    if (rc) {
+        if (g) hipGraphDestroy(g);
+        return rc;
+    }
+    if (he != hipSuccess) return fail((int)he, "probe capture: %s", hipGetErrorString(he));
+    he = hipGraphInstantiate(&gx, g, nullptr, nullptr, 0);
+    hipGraphDestroy(g);
+    if (he != hipSuccess) return fail((int)he, "probe instantiate: %s", hipGetErrorString(he));
+    double sum[6] = {0, 0, 0, 0, 0, 0};
+    int cnt[6] = {0, 0, 0, 0, 0, 0};
+    int err = 0;
+    for (int i = 0; i < n_steps && !err; i++) {
+        he = hipGraphLaunch(gx, e->stream);
+        if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+        if (he != hipSuccess) {
+            err = fail((int)he, "probe replay: %s", hipGetErrorString(he));
+            break;
+        }
+        for (int m = 0; m < b->B; m++) b->h_pos[m] += 1;
+        for (int l = 1; l <= L; l++)
+            for (int r = 0; r < 6; r++) {
+                if ((l == L) != (r == 4)) continue;   // the head row holds lm_head only
+                float ms = 0.f;
+                if (hipEventElapsedTime(&ms, b->pev[((size_t)l * 6 + r) * 2], b->pev[((size_t)l * 6 + r) * 2 + 1]) ==
+                    hipSuccess) {
+                    sum[r] += ms * 1e3;
+                    cnt[r] += 1;
+                }
+            }
+    }
+    hipGraphExecDestroy(gx);
+    for (int r = 0; r < 6; r++) avg_us[r] = cnt[r] ? sum[r] / cnt[r] : -1.0;
+    return err;
 }
 
 int qie_linear(const qie_linear_args* a, void* stream) {

@@ -228,6 +228,13 @@ struct DecodeAttnParams {
     float* part_ml;           // [B][nq][nsplit_max][2]
     unsigned* counters;       // [B][nkv], zero at rest
     uint16_t* out;            // [B][nq * HD]
+    // engine-maintained RoPE row of each sequence's CURRENT position (finalize / set_state
+    // write it, tagged with the position; [B][rope_cur_stride(HD)]): the prologue's RoPE
+    // loads need no position, so with the speculative K / V step every load of the launch
+    // goes out at once.  Null (operator API) or a stale tag: the table row at pos.
+    const float* rc;
+    int pv3;                  // P.V with three bf16 parts of P (else two; dev A/B)
+    int ks;                   // keys per block step (host: picks the kernel instance)
 };
 
 constexpr int kDecMaxSplits = 512;   // 64k keys per (row, kv head)
@@ -522,17 +529,17 @@ constexpr int kDecMStep = 128;      // keys per block step (4 waves x 32)
 constexpr int kDecMSplits = 32;     // default split target
 constexpr int kDecMOneSplit = 2;    // contexts of up to this many steps run as ONE split
 
-__host__ __device__ __forceinline__ int decm_chunk(int ctx, int target) {
+__host__ __device__ __forceinline__ int decm_chunk(int ctx, int target, int ks = kDecMStep) {
     // Short contexts: one block walks both steps instead of two one-step splits that pay
     // the publish + ticket + combine round trips (Qwen2-0.5B, ctx 129-256: 8.8 -> 7.4 us
     // per launch, 1,235 -> 1,271 tok/s).  Longer contexts want the CUs: a split's K/V comes
     // through one CU, so at ctx 2k ten two-step splits took 13.1 us against 10.5 for twenty
     // one-step ones — also with the second step's loads issued up front (13.6 vs 10.7,
     // measured and dropped: that second register set halved the occupancy).
-    if (ctx <= kDecMOneSplit * kDecMStep) return kDecMOneSplit * kDecMStep;
-    const int per = kDecMStep * target;
+    if (ctx <= kDecMOneSplit * ks) return kDecMOneSplit * ks;
+    const int per = ks * target;
     const int steps = (ctx + per - 1) / per;
-    return kDecMStep * (steps < 1 ? 1 : steps);
+    return ks * (steps < 1 ? 1 : steps);
 }
 
 
@@ -553,9 +560,20 @@ struct DecPro {
     bool is_q, is_k, is_v, pro, nrm, hf;
 };
 
+// this lane's RoPE coefficients from a table row (cos row cp, sin row sp)
+template <int HD>
+__device__ __forceinline__ void dec_rope_load(DecPro& d, int dl, const float* cp, const float* sp) {
+    const int rb = d.hf ? (dl * 8) % (HD / 2) : dl * 4;
+    const int rb2 = d.hf ? rb + 4 : rb;
+    d.c0 = *reinterpret_cast<const float4*>(cp + rb);
+    d.s0 = *reinterpret_cast<const float4*>(sp + rb);
+    d.c1 = *reinterpret_cast<const float4*>(cp + rb2);
+    d.s1 = *reinterpret_cast<const float4*>(sp + rb2);
+}
+
 template <int HD, bool PR>
 __device__ __forceinline__ DecPro dec_pro_issue(const DecodeAttnParams& a, const uint16_t* row, int g, int G, int grp,
-                                                int dl, int p, bool has_new) {
+                                                int dl, const float* cp, const float* sp, bool has_new) {
     DecPro d;
     d.is_q = grp < G;
     d.is_k = grp == G;
@@ -573,14 +591,7 @@ __device__ __forceinline__ DecPro dec_pro_issue(const DecodeAttnParams& a, const
     const uint16_t* nwp = d.is_q ? a.q_norm : a.k_norm;
     d.nrm = nwp != nullptr && !d.is_v;
     d.nraw = *reinterpret_cast<const uint4*>((nwp ? nwp : row) + dl * 8);
-    const float* cp = a.cs + (int64_t)p * (HD / 2);
-    const float* sp = a.sn + (int64_t)p * (HD / 2);
-    const int rb = d.hf ? (dl * 8) % (HD / 2) : dl * 4;
-    const int rb2 = d.hf ? rb + 4 : rb;
-    d.c0 = *reinterpret_cast<const float4*>(cp + rb);
-    d.s0 = *reinterpret_cast<const float4*>(sp + rb);
-    d.c1 = *reinterpret_cast<const float4*>(cp + rb2);
-    d.s1 = *reinterpret_cast<const float4*>(sp + rb2);
+    dec_rope_load<HD>(d, dl, cp, sp);
     return d;
 }
 
@@ -609,7 +620,7 @@ __device__ __forceinline__ void dec_pro_finish(const DecodeAttnParams& a, DecPro
     // qk-norm (Qwen3) and HF numerics are launch-uniform: branch around them instead of
     // computing both forms per element (Qwen2, REF: neither — 8 divisions and the HF RoPE
     // products per lane were dead work on the critical path)
-    if (a.q_norm != nullptr) {
+    if (a.q_norm != nullptr || a.k_norm != nullptr) {   // per lane: d.nrm picks q_norm / k_norm
         float ss = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; j++) ss += x[j] * x[j];
@@ -660,7 +671,7 @@ __device__ __forceinline__ void dec_pro_finish(const DecodeAttnParams& a, DecPro
 
 // Body of the decode attention for workgroup (bx, by); true when this workgroup wrote a
 // combined (row, kv head) output (its stores are write-through, sc1).
-template <int HD, bool PG, int NWA, bool PR>
+template <int HD, bool PG, int NWA, bool PR, int KS>
 __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a, const int bx, const int by) {
 #pragma clang fp contract(off)
     constexpr int LPT = HD / 8;          // prologue: lanes per head row
@@ -669,14 +680,14 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
     constexpr int DW = HD / NWA;         // output dims per wave
     constexpr int DTW = DW / 16;         // output d tiles per wave (2 at hd 128 x 4 waves, else 1)
     constexpr int CPW = DW / 8;          // 16-byte chunks of a V row per wave
-    constexpr int VCH = kDecMStep * CPW / 64;   // V chunks per lane per step
-    constexpr int TPW = kDecMStep / (16 * NWA);  // 16-key S tiles per wave per step
+    constexpr int VCH = KS * CPW / 64;   // V chunks per lane per step
+    constexpr int TPW = KS / (16 * NWA);  // 16-key S tiles per wave per step
     constexpr int NT = 64 * NWA;         // threads
     static_assert(DTW >= 1 && TPW >= 1, "attn_decode: NWA too large for HD");
     __shared__ __attribute__((aligned(16))) uint16_t q_s[16][HD];
     __shared__ __attribute__((aligned(16))) uint16_t kv_new[2][HD];
-    __shared__ __attribute__((aligned(16))) uint16_t v_s[NWA][kDecMStep * DW];
-    __shared__ __attribute__((aligned(16))) float s_s[16][kDecMStep + 4];
+    __shared__ __attribute__((aligned(16))) uint16_t v_s[NWA][KS * DW];
+    __shared__ __attribute__((aligned(16))) float s_s[16][KS + 4];
     __shared__ int last_flag;
 
     const int64_t m = by;
@@ -714,30 +725,42 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
     // K / V loads go out with the position load instead of one HBM round trip behind it.
     // The rotated q / k / v row goes out first (position-independent): vmcnt retires in
     // order, and the prologue that waits for it must not wait behind the whole K / V step.
-    constexpr bool SPEC = PR && !PG;
+    // Without the pre-rotation the same holds when the engine keeps the current position's
+    // RoPE row (a.rc, tagged with the position): the prologue's loads then need no position
+    // either, and a stale tag (a position set some other way) reloads the table row.
+    constexpr bool SPEC = !PG;
+    const bool spec = PR || a.rc != nullptr;   // uniform
     const int p = a.pos[m];
+    const float* rcm = a.rc ? a.rc + m * rope_cur_stride(HD) : a.cs;
+    const int rtag = a.rc ? __float_as_int(rcm[0]) : -1;
     DecPro pr;
-    if constexpr (SPEC) {
-        pr = dec_pro_issue<HD, PR>(a, row, g, G, grp, dl, 0, false);
+    if (SPEC && spec) {
+        pr = dec_pro_issue<HD, PR>(a, row, g, G, grp, dl, rcm + 8, rcm + 8 + HD / 2, false);
         __builtin_amdgcn_sched_barrier(0);
-        load_step_at(kDecMStep * s, a.max_ctx - 1);
+        load_step_at(KS * s, a.max_ctx - 1);
         __builtin_amdgcn_sched_barrier(0);
     }
     const int ctx = p + 1;
-    const int chunk = decm_chunk(ctx, a.splits_target);
+    const int chunk = decm_chunk(ctx, a.splits_target, KS);
     const int nsplit = (ctx + chunk - 1) / chunk;
     if (s >= nsplit || QIE_DBG(a.dbg & 64)) return false;
     const int t0 = s * chunk, t1 = min(ctx, t0 + chunk);
-    const int nstep = (t1 - t0 + kDecMStep - 1) / kDecMStep;
+    const int nstep = (t1 - t0 + KS - 1) / KS;
     const bool has_new = (t1 == ctx);
-    auto load_step = [&](int st) { load_step_at(t0 + st * kDecMStep, t1 - 1); };
+    auto load_step = [&](int st) { load_step_at(t0 + st * KS, t1 - 1); };
 
     // ---------------- loads: prologue operands, then step 0's K tiles and V slice
-    if constexpr (SPEC) pr.pro = pr.is_q || ((pr.is_k || pr.is_v) && has_new);
-    else pr = dec_pro_issue<HD, PR>(a, row, g, G, grp, dl, p, has_new);
+    if (SPEC && spec) {
+        pr.pro = pr.is_q || ((pr.is_k || pr.is_v) && has_new);
+        if (!PR && rtag != p)   // uniform: the kept row is not this position's
+            dec_rope_load<HD>(pr, dl, a.cs + (int64_t)p * (HD / 2), a.sn + (int64_t)p * (HD / 2));
+    } else {
+        pr = dec_pro_issue<HD, PR>(a, row, g, G, grp, dl, a.cs + (int64_t)p * (HD / 2), a.sn + (int64_t)p * (HD / 2),
+                                   has_new);
+    }
     __builtin_amdgcn_sched_barrier(0);
-    if (!SPEC || chunk != kDecMStep) load_step(0);   // (uniform) the speculative step was not this split's
-    if constexpr (SPEC) {
+    if (!(SPEC && spec) || chunk != KS) load_step(0);   // (uniform) the speculative step was not this split's
+    if (SPEC && spec) {
         // rows past the context hold whatever the cache has there: their scores are masked
         // to -inf (P = 0), and their V rows are zeroed so that 0 * V stays 0 for any bits
 #pragma unroll
@@ -769,7 +792,7 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
     const int q4 = fr >> 2, p4 = fr & 3;
 
     for (int st = 0; st < nstep; st++) {
-        const int kb0 = t0 + st * kDecMStep;
+        const int kb0 = t0 + st * KS;
         // ---- S^T for this wave's 32 keys -> LDS (raw dots)
 #pragma unroll
         for (int t = 0; t < TPW; t++) {
@@ -796,10 +819,10 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
         __syncthreads();   // scores and V slices visible
         // ---- online softmax over the step's 128 keys (every wave, identical); lane:
         // head fr, keys 32 c + 8 gq + j (natural order, the P.V k slots)
-        float e[4][8];
+        float e[KS / 32][8];
         float mt = -INFINITY;
 #pragma unroll
-        for (int c = 0; c < 4; c++) {
+        for (int c = 0; c < KS / 32; c++) {
             const float4 lo = *reinterpret_cast<const float4*>(&s_s[fr][32 * c + 8 * gq]);
             const float4 hi = *reinterpret_cast<const float4*>(&s_s[fr][32 * c + 8 * gq + 4]);
             const float v8[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
@@ -819,7 +842,7 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
         const float alpha = __expf(m_run - m_use);
         float ls = 0.f;
 #pragma unroll
-        for (int c = 0; c < 4; c++)
+        for (int c = 0; c < KS / 32; c++)
 #pragma unroll
             for (int j = 0; j < 8; j++) {
                 e[c][j] = __expf(e[c][j] - m_use);
@@ -839,7 +862,7 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
         // 24 bits of the fp32 probability, so every P.V product is the reference's fp32
         // product (self_attension.cu:127-135) — only the accumulation order differs
 #pragma unroll
-        for (int c = 0; c < 4; c++) {
+        for (int c = 0; c < KS / 32; c++) {
             bf16x8_t ph, pm, pl;
 #pragma unroll
             for (int j = 0; j < 8; j++) {
@@ -858,7 +881,7 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
                 const bf16x8_t vb8 = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
                 oacc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph, vb8, oacc[d], 0, 0, 0);
                 oacc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pm, vb8, oacc[d], 0, 0, 0);
-                oacc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pl, vb8, oacc[d], 0, 0, 0);
+                if (!QIE_DBG(!a.pv3)) oacc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pl, vb8, oacc[d], 0, 0, 0);
             }
         }
         __syncthreads();   // scores / V slots free for the next step
@@ -926,7 +949,7 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
     // head together with its 16-byte slice of every split's partial O (one batch of JB
     // splits = one round trip; ctx <= JB * 128 keys in one), then merges them itself — no
     // per-head wave pass, LDS weight table or barrier between the two load rounds.
-    constexpr int JB = 24;
+    constexpr int JB = KS == 128 ? 24 : 40;   // splits per combine round trip
     const bool has_item = tid < G * (HD / 4);
     const int gi = has_item ? tid / (HD / 4) : 0, d4 = tid % (HD / 4);
     const int64_t hbase = (m * nq + g * G + gi) * (int64_t)a.nsplit_max;
@@ -991,9 +1014,9 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
     return true;
 }
 
-template <int HD, bool PG, int NWA, bool PR>
+template <int HD, bool PG, int NWA, bool PR, int KS = kDecMStep>
 __global__ __launch_bounds__(64 * NWA) void attn_decode_mfma2_kernel(DecodeAttnParams a) {
-    attn_decode_mfma2_body<HD, PG, NWA, PR>(a, blockIdx.x, blockIdx.y);
+    attn_decode_mfma2_body<HD, PG, NWA, PR, KS>(a, blockIdx.x, blockIdx.y);
 }
 
 
@@ -1017,6 +1040,9 @@ static int attn_nsplit(int64_t M, int32_t max_ctx) {
     return ns;
 }
 
+static thread_local const float* g_rope_cur = nullptr;
+void set_decode_rope_cur(const float* rc) { g_rope_cur = rc; }
+
 static int fill_dec_params(DecodeAttnParams& a, const void* qkv, int64_t B, const int32_t* pos, const void* q_norm,
                            const void* k_norm, const float* rope_cos, const float* rope_sin, int32_t n_heads,
                            const qie_kv_cache* cache, int32_t layer, float eps, int32_t numerics, void* out, void* ws) {
@@ -1037,7 +1063,9 @@ static int fill_dec_params(DecodeAttnParams& a, const void* qkv, int64_t B, cons
     a.splits_target = senv > 0 ? senv : kDecMSplits;
     a.dbg = dev_env("QIE_DEC_DBG", 0);
     a.sc1 = dev_env("QIE_DEC_SC1", 1);   // 9.79 -> 9.56 us per launch (ctx 2.3k, Qwen2-7B)
-    a.nsplit_max = std::min(a.splits_target, (cache->max_ctx + kDecMStep - 1) / kDecMStep);
+    const int ks = dev_env("QIE_DEC_KS", kDecMStep) == 64 ? 64 : kDecMStep;   // keys per block step
+    a.ks = ks;
+    a.nsplit_max = std::min(a.splits_target, (cache->max_ctx + ks - 1) / ks);
     QIE_REQUIRE(a.nsplit_max <= kDecMaxSplits, "qie_attention_decode: max_ctx %d too long", cache->max_ctx);
     a.eps = eps;
     a.numerics = numerics & QIE_NUMERICS_MASK;
@@ -1049,6 +1077,8 @@ static int fill_dec_params(DecodeAttnParams& a, const void* qkv, int64_t B, cons
     a.part_o = (float*)((char*)ws + cnt);
     a.part_ml = a.part_o + B * n_heads * (int64_t)a.nsplit_max * cache->head_dim;
     a.out = (uint16_t*)out;
+    a.rc = dev_env("QIE_DEC_ROPECUR", 1) ? g_rope_cur : nullptr;
+    a.pv3 = dev_env("QIE_DEC_PV3", 1);
     return 0;
 }
 
@@ -1143,7 +1173,7 @@ int qie_debug_tr16_probe(int32_t* out_dev) {
 int64_t qie_attention_decode_workspace_bytes(int64_t B, int32_t n_heads, int32_t n_kv_heads, int32_t head_dim,
                                              int32_t max_ctx) {
     // an upper bound for every splits_target <= kDecMaxSplits (nsplit_max in fill_dec_params)
-    const int64_t ns = std::min<int64_t>(kDecMaxSplits, (max_ctx + kDecMStep - 1) / kDecMStep);
+    const int64_t ns = std::min<int64_t>(kDecMaxSplits, (max_ctx + 63) / 64);   // 64- or 128-key steps
     const int64_t cnt = ((B * n_kv_heads * 4 + 255) / 256) * 256;
     return cnt + B * n_heads * ns * (head_dim + 2) * 4;
 }
@@ -1173,6 +1203,8 @@ int qie_attention_decode(const void* qkv, int64_t B, const int32_t* pos, const v
                         : (pg ? attn_decode_mfma2_kernel<128, true, 4, false> : attn_decode_mfma2_kernel<128, false, 4, false>))
                   : (pr ? (pg ? attn_decode_mfma2_kernel<64, true, 4, true> : attn_decode_mfma2_kernel<64, false, 4, true>)
                         : (pg ? attn_decode_mfma2_kernel<64, true, 4, false> : attn_decode_mfma2_kernel<64, false, 4, false>));
+    if (a.ks == 64 && cache->head_dim == 128 && !pr)   // 64-key steps (dev A/B)
+        k2 = pg ? attn_decode_mfma2_kernel<128, true, 4, false, 64> : attn_decode_mfma2_kernel<128, false, 4, false, 64>;
     hipLaunchKernelGGL(k2, grid, dim3(256), 0, (hipStream_t)stream, a);
     QIE_LAUNCH_CHECK();
     return 0;

@@ -56,7 +56,20 @@ struct GemvParams {
     const float* rope_sn;
     int rope_hd;
     int64_t rope_rows;
+    int epre;          // M = 1: the first task's epilogue operands (bias / residual) loaded up front
+    int mkdiv;         // x-first fused norm: REF quotient by the FMA-corrected reciprocal (dev A/B)
 };
+
+// REF RMSNorm quotient f / rms: the FMA-corrected product with the reciprocal (Markstein),
+// the real division outside [1e-30, 1e30] (and for 0) — see skinny_mfma_kernel's prologue
+__device__ __forceinline__ float div_mk(float f, float rms, float inv) {
+#pragma clang fp contract(off)
+    const float q = f * inv;
+    float d = fmaf(fmaf(-q, rms, f), inv, q);
+    const float af = fabsf(f);
+    if (af != 0.f && (af < 1e-30f || af > 1e30f)) d = f / rms;
+    return d;
+}
 
 // uniform loads through the scalar cache (constant address space): the RoPE coefficients
 // wait on lgkmcnt, not behind the weight stream's in-order vmcnt
@@ -174,6 +187,37 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
     // (wave_sum, no cross-wave exchange); wave w then normalises chunks w, w + NW, ... into
     // LDS — one barrier in all, instead of the x-first prologue's two around a block reduction.
     uint4 xr[XCH == 3 ? U : 1];
+    // XCH == 4 (MT = 1, fused RMSNorm, K <= 512 U): as XCH == 3, but every wave also
+    // normalises ITS OWN chunks in registers — lane l's x chunk u is exactly the 8 elements
+    // its weight chunk u multiplies — so there is no LDS image, no barrier and no LDS read
+    // in the weight loop; the norm's divisions are repeated per wave (56 per lane at
+    // K = 3,584) while the weight stream is in flight.
+    uint4 xq[XCH == 4 ? U : 1];
+    // Epilogue operands of the wave's FIRST task (M = 1: bias values of STORE rows, the old
+    // residual values of RESIDUAL rows) loaded before its weight stream, so the epilogue of a
+    // one-task wave — every small decode GEMV — has no dependent load after the reduction.
+    // Unconditional buffer loads (a missing bias reads element 0 of x; the epilogue ignores it).
+    constexpr bool EPRE = MT == 1 && (EPI == QIE_EPI_RESIDUAL || EPI == QIE_EPI_STORE);
+    uint32_t epre_v[EPRE ? RPW : 1];
+    const bool epre_on = EPRE && XCH > 0 && p.epre != 0 && p.M == 1;   // uniform; the XCH > 0 prologues issue them
+    auto epre_issue = [&](int64_t task) {
+        if constexpr (EPRE) {
+#pragma unroll
+            for (int i = 0; i < RPW; i++) {
+                int64_t c = task * RPW + i;
+                c = c < p.N ? c : p.N - 1;
+                if constexpr (EPI == QIE_EPI_RESIDUAL) {
+                    const auto ry = rsrc(p.y, p.N * 2);
+                    epre_v[i] = __builtin_amdgcn_raw_buffer_load_b16(ry, (int)(c * 2), 0, 0);
+                } else {
+                    const uint16_t* b = c < p.n0 ? p.b0 : (c < p.n01 ? p.b1 : p.b2);
+                    const int64_t bi = c < p.n0 ? c : (c < p.n01 ? c - p.n0 : c - p.n01);
+                    const auto rb = rsrc(b ? (const void*)b : (const void*)p.x, b ? (bi + 1) * 2 : 2);
+                    epre_v[i] = __builtin_amdgcn_raw_buffer_load_b16(rb, b ? (int)(bi * 2) : 0, 0, 0);
+                }
+            }
+        }
+    };
     auto load_chunk = [&](const u32x4* const (&wr)[RPW], int64_t k0, u32x4 (&wv)[U][RPW]) {
         const int voff = (int)(k0 * EB);   // this lane's byte offset in the row (< 2^31)
         const auto rx = rsrc(p.x, K * 2);
@@ -201,7 +245,7 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
                 if constexpr (WT == 0) {
 #pragma unroll
                     for (int m = 0; m < MT; m++) {
-                        const uint4 xv = XCH == 1 ? xg[XCH == 1 ? u : 0] : x_at(m, k);
+                        const uint4 xv = XCH == 1 ? xg[XCH == 1 ? u : 0] : (XCH == 4 ? xq[XCH == 4 ? u : 0] : x_at(m, k));
                         float xf[8];
                         unpack8(u32x4{xv.x, xv.y, xv.z, xv.w}, xf);
 #pragma unroll
@@ -244,6 +288,7 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
     constexpr bool PF = XCH > 0;
 
     if constexpr (XCH == 1) {
+        if (epre_on) epre_issue(task0 < p.n_tasks ? task0 : p.n_tasks - 1);
         task_ptrs(task0 < p.n_tasks ? task0 : p.n_tasks - 1, wr);
         load_chunk(wr, (int64_t)lane * EL, wv);
     } else if constexpr (XCH == 3) {
@@ -265,6 +310,7 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
             nvw[c] = __builtin_amdgcn_raw_buffer_load_b128(rn, lane * 16, (u < U ? u : 0) * 1024, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
+        if (epre_on) epre_issue(task0 < p.n_tasks ? task0 : p.n_tasks - 1);
         task_ptrs(task0 < p.n_tasks ? task0 : p.n_tasks - 1, wr);
         load_chunk(wr, (int64_t)lane * EL, wv);
         __builtin_amdgcn_sched_barrier(0);
@@ -312,6 +358,59 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
             if (k < K) *reinterpret_cast<uint4*>(xs + k) = make_uint4(o[0], o[1], o[2], o[3]);
         }
         __syncthreads();
+    } else if constexpr (XCH == 4) {
+        // x and the norm weights first (one 16-B chunk per wave-load slot u, a chunk past K
+        // reads zeros), then the first task's weight stream, THEN the norm arithmetic
+        const auto rx = rsrc(p.x, K * 2), rn = rsrc(p.norm_w, K * 2);
+        u32x4 xa[U], na[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            xa[u] = __builtin_amdgcn_raw_buffer_load_b128(rx, lane * 16, u * 1024, 0);
+            na[u] = __builtin_amdgcn_raw_buffer_load_b128(rn, lane * 16, u * 1024, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (epre_on) epre_issue(task0 < p.n_tasks ? task0 : p.n_tasks - 1);
+        task_ptrs(task0 < p.n_tasks ? task0 : p.n_tasks - 1, wr);
+        load_chunk(wr, (int64_t)lane * EL, wv);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < U; u++) asm volatile("" : "+v"(xa[u]), "+v"(na[u]));
+        float ss = 0.f;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            float f[8];
+            unpack8(xa[u], f);
+#pragma unroll
+            for (int j = 0; j < 8; j++) ss += f[j] * f[j];
+        }
+        ss = wave_sum(ss);
+        const float rms = sqrtf((ss / (float)K) + p.eps);
+        const float inv = 1.0f / rms;
+        const bool hf = p.numerics == QIE_NUMERICS_HF;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+#pragma clang fp contract(off)
+            float f[8], wf[8];
+            unpack8(xa[u], f);
+            unpack8(na[u], wf);
+            uint32_t o[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                float y0, y1;
+                if (hf) {
+                    y0 = wf[2 * j] * rbf(f[2 * j] * inv);
+                    y1 = wf[2 * j + 1] * rbf(f[2 * j + 1] * inv);
+                } else if (p.mkdiv) {
+                    y0 = div_mk(f[2 * j], rms, inv) * wf[2 * j];
+                    y1 = div_mk(f[2 * j + 1], rms, inv) * wf[2 * j + 1];
+                } else {
+                    y0 = (f[2 * j] / rms) * wf[2 * j];
+                    y1 = (f[2 * j + 1] / rms) * wf[2 * j + 1];
+                }
+                o[j] = pack2(y0, y1);
+            }
+            xq[u] = make_uint4(o[0], o[1], o[2], o[3]);
+        }
     } else if constexpr (XCH > 0) {
         // ---------------- x-first prologue (MT = 1, x staged in LDS, K <= 2048 * XCH; the
         // host guarantees it).  Order of issue: this thread's x chunks (+ norm weights),
@@ -331,6 +430,7 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
         __builtin_amdgcn_sched_barrier(0);
         // unconditional (a wave without a task re-reads the last row): a load under a
         // branch makes the vmcnt bookkeeping at the join wait for everything
+        if (epre_on) epre_issue(task0 < p.n_tasks ? task0 : p.n_tasks - 1);
         task_ptrs(task0 < p.n_tasks ? task0 : p.n_tasks - 1, wr);
         load_chunk(wr, (int64_t)lane * EL, wv);
         __builtin_amdgcn_sched_barrier(0);
@@ -376,6 +476,9 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
                     if (hf) {
                         y0 = wf[2 * j] * rbf(f[2 * j] * inv);
                         y1 = wf[2 * j + 1] * rbf(f[2 * j + 1] * inv);
+                    } else if (p.mkdiv) {
+                        y0 = div_mk(f[2 * j], rms, inv) * wf[2 * j];
+                        y1 = div_mk(f[2 * j + 1], rms, inv) * wf[2 * j + 1];
                     } else {
                         y0 = (f[2 * j] / rms) * wf[2 * j];
                         y1 = (f[2 * j + 1] / rms) * wf[2 * j + 1];
@@ -450,7 +553,7 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
         }
         __syncthreads();
     }
-    if constexpr (XCH == 0 || XCH == 1 || XCH == 3)   // prologues without the early position load
+    if constexpr (XCH == 0 || XCH == 1 || XCH == 3 || XCH == 4)   // prologues without the early position load
         if (rope) rpos = sload(p.rope_pos, 0);
     float rc[ROPE ? RPW / 2 : 1], rs[ROPE ? RPW / 2 : 1];
     auto rope_coef = [&](int64_t task, float* c_out, float* s_out) {
@@ -535,10 +638,12 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
                     for (int i = 0; i < RPW; i++)
                         if (col[i] < p.N) yf[col[i]] = acc[m][i];
                 } else if constexpr (EPI == QIE_EPI_RESIDUAL) {
+                    const bool pre = epre_on && task == task0;
 #pragma unroll
                     for (int i = 0; i < RPW; i++) {
                         if (col[i] >= p.N) continue;
-                        yr[col[i]] = f2bf(bf2f(yr[col[i]]) + rbf(acc[m][i]));
+                        const float old = pre ? bf2f(epre_v[EPRE ? i : 0]) : bf2f(yr[col[i]]);
+                        yr[col[i]] = f2bf(old + rbf(acc[m][i]));
                     }
                 } else {
                     unsigned long long best = kbest[m];
@@ -548,7 +653,9 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
                         const int64_t c = col[i] < p.N ? col[i] : p.N - 1;
                         float v = acc[m][i];
                         const uint16_t* b = c < p.n0 ? p.b0 : (c < p.n01 ? p.b1 : p.b2);
-                        if (b) {
+                        if (epre_on && task == task0) {
+                            if (b) v = v + bf2f(epre_v[EPRE ? i : 0]);
+                        } else if (b) {
                             int64_t bi = c < p.n0 ? c : (c < p.n01 ? c - p.n0 : c - p.n01);
                             v = v + bf2f(b[bi]);
                         }
@@ -1096,6 +1203,11 @@ static int launch_gemv_1(const GemvParams& p, int rpw, int epi, hipStream_t st, 
     const int64_t n = (p.K + 511) / 512;   // bf16 wave-loads per row
     const bool vocab = p.n_tasks * rpw >= 65536;
     const int64_t ub = (n + (n + 7) / 8 - 1) / ((n + 7) / 8);   // balanced slots per pass (<= 8)
+    if (xch == 4) {   // fused norm, normalised x in every wave's registers
+        if (n <= 2) return launch_gemv_m<1, 4, 0, 2>(p, rpw, epi, st, bpc);
+        if (n == 7 && !vocab) return launch_gemv_m<1, 4, 0, 7>(p, rpw, epi, st, bpc);
+        return launch_gemv_m<1, 4, 0, 8>(p, rpw, epi, st, bpc);
+    }
     if (xch == 3) {   // fused norm, x in registers: one batch of wave-loads covers a row
         if (n <= 2) return launch_gemv_m<1, 3, 0, 2>(p, rpw, epi, st, bpc);
         if (n == 7 && !vocab) return launch_gemv_m<1, 3, 0, 7>(p, rpw, epi, st, bpc);
@@ -1239,6 +1351,8 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
     p.rope_sn = g_rope.sn;
     p.rope_hd = g_rope.hd;
     p.rope_rows = g_rope.rows;
+    p.epre = env_int("QIE_GEMV_EPRE", 0);
+    p.mkdiv = env_int("QIE_GEMV_MKDIV", 0);
     if (a->M >= 2 && a->M <= 16 && env_int("QIE_SKINNY_MFMA", 1) != 0) {
         const bool fp8w = (a->flags & QIE_LINEAR_FP8) != 0;
         const int kstep = 64;
@@ -1284,7 +1398,7 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
     // waves where 4..9 tasks per CU (Qwen2-7B QKV, O, down), else the occupancy-balanced
     // persistent grid (lm_head 169 vs 183 us, gate/up 43.1 vs 43.5 against a cap of 8 blocks
     // per CU); 0 = always the occupancy grid; N > 0 = cap of N blocks per CU.
-    const int bpc = env_int("QIE_GEMV_BLOCKS_PER_CU", -1);
+    int bpc = env_int("QIE_GEMV_BLOCKS_PER_CU", -1);
     // x-first prologue + cross-task weight prefetch (QIE_GEMV_XFIRST, MT = 1).  A first
     // attempt that issued the weights BEFORE x was slower everywhere (qkv 11.4 vs 9.4 us):
     // x then queued behind the weights in the in-order vmcnt.
@@ -1315,6 +1429,18 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
     if (MT == 1 && p.M == 1 && p.norm_w && a->K % 8 == 0 && a->K <= 4096 &&
         env_int("QIE_GEMV_XREG", vocab_rows ? 1 : 0) != 0) {
         xch = 3;
+    }
+    // Normalised x in every wave's registers (XCH 4): no LDS image, no barrier (A/B knobs
+    // QIE_GEMV_XREG4 for the STORE projections (QKV, lm_head) and QIE_GEMV_XREG4_SW for gate/up)
+    if (MT == 1 && p.M == 1 && p.norm_w && a->K % 8 == 0 && a->K <= 4096 &&
+        env_int(a->epilogue == QIE_EPI_SWIGLU ? "QIE_GEMV_XREG4_SW" : "QIE_GEMV_XREG4", 0) != 0) {
+        xch = 4;
+        p.xlds = 0;
+    }
+    // gate/up grid override (A/B): blocks per CU for the SwiGLU launch only
+    if (a->epilogue == QIE_EPI_SWIGLU && MT == 1) {
+        const int sb = env_int("QIE_GEMV_SWIGLU_BPC", -1);
+        if (sb >= 0) bpc = sb;
     }
     // Batch-1 GEMVs without a fused norm on the one-block-per-CU grid (one row task per
     // wave: Qwen2-7B O, down) read x from L2 beside each weight chunk (XCH = 1) instead of

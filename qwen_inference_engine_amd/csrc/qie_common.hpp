@@ -132,13 +132,10 @@ __device__ __forceinline__ void fp8x4_to_f32(uint32_t w, float* f) {
     f[3] = hi[1];
 }
 
-// four e4m3 codes -> four bf16, exact (every e4m3 value, subnormals included, is a bf16):
-// the exact fp32 conversion, then one v_cvt_pk_bf16_f32 per pair.  (The one-step
-// v_cvt_scalef32_pk_bf16_fp8 does not reproduce the subnormal codes: the fp8 engine test
-// against the dequantised oracle model fails with it.)
-// Two codes -> two bf16 per instruction (gfx950 v_cvt_scalef32_pk_bf16_fp8, scale 1.0):
-// every e4m3 value is a bf16, so the convert is exact (all 256 codes are checked against
-// the e4m3fn table by qie_debug_fp8_decode_bf16); half the VALU of fp8 -> f32 -> bf16.
+// four e4m3 codes -> four bf16, two per instruction (gfx950 v_cvt_scalef32_pk_bf16_fp8,
+// scale 1.0).  Every e4m3 value, subnormals included, is a bf16, so the conversion is exact;
+// tests/test_gpu_fp8.py::test_fp8_decode_bf16_all_codes checks all 256 codes against the
+// e4m3fn table (qie_debug_fp8_decode_bf16).  Half the VALU of fp8 -> f32 -> bf16.
 __device__ __forceinline__ uint2 fp8x4_to_bf16x4(uint32_t w) {
     const auto lo = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)w, 1.0f, false);
     const auto hi = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)w, 1.0f, true);
@@ -263,6 +260,12 @@ __device__ __forceinline__ float key_val(uint64_t key) {
 }
 
 inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+// Per-sequence RoPE row of the current decode position (engine-owned, see DecodeAttnParams::rc):
+// float [B][rope_cur_stride(hd)] = {tag (the position, int bits), 7 pad, cos[hd / 2], sin[hd / 2]}
+__host__ __device__ constexpr int rope_cur_stride(int hd) { return 8 + hd; }
+// the decode attention launches of this host thread read this table (null: none)
+void set_decode_rope_cur(const float* rc);
 
 // Device properties cached per process (CU count for persistent grids).
 int device_cu_count();

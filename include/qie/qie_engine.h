@@ -62,6 +62,22 @@ void qie_index_destroy(qie_index* idx);
 int qie_comm_unique_id(void* id_out);
 int qie_comm_create_rccl(const void* id, int32_t world, int32_t rank, int32_t device, qie_comm** out);
 int qie_comm_create_local(int32_t world, qie_comm** out);
+/* Peer backend: every rank's exchange buffer mapped into every rank, one
+ * kernel per collective (push + per-block generation flags + rank-ordered reduce, the
+ * residual add fused into the row-parallel all-reduce); graph-capturable.  Across
+ * processes: qie_comm_create_peer() returns this rank's QIE_COMM_PEER_HANDLE_BYTES IPC
+ * handle, the host ships all handles to every rank (handles[r] = rank r's), then
+ * qie_comm_peer_connect().  Ranks of one process on one device:
+ * qie_comm_create_peer_local(world, out[world]).  A rank that waited ~2 s for a peer
+ * sets the error word qie_comm_peer_error() reads (no kernel waits forever). */
+#define QIE_COMM_PEER_HANDLE_BYTES 128
+int qie_comm_create_peer(int32_t world, int32_t rank, int32_t device, qie_comm** out, void* handle_out);
+int qie_comm_peer_connect(qie_comm* c, const void* handles);
+int qie_comm_create_peer_local(int32_t world, qie_comm** out);
+int qie_comm_peer_error(const qie_comm* c, int32_t* err);
+/* x (bf16 [n]) = bf16(x + bf16(sum over ranks of part)), in place on x (part may be
+ * overwritten): the exchange after a row-parallel projection */
+int qie_comm_allreduce_residual_bf16(qie_comm* c, const float* part, void* x, int64_t n, void* stream);
 int qie_comm_rank(const qie_comm* c, int32_t* world, int32_t* rank);
 int qie_comm_allreduce_sum_f32(qie_comm* c, float* buf, int64_t n, void* stream);
 void qie_comm_destroy(qie_comm* c);

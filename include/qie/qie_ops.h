@@ -42,6 +42,10 @@ int qie_memcpy_h2d(void* dst, const void* src, int64_t bytes);
 int qie_memcpy_d2h(void* dst, const void* src, int64_t bytes);
 int qie_memset(void* ptr, int value, int64_t bytes);
 int qie_synchronize(void);
+/* a non-blocking stream of the current device (ops take it as `void* stream`) */
+int qie_stream_create(void** stream_out);
+int qie_stream_synchronize(void* stream);
+int qie_stream_destroy(void* stream);
 
 /* ---------------------------------------------------------------- tables
  * Replaces precompute_cos_sin (layers/src/include.cpp:5-16, called at

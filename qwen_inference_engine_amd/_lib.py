@@ -25,6 +25,7 @@ QIE_LINEAR_TILE256 = 2
 QIE_LINEAR_TILE128 = 4
 QIE_ATTN_PREROPED = 0x100   # qie_attention_decode numerics flag: q / new k arrive rotated
 QIE_COMM_ID_BYTES = 128
+QIE_COMM_PEER_HANDLE_BYTES = 128
 
 
 class ModelSpecC(C.Structure):
@@ -96,6 +97,9 @@ SIGNATURES = [
     ("qie_memcpy_d2h", C.c_int, [_P, _P, _I64]),
     ("qie_memset", C.c_int, [_P, C.c_int, _I64]),
     ("qie_synchronize", C.c_int, []),
+    ("qie_stream_create", C.c_int, [C.POINTER(_P)]),
+    ("qie_stream_synchronize", C.c_int, [_P]),
+    ("qie_stream_destroy", C.c_int, [_P]),
     ("qie_rope_table_host", C.c_int, [_PF, _PF, _I32, _I32, _F, _I32]),
     ("qie_embedding", C.c_int, [_P, _P, _P, _I64, _I64, _P]),
     ("qie_rmsnorm", C.c_int, [_P, _P, _P, _I64, _I64, _F, _I32, _P]),
@@ -135,6 +139,11 @@ SIGNATURES = [
     ("qie_comm_unique_id", C.c_int, [_P]),
     ("qie_comm_create_rccl", C.c_int, [_P, _I32, _I32, _I32, C.POINTER(_P)]),
     ("qie_comm_create_local", C.c_int, [_I32, C.POINTER(_P)]),
+    ("qie_comm_create_peer", C.c_int, [_I32, _I32, _I32, C.POINTER(_P), _P]),
+    ("qie_comm_peer_connect", C.c_int, [_P, _P]),
+    ("qie_comm_create_peer_local", C.c_int, [_I32, C.POINTER(_P)]),
+    ("qie_comm_peer_error", C.c_int, [_P, _PI32]),
+    ("qie_comm_allreduce_residual_bf16", C.c_int, [_P, _P, _P, _I64, _P]),
     ("qie_comm_rank", C.c_int, [_P, _PI32, _PI32]),
     ("qie_comm_allreduce_sum_f32", C.c_int, [_P, _P, _I64, _P]),
     ("qie_comm_destroy", None, [_P]),

@@ -9,10 +9,13 @@
 #include "qie_common.hpp"
 #include "qie_comm.hpp"
 #include "../../include/qie/qie_engine.h"
+#include "../../include/qie/qie_ops.h"
 
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <condition_variable>
+#include <type_traits>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -171,7 +174,206 @@ struct LocalComm : qie_comm {
     bool graph_capturable() const override { return false; }
 };
 
+// ------------------------------------------------------------- peer backend
+// One-shot exchange through every rank's buffer mapped into every other rank (HIP IPC across
+// processes; plain pointers for ranks of one process): each collective is ONE kernel that
+// pushes this rank's slice into slot [parity][rank] of EVERY rank's buffer, raises a
+// per-block flag (the generation) in every buffer, waits for the W flags of its block in its
+// own buffer, and reduces the W slots in rank order 0..W-1 (the local backend's order: the
+// results are bit-identical to it).  The all-reduce after the row-parallel projections
+// fuses the residual add, x = bf16(x + bf16(sum)) (qie_residual_add_f32), so a layer's
+// exchange is one graph node instead of RCCL's collective + a residual launch.
+//   * buffers are uncached device memory (hipDeviceMallocUncached): another device's stores
+//     and this device's loads meet in memory, never in a stale L2 line;
+//   * generation e lives in device memory (graph replays advance it): every block reads it
+//     first, the last block to finish (ticket) stores e + 1; data and flags alternate
+//     between two parities, and a rank can only reach generation e + 2 after every peer
+//     raised its e + 1 flags, i.e. after every peer finished reading generation e;
+//   * the wait is bounded (~2 s of s_memrealtime): a peer that never arrives sets the error
+//     word and the kernel ends (no hang); qie_comm_peer_error() reports it.
+constexpr int kPeerMaxWorld = 8;
+constexpr int kPeerBlocks = 16;
+constexpr int64_t kPeerFlagBytes = 4096;             // [2][8][16] uint32 flags, padded
+constexpr int64_t kPeerCap = 2 << 20;                // data bytes per (parity, rank) slot
+
+struct PeerArgs {
+    char* buf[kPeerMaxWorld];   // every rank's exchange buffer (this rank's own included)
+    int world, rank;
+    unsigned* ctl;              // this rank's [0] generation, [1] ticket, [2] error
+};
+
+enum { kPeerSumF32 = 0, kPeerSumResid = 1, kPeerMaxU64 = 2, kPeerGather = 3 };
+
+__device__ __forceinline__ unsigned* peer_flag(char* b, int par, int src, int blk) {
+    return reinterpret_cast<unsigned*>(b) + (par * kPeerMaxWorld + src) * kPeerBlocks + blk;
+}
+__device__ __forceinline__ char* peer_slot(char* b, int par, int src) {
+    return b + kPeerFlagBytes + (int64_t)(par * kPeerMaxWorld + src) * kPeerCap;
+}
+
+// n elements of 4 (f32 / gather words) or 8 (u64) bytes; dst: f32 sum, u64 max, gathered
+// words [world][n], or (kPeerSumResid) the bf16 residual stream x updated in place
+template <int OP>
+__global__ __launch_bounds__(256) void peer_kernel(PeerArgs A, const void* src, void* dst, int64_t n) {
+    using T = typename std::conditional<OP == kPeerMaxU64, uint64_t, uint32_t>::type;
+    __shared__ unsigned e_s;
+    const int blk = blockIdx.x, tid = threadIdx.x;
+    if (tid == 0) e_s = __hip_atomic_load(A.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const unsigned e = e_s;
+    const int par = e & 1;
+    // this block's slice (resid: whole groups of 8 so the bf16 row is read in 16-B pieces)
+    const int64_t gran = OP == kPeerSumResid ? 8 : 1;
+    const int64_t ng = (n + gran - 1) / gran;
+    const int64_t i0 = (ng * blk / kPeerBlocks) * gran, i1 = (ng * (blk + 1) / kPeerBlocks) * gran;
+    const int64_t e1 = i1 < n ? i1 : n;
+    const T* in = reinterpret_cast<const T*>(src);
+    for (int q = 0; q < A.world; q++) {
+        T* slot = reinterpret_cast<T*>(peer_slot(A.buf[q], par, A.rank));
+        for (int64_t i = i0 + tid; i < e1; i += 256) slot[i] = in[i];
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (tid < A.world)
+        __hip_atomic_store(peer_flag(A.buf[tid], par, A.rank, blk), e + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (tid < A.world) {   // wait for rank tid's push of this block's slice
+        const unsigned* f = peer_flag(A.buf[A.rank], par, tid, blk);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != e + 1) {
+            __builtin_amdgcn_s_sleep(2);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {   // ~2 s at 100 MHz
+                __hip_atomic_store(A.ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    __threadfence_system();
+    char* mine = A.buf[A.rank];
+    if constexpr (OP == kPeerGather) {
+        for (int q = 0; q < A.world; q++) {
+            const T* sl = reinterpret_cast<const T*>(peer_slot(mine, par, q));
+            T* out = reinterpret_cast<T*>(dst) + (int64_t)q * n;
+            for (int64_t i = i0 + tid; i < e1; i += 256) out[i] = sl[i];
+        }
+    } else if constexpr (OP == kPeerSumResid) {
+        uint16_t* x = reinterpret_cast<uint16_t*>(dst);
+        for (int64_t i = i0 + tid; i < e1; i += 256) {
+            float s = reinterpret_cast<const float*>(peer_slot(mine, par, 0))[i];
+            for (int q = 1; q < A.world; q++) s += reinterpret_cast<const float*>(peer_slot(mine, par, q))[i];
+            x[i] = f2bf(bf2f(x[i]) + rbf(s));
+        }
+    } else {
+        for (int64_t i = i0 + tid; i < e1; i += 256) {
+            if constexpr (OP == kPeerSumF32) {
+                float s = reinterpret_cast<const float*>(peer_slot(mine, par, 0))[i];
+                for (int q = 1; q < A.world; q++) s += reinterpret_cast<const float*>(peer_slot(mine, par, q))[i];
+                reinterpret_cast<float*>(dst)[i] = s;
+            } else {
+                uint64_t s = reinterpret_cast<const uint64_t*>(peer_slot(mine, par, 0))[i];
+                for (int q = 1; q < A.world; q++) {
+                    const uint64_t v = reinterpret_cast<const uint64_t*>(peer_slot(mine, par, q))[i];
+                    s = v > s ? v : s;
+                }
+                reinterpret_cast<uint64_t*>(dst)[i] = s;
+            }
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {   // the last block of this generation advances it
+        const unsigned old = __hip_atomic_fetch_add(A.ctl + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == kPeerBlocks - 1) {
+            __hip_atomic_store(A.ctl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(A.ctl, e + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+struct PeerComm : qie_comm {
+    char* own = nullptr;          // this rank's exchange buffer (uncached)
+    unsigned* ctl = nullptr;      // generation, ticket, error
+    char* peer[kPeerMaxWorld] = {};
+    bool opened[kPeerMaxWorld] = {};   // IPC-mapped (closed on destroy)
+    float* tmp = nullptr;
+    size_t tmp_bytes = 0;
+    ~PeerComm() override {
+        for (int r = 0; r < kPeerMaxWorld; r++)
+            if (opened[r] && peer[r]) hipIpcCloseMemHandle(peer[r]);
+        if (own_alloc && own) hipFree(own);
+        if (ctl) hipFree(ctl);
+        if (tmp) hipFree(tmp);
+    }
+    bool own_alloc = true;
+    PeerArgs args() const {
+        PeerArgs a{};
+        for (int r = 0; r < world; r++) a.buf[r] = peer[r];
+        a.world = world;
+        a.rank = rank;
+        a.ctl = ctl;
+        return a;
+    }
+    template <int OP>
+    int run(const void* src, void* dst, int64_t n, hipStream_t st) {
+        hipLaunchKernelGGL((peer_kernel<OP>), dim3(kPeerBlocks), dim3(256), 0, st, args(), src, dst, n);
+        QIE_LAUNCH_CHECK();
+        return 0;
+    }
+    // large exchanges (prefill rows) go through in slot-sized chunks, one generation each
+    int allreduce_sum_f32(float* buf, int64_t n, hipStream_t st) override {
+        const int64_t per = kPeerCap / 4;
+        for (int64_t o = 0; o < n; o += per) QIE_TRY_C(run<kPeerSumF32>(buf + o, buf + o, std::min(per, n - o), st));
+        return 0;
+    }
+    int allreduce_residual_bf16(const float* part, uint16_t* x, int64_t n, hipStream_t st) override {
+        const int64_t per = kPeerCap / 4;   // a multiple of 8
+        for (int64_t o = 0; o < n; o += per)
+            QIE_TRY_C(run<kPeerSumResid>(part + o, x + o, std::min(per, n - o), st));
+        return 0;
+    }
+    int allreduce_max_u64(uint64_t* buf, int64_t n, hipStream_t st) override {
+        const int64_t per = kPeerCap / 8;
+        for (int64_t o = 0; o < n; o += per) QIE_TRY_C(run<kPeerMaxU64>(buf + o, buf + o, std::min(per, n - o), st));
+        return 0;
+    }
+    int allgather(const void* send, void* recv, int64_t bytes, hipStream_t st) override {
+        QIE_REQUIRE(bytes % 4 == 0, "peer allgather: bytes must be a multiple of 4");
+        const int64_t words = bytes / 4, per = kPeerCap / 4;
+        if (words <= per) return run<kPeerGather>(send, recv, words, st);
+        // chunked: gather each chunk into tmp [world][chunk], then scatter into recv rows
+        if ((size_t)(world * per * 4) > tmp_bytes) {
+            if (tmp) hipFree(tmp);
+            tmp = nullptr;
+            QIE_HIP(hipMalloc((void**)&tmp, (size_t)world * per * 4));
+            tmp_bytes = (size_t)world * per * 4;
+        }
+        for (int64_t o = 0; o < words; o += per) {
+            const int64_t c = std::min(per, words - o);
+            QIE_TRY_C(run<kPeerGather>((const uint32_t*)send + o, tmp, c, st));
+            for (int r = 0; r < world; r++)
+                QIE_HIP(hipMemcpyAsync((char*)recv + (int64_t)r * bytes + o * 4, (char*)tmp + (int64_t)r * c * 4,
+                                       (size_t)c * 4, hipMemcpyDeviceToDevice, st));
+        }
+        return 0;
+    }
+    bool graph_capturable() const override { return true; }
+};
+
+static int peer_alloc(PeerComm* c) {
+    const size_t bytes = (size_t)kPeerFlagBytes + (size_t)2 * kPeerMaxWorld * kPeerCap;
+    QIE_HIP(hipExtMallocWithFlags((void**)&c->own, bytes, hipDeviceMallocUncached));
+    QIE_HIP(hipMemset(c->own, 0, kPeerFlagBytes));
+    QIE_HIP(hipMalloc((void**)&c->ctl, 64));
+    QIE_HIP(hipMemset(c->ctl, 0, 64));
+    return 0;
+}
+
 }  // namespace qie
+
+int qie_comm::allreduce_residual_bf16(const float* part, uint16_t* x, int64_t n, hipStream_t st) {
+    const int rc = allreduce_sum_f32(const_cast<float*>(part), n, st);   // the engine's own scratch
+    if (rc) return rc;
+    return qie_residual_add_f32(x, part, n, st);
+}
 
 using namespace qie;
 
@@ -223,6 +425,85 @@ int qie_comm_create_local(int32_t world, qie_comm** out) {
         out[r] = c;
     }
     return 0;
+}
+
+int qie_comm_create_peer(int32_t world, int32_t rank, int32_t device, qie_comm** out, void* handle_out) {
+    QIE_REQUIRE(out && handle_out && world >= 1 && world <= kPeerMaxWorld && rank >= 0 && rank < world,
+                "qie_comm_create_peer: bad arguments (world 1..%d)", kPeerMaxWorld);
+    QIE_HIP(hipSetDevice(device));
+    auto* c = new PeerComm();
+    c->world = world;
+    c->rank = rank;
+    const int rc = peer_alloc(c);
+    if (rc) {
+        delete c;
+        return rc;
+    }
+    c->peer[rank] = c->own;
+    hipIpcMemHandle_t h;
+    const hipError_t he = hipIpcGetMemHandle(&h, c->own);
+    if (he != hipSuccess) {
+        delete c;
+        return fail((int)he, "qie_comm_create_peer: hipIpcGetMemHandle: %s", hipGetErrorString(he));
+    }
+    static_assert(sizeof(hipIpcMemHandle_t) <= QIE_COMM_PEER_HANDLE_BYTES, "IPC handle size");
+    std::memset(handle_out, 0, QIE_COMM_PEER_HANDLE_BYTES);
+    std::memcpy(handle_out, &h, sizeof(h));
+    *out = c;
+    return 0;
+}
+
+int qie_comm_peer_connect(qie_comm* comm, const void* handles) {
+    auto* c = dynamic_cast<PeerComm*>(comm);
+    QIE_REQUIRE(c && handles, "qie_comm_peer_connect: not a peer communicator");
+    for (int r = 0; r < c->world; r++) {
+        if (r == c->rank) continue;
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, (const char*)handles + (int64_t)r * QIE_COMM_PEER_HANDLE_BYTES, sizeof(h));
+        void* p = nullptr;
+        const hipError_t he = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+        if (he != hipSuccess)
+            return fail((int)he, "qie_comm_peer_connect: rank %d: hipIpcOpenMemHandle: %s", r, hipGetErrorString(he));
+        c->peer[r] = (char*)p;
+        c->opened[r] = true;
+    }
+    return 0;
+}
+
+int qie_comm_create_peer_local(int32_t world, qie_comm** out) {
+    QIE_REQUIRE(out && world >= 1 && world <= kPeerMaxWorld, "qie_comm_create_peer_local: world must be 1..%d",
+                kPeerMaxWorld);
+    std::vector<PeerComm*> cs;
+    for (int r = 0; r < world; r++) {
+        auto* c = new PeerComm();
+        c->world = world;
+        c->rank = r;
+        const int rc = peer_alloc(c);
+        if (rc) {
+            delete c;
+            for (auto* d : cs) delete d;
+            return rc;
+        }
+        cs.push_back(c);
+    }
+    for (auto* c : cs)
+        for (int r = 0; r < world; r++) c->peer[r] = cs[r]->own;
+    for (int r = 0; r < world; r++) out[r] = cs[r];
+    return 0;
+}
+
+int qie_comm_peer_error(const qie_comm* comm, int32_t* err) {
+    auto* c = dynamic_cast<const PeerComm*>(comm);
+    QIE_REQUIRE(c && err, "qie_comm_peer_error: not a peer communicator");
+    unsigned v[3] = {0, 0, 0};
+    QIE_HIP(hipMemcpy(v, c->ctl, sizeof(v), hipMemcpyDeviceToHost));
+    *err = (int32_t)v[2];
+    return 0;
+}
+
+int qie_comm_allreduce_residual_bf16(qie_comm* c, const float* part, void* x, int64_t n, void* stream) {
+    QIE_REQUIRE(c && part && x && n >= 0, "qie_comm_allreduce_residual_bf16: bad arguments");
+    return c->allreduce_residual_bf16(part, (uint16_t*)x, n, (hipStream_t)stream);
 }
 
 int qie_comm_rank(const qie_comm* c, int32_t* world, int32_t* rank) {

@@ -427,8 +427,7 @@ static int row_parallel(qie_batch* b, qie_linear_args& a, uint16_t* x, float* pa
     a.epilogue = QIE_EPI_F32;
     QIE_TRY(qie_linear(&a, e->stream));
     const int64_t n = rows * e->spec.hidden;
-    QIE_TRY(e->comm->allreduce_sum_f32(part, n, e->stream));
-    return qie_residual_add_f32(x, part, n, e->stream);
+    return e->comm->allreduce_residual_bf16(part, x, n, e->stream);   // one kernel on the peer backend
 }
 
 // Batched rows (2 <= M <= 16, the skinny MFMA kernel): RMSNorm the M rows once into b->xn

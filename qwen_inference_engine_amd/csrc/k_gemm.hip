@@ -17,6 +17,9 @@
 #include "qie_common.hpp"
 #include "../../include/qie/qie_ops.h"
 
+#include <map>
+#include <mutex>
+
 namespace qie {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -426,6 +429,345 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p, int n_mt) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Prefill GEMM, phase-interleaved (round 4; cdna_hip_programming.md §5 "The 256² 8-phase
+// template", written for this NT layout).  256x256 block tile, BK = 64, 8 waves as 2 (M) x 4
+// (N), 128x64 per wave = 8x4 accumulators; LDS = two 64-KB k-tile buffers (A rows then W
+// rows, 128-B rows, 16-B chunk c of row r at c ^ ((r >> 1) & 7): conflict-free
+// ds_read_b128 for the 16x16x32 fragments).  A k-tile is consumed in FOUR phases, one C
+// quadrant (64 x 32 per wave, 16 MFMAs) each:
+//   P1 (qa0, qb0) reads A[qa0] + B[qb0]    P2 (qa0, qb1) reads B[qb1]
+//   P3 (qa1, qb1) reads A[qa1]             P4 (qa1, qb0) (B[qb0] kept in registers)
+// and the k-tile is staged as four 16-KB units in the order it is read: UA0 (the qa0 A rows
+// of both M halves), UB0, UB1, UA1 (2 LDS-DMA instructions per wave each).  Phase P3 of tile
+// t stages UA0(t+2), P4 UB0(t+2), P1 of t+1 UB1(t+2), P2 of t+1 UA1(t+2): every unit lands in
+// its buffer >= 2 phases after the last read of what it overwrites, and is read 5-6 phases
+// after it was issued.  Each phase = [fragment reads, one unit's DMAs, the counted wait]
+// s_barrier [lgkmcnt(0), 16 MFMAs] s_barrier; the wait is vmcnt(8) at the end of P4, P1,
+// P2 (the unit read next phase has landed; 4 units stay in flight), never 0 before the
+// last two tiles.  Waves 4-7 run one barrier behind waves 0-3 (an extra s_barrier before the
+// loop, waves 0-3 one after it), so on every SIMD one wave's MFMAs overlap the other
+// wave's reads and DMA issue.  Accumulation order per output = k order (as gemm_big).
+typedef unsigned int u32x4_g8 __attribute__((ext_vector_type(4)));
+namespace g8 {
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int BUF = (BM + BN) * BK * 2;   // 64 KB: A rows [0, 256) then W rows, 128 B each
+}  // namespace g8
+
+__device__ __forceinline__ int g8_swz(int r) { return (r >> 1) & 7; }
+
+// Split-K (tiles < CUs: Qwen2-7B O / down at 2,048 rows have 112 256x256 tiles, QKV 144): the
+// k-tiles of a tile are cut into `splitk` consecutive parts, one workgroup each (the remap
+// keeps a tile's parts on one XCD).  Every part stores its fp32 accumulators write-through
+// (sc1) into its slab [tile][part] (256 KB, each lane's 16-B accumulator quads in fragment
+// order), drains, and adds to the tile's ticket; the part whose add comes last sums the slabs
+// in PART order (sc1 loads: cdna_hip_programming.md §5 'Projection GEMM' item 2), so the result
+// does not depend on arrival order, runs the epilogue and resets the ticket.
+struct G8Split {
+    int splitk;
+    float* slab;       // [tiles][splitk][256 * 256] fp32
+    unsigned* cnt;     // [tiles], zero at rest
+};
+
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm8_kernel(GemmParams p, int n_mt, G8Split sk) {
+#pragma clang fp contract(off)
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    const int fr = lane & 15, g = lane >> 4;
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int q8 = nwg >> 3, r8 = nwg & 7, xcd = orig & 7;
+    const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+    const int tile = wid / sk.splitk, part = wid % sk.splitk;
+    const int64_t mt = tile % n_mt, nt = tile / n_mt;
+    const int64_t m0 = mt * g8::BM;
+
+    // DMA sources: unit u (0 UA0, 1 UB0, 2 UB1, 3 UA1), instruction i of this wave moves the
+    // 8-row block b = 2 wave + i of the unit; lane -> row + (lane >> 3), LDS chunk lane & 7
+    // (holding source chunk (lane & 7) ^ swz(row))
+    const uint16_t* src[4][2];
+    int dst_row[4][2];   // tile row of the block (A: 0..255, W: 0..255), wave-uniform
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const int b = 2 * wave + i;
+            int row0;
+            if (u == 0 || u == 3) row0 = (b < 8 ? 8 * b : 128 + 8 * (b - 8)) + (u == 3 ? 64 : 0);
+            else row0 = 64 * (b >> 2) + 8 * (b & 3) + (u == 2 ? 32 : 0);
+            dst_row[u][i] = row0;
+            const int r = row0 + (lane >> 3);
+            const int cs = (lane & 7) ^ g8_swz(r);
+            if (u == 0 || u == 3) {
+                int64_t ar = m0 + r;
+                ar = ar < p.M ? ar : p.M - 1;   // rows past M: re-read row M-1, never stored
+                src[u][i] = p.A + ar * p.lda + cs * 8;
+            } else {
+                src[u][i] = big_wrow<EPI, 256>(p, nt, r) + cs * 8;
+            }
+        }
+    const int nk_all = (int)(p.K / g8::BK);
+    const int kb = (int)((int64_t)part * nk_all / sk.splitk);        // this part's k-tiles [kb, kb + nk)
+    const int nk = (int)((int64_t)(part + 1) * nk_all / sk.splitk) - kb;
+    auto stage = [&](int u, int kt) {   // unit u of local k-tile kt into buffer kt & 1
+        unsigned char* buf = smem + (kt & 1) * g8::BUF + ((u == 0 || u == 3) ? 0 : g8::BM * 128);
+        const int64_t k0 = (int64_t)(kb + kt) * g8::BK;
+#pragma unroll
+        for (int i = 0; i < 2; i++) glds16(src[u][i] + k0, buf + dst_row[u][i] * 128);
+    };
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
+
+    auto read_a = [&](const unsigned char* buf, int qa) {
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; s2++) {
+                const int row = 128 * wm + 64 * qa + 16 * i + fr;
+                fa[i][s2] = *reinterpret_cast<const bf16x8*>(buf + row * 128 + (((4 * s2 + g) ^ g8_swz(row)) * 16));
+            }
+    };
+    auto read_b = [&](const unsigned char* buf, int qb, bf16x8 (&fb)[2][2]) {
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; s2++) {
+                const int row = 64 * wn + 32 * qb + 16 * j + fr;
+                fb[j][s2] = *reinterpret_cast<const bf16x8*>(buf + g8::BM * 128 + row * 128 +
+                                                             (((4 * s2 + g) ^ g8_swz(row)) * 16));
+            }
+    };
+    auto mfma_q = [&](int qa, int qb, const bf16x8 (&fb)[2][2]) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; s2++)
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < 2; j++)
+                    acc[4 * qa + i][2 * qb + j] =
+                        __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s2], fb[j][s2], acc[4 * qa + i][2 * qb + j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto bar = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto wait8 = [&](bool tail) {
+        if (tail) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    };
+
+    // prologue: UA0(0) UB0(0) UB1(0) UA1(0) UA0(1) UB0(1); P1(0) reads UA0(0), UB0(0)
+    stage(0, 0); stage(1, 0); stage(2, 0); stage(3, 0);
+    stage(0, 1); stage(1, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    bar();
+    if (wm == 1) bar();   // waves 4-7 one barrier behind
+    for (int t = 0; t < nk; t++) {
+        const unsigned char* buf = smem + (t & 1) * g8::BUF;
+        const bool tail = t >= nk - 2;
+        // ---- P1 (qa0, qb0): reads A[qa0], B[qb0]; stages UB1(t+1); retires UB1(t)
+        read_b(buf, 0, fb0);
+        __builtin_amdgcn_sched_barrier(0);
+        read_a(buf, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + 1 < nk) stage(2, t + 1);
+        wait8(tail);
+        bar();
+        mfma_q(0, 0, fb0);
+        bar();
+        // ---- P2 (qa0, qb1): reads B[qb1]; stages UA1(t+1); retires UA1(t)
+        read_b(buf, 1, fb1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + 1 < nk) stage(3, t + 1);
+        wait8(tail);
+        bar();
+        mfma_q(0, 1, fb1);
+        bar();
+        // ---- P3 (qa1, qb1): reads A[qa1]; stages UA0(t+2)
+        read_a(buf, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + 2 < nk) stage(0, t + 2);
+        bar();
+        mfma_q(1, 1, fb1);
+        bar();
+        // ---- P4 (qa1, qb0): B[qb0] from registers; stages UB0(t+2); retires UA0/UB0(t+1)
+        if (t + 2 < nk) stage(1, t + 2);
+        wait8(tail);
+        bar();
+        mfma_q(1, 0, fb0);
+        bar();
+    }
+    if (wm == 0) bar();   // balance the barrier count of the two wave groups
+
+    if (sk.splitk > 1) {   // uniform
+        // this wave's quads: slab float offset ((wave * 32 + i * 4 + j) * 64 + lane) * 4
+        const int64_t tb = (int64_t)tile * sk.splitk;
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(sk.slab + (tb + part) * 65536, (short)0, 65536 * 4, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_g8, acc[i][j]), rs,
+                                                       ((wave * 32 + i * 4 + j) * 64 + lane) * 16, 0, 16);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
+        __syncthreads();
+        int* flag = reinterpret_cast<int*>(smem);   // the staging array is free (one LDS object)
+        if (tid == 0) {
+            const unsigned old = __hip_atomic_fetch_add(sk.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            *flag = old == (unsigned)sk.splitk - 1 ? 1 : 0;
+        }
+        __syncthreads();
+        if (*flag == 0) return;   // uniform
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int q = 0; q < sk.splitk; q++) {   // part order: independent of who arrived last
+            const auto rq = __builtin_amdgcn_make_buffer_rsrc(sk.slab + (tb + q) * 65536, (short)0, 65536 * 4, 0x00020000);
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                  rq, ((wave * 32 + i * 4 + j) * 64 + lane) * 16, 0, 16));
+                    acc[i][j] = q == 0 ? v : acc[i][j] + v;
+                }
+        }
+        if (tid == 0) __hip_atomic_store(sk.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+
+    // ---------------- epilogue (as gemm_big_kernel at BNT = 256)
+    constexpr int NJ = 4;
+    if constexpr (EPI == QIE_EPI_SWIGLU) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+#pragma unroll
+            for (int jj = 0; jj < NJ / 2; jj++) {
+                const int64_t col = nt * 128 + 32 * wn + 16 * jj + fr;
+                if (col >= p.N) continue;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int64_t row = m0 + wm * 128 + i * 16 + g * 4 + r;
+                    if (row >= p.M) continue;
+                    const float gg = rbf(acc[i][jj][r]);
+                    const float uu = rbf(acc[i][jj + NJ / 2][r]);
+                    const float av = rbf(gg * (1.0f / (1.0f + expf(-gg))));
+                    p.C[row * p.ldc + col] = f2bf(uu * av);
+                }
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < NJ; j++) {
+            const int64_t col = nt * 256 + wn * 64 + j * 16 + fr;
+            if (col >= p.N) continue;
+            float bias = 0.f;
+            if constexpr (EPI == QIE_EPI_STORE) {
+                const uint16_t* b = col < p.n0 ? p.b0 : (col < p.n01 ? p.b1 : p.b2);
+                if (b) bias = bf2f(b[col < p.n0 ? col : (col < p.n01 ? col - p.n0 : col - p.n01)]);
+            }
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int64_t row = m0 + wm * 128 + i * 16 + g * 4 + r;
+                    if (row >= p.M) continue;
+                    if constexpr (EPI == QIE_EPI_F32) {
+                        reinterpret_cast<float*>(p.C)[row * p.ldc + col] = acc[i][j][r];
+                        continue;
+                    }
+                    uint16_t* dst = p.C + row * p.ldc + col;
+                    if constexpr (EPI == QIE_EPI_RESIDUAL)
+                        *dst = f2bf(bf2f(*dst) + rbf(acc[i][j][r]));
+                    else
+                        *dst = f2bf(acc[i][j][r] + bias);
+                }
+            }
+        }
+    }
+}
+
+template <int EPI>
+static int launch_gemm8_t(const GemmParams& p, int n_mt, int n_tiles, const G8Split& sk, hipStream_t st) {
+    const void* fn = (const void*)gemm8_kernel<EPI>;
+    constexpr size_t shm = 2 * (size_t)g8::BUF;
+    static bool raised = false;
+    if (!raised) {
+        QIE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+        raised = true;
+    }
+    hipLaunchKernelGGL((gemm8_kernel<EPI>), dim3((unsigned)(n_tiles * sk.splitk)), dim3(512), shm, st, p, n_mt, sk);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+static int launch_gemm8(int epi, const GemmParams& p, int n_mt, int n_tiles, const G8Split& sk, hipStream_t st) {
+    if (epi == QIE_EPI_SWIGLU) return launch_gemm8_t<QIE_EPI_SWIGLU>(p, n_mt, n_tiles, sk, st);
+    if (epi == QIE_EPI_RESIDUAL) return launch_gemm8_t<QIE_EPI_RESIDUAL>(p, n_mt, n_tiles, sk, st);
+    if (epi == QIE_EPI_F32) return launch_gemm8_t<QIE_EPI_F32>(p, n_mt, n_tiles, sk, st);
+    return launch_gemm8_t<QIE_EPI_STORE>(p, n_mt, n_tiles, sk, st);
+}
+
+// Split-K slabs + tickets, one set per stream (streams of one device may run GEMMs at the same
+// time: tensor-parallel ranks on one GPU in the tests), grown on demand outside graph capture.
+struct G8Ws {
+    float* slab = nullptr;
+    unsigned* cnt = nullptr;
+    size_t slab_bytes = 0, cnt_n = 0;
+};
+static std::mutex g8_mu;
+static std::map<hipStream_t, G8Ws> g8_ws;
+
+static int g8_workspace(hipStream_t st, int tiles, int splitk, G8Split* out) {
+    std::lock_guard<std::mutex> lk(g8_mu);
+    G8Ws& w = g8_ws[st];
+    const size_t need = (size_t)tiles * splitk * 65536 * 4;
+    if (need > w.slab_bytes || (size_t)tiles > w.cnt_n) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return 1;   // no split
+        QIE_HIP(hipStreamSynchronize(st));
+        if (w.slab) hipFree(w.slab);
+        if (w.cnt) hipFree(w.cnt);
+        w = G8Ws{};
+        QIE_HIP(hipMalloc((void**)&w.slab, need));
+        QIE_HIP(hipMalloc((void**)&w.cnt, (size_t)tiles * 4));
+        QIE_HIP(hipMemset(w.cnt, 0, (size_t)tiles * 4));
+        w.slab_bytes = need;
+        w.cnt_n = tiles;
+    }
+    out->slab = w.slab;
+    out->cnt = w.cnt;
+    out->splitk = splitk;
+    return 0;
+}
+
+// parts per tile: the fewest rounds of (tile, part) items over the CUs, in units of a tile
+// (112 tiles: 2 parts = one round of half tiles; 144 tiles: 3 parts, two rounds of thirds)
+static int g8_splitk(int64_t tiles, int64_t cus, int nk) {
+    int best = 1;
+    double best_t = 1e30;
+    for (int s = 1; s <= 4 && nk / s >= 4; s++) {
+        const double t = (double)((tiles * s + cus - 1) / cus) / s;
+        if (t < best_t - 1e-9) {
+            best_t = t;
+            best = s;
+        }
+    }
+    return best;
+}
+
 template <int EPI, int BNT>
 static int launch_gemm_big_t(const GemmParams& p, int n_mt, int n_tiles, hipStream_t st) {
     const void* fn = (const void*)gemm_big_kernel<EPI, BNT>;
@@ -500,6 +842,19 @@ int gemm(const qie_linear_args* a, hipStream_t st) {
         const int64_t cus = device_cu_count();
         const int force = (a->flags & QIE_LINEAR_TILE256) ? 1 : (a->flags & QIE_LINEAR_TILE128) ? 2
                                                                                             : dev_env("QIE_GEMM_BIG", -1);
+        // phase-interleaved 256x256 kernel (QIE_GEMM8, dev A/B; K a multiple of 64, >= 4 k-tiles)
+        const bool g8ok = a->K % g8::BK == 0 && a->K >= 4 * g8::BK;
+        const int g8mode = dev_env("QIE_GEMM8", 0);   // 1: full-chip grids only, 2: also split-K below
+        if (g8ok && g8mode != 0 && force != 2 && (force == 1 || (force < 0 && a->M >= big::BM && t256 >= cus))) {
+            G8Split sk{1, nullptr, nullptr};
+            return launch_gemm8(a->epilogue, p, (int)n_mt, (int)t256, sk, st);
+        }
+        if (g8ok && g8mode == 2 && force < 0 && a->M >= big::BM && t256 < cus) {
+            const int s = g8_splitk(t256, cus, (int)(a->K / g8::BK));
+            G8Split sk{1, nullptr, nullptr};
+            if (s == 1 || g8_workspace(st, (int)t256, s, &sk) == 0)
+                return launch_gemm8(a->epilogue, p, (int)n_mt, (int)t256, sk, st);
+        }
         if (force == 1 || (force < 0 && a->M >= big::BM && t256 >= cus))
             return launch_gemm_big<256>(a->epilogue, p, (int)n_mt, (int)t256, st);
         if (force == 2 || (force < 0 && a->M >= big::BM && t128 >= (3 * cus) / 4 && t128 <= cus))

@@ -418,7 +418,7 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
         // the weight stream's first HBM round trip overlaps the x round trip instead of
         // following it (vmcnt retires in order: x must be issued first).
         constexpr int NV = XCH <= 5 ? XCH : 1;   // norm weights: fused-norm variants only (XCH <= 5)
-        const bool nrm = NV == XCH && p.norm_w != nullptr;
+        const bool nrm = NV == XCH && p.norm_w != nullptr && !QIE_DBG(p.dbg & 1);   // dev: 1 skips the norm
         uint4 xv[XCH], nv[NV];
 #pragma unroll
         for (int c = 0; c < XCH; c++) {
@@ -653,7 +653,8 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
                         const int64_t c = col[i] < p.N ? col[i] : p.N - 1;
                         float v = acc[m][i];
                         const uint16_t* b = c < p.n0 ? p.b0 : (c < p.n01 ? p.b1 : p.b2);
-                        if (epre_on && task == task0) {
+                        if (QIE_DBG(p.dbg & 2)) {   // dev: 2 skips the bias
+                        } else if (epre_on && task == task0) {
                             if (b) v = v + bf2f(epre_v[EPRE ? i : 0]);
                         } else if (b) {
                             int64_t bi = c < p.n0 ? c : (c < p.n01 ? c - p.n0 : c - p.n01);
@@ -1380,6 +1381,7 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
         }
     }
     if (a->M > 8) return gemm(a, st);   // 9..16 rows the skinny kernel could not take
+    p.dbg = a->M == 1 ? env_int("QIE_GEMV_DBG", 0) : 0;   // dev timing experiments (1 no norm, 2 no bias)
     const int MT = a->M <= 1 ? 1 : a->M <= 2 ? 2 : a->M <= 4 ? 4 : 8;
     p.xlds = ((size_t)MT * a->K * 2 <= kGemvLdsCap) ? 1 : 0;
     QIE_REQUIRE(p.xlds || !p.norm_w,
@@ -1433,7 +1435,8 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
     // Normalised x in every wave's registers (XCH 4): no LDS image, no barrier (A/B knobs
     // QIE_GEMV_XREG4 for the STORE projections (QKV, lm_head) and QIE_GEMV_XREG4_SW for gate/up)
     if (MT == 1 && p.M == 1 && p.norm_w && a->K % 8 == 0 && a->K <= 4096 &&
-        env_int(a->epilogue == QIE_EPI_SWIGLU ? "QIE_GEMV_XREG4_SW" : "QIE_GEMV_XREG4", 0) != 0) {
+        env_int(a->epilogue == QIE_EPI_SWIGLU ? "QIE_GEMV_XREG4_SW" : (vocab_rows ? "QIE_GEMV_XREG4_LM" : "QIE_GEMV_XREG4"),
+                0) != 0) {
         xch = 4;
         p.xlds = 0;
     }

@@ -603,6 +603,24 @@ int qie_synchronize(void) {
     return 0;
 }
 
+int qie_stream_create(void** stream_out) {
+    QIE_REQUIRE(stream_out, "qie_stream_create: null output");
+    hipStream_t st = nullptr;
+    QIE_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    *stream_out = st;
+    return 0;
+}
+
+int qie_stream_synchronize(void* stream) {
+    QIE_HIP(hipStreamSynchronize((hipStream_t)stream));
+    return 0;
+}
+
+int qie_stream_destroy(void* stream) {
+    if (stream) QIE_HIP(hipStreamDestroy((hipStream_t)stream));
+    return 0;
+}
+
 int qie_rope_table_host(float* cos_out, float* sin_out, int32_t n_pos, int32_t head_dim,
                         float theta, int32_t numerics) {
     QIE_REQUIRE(cos_out && sin_out && n_pos > 0 && head_dim > 0 && head_dim % 2 == 0,

@@ -1,7 +1,7 @@
 // qie_comm.hpp — internal definition of the tensor-parallel communicator behind the
 // opaque qie_comm handle of qie_engine.h.
 //
-// Two backends:
+// Three backends (the peer one in comm.hip's header comment):
 //   * RCCL (one process per GPU, xGMI): ncclAllReduce / ncclAllGather enqueued on the
 //     engine stream, so they are captured into the decode hipGraph;
 //   * local (test backend): `world` ranks driven by host threads of ONE process, all
@@ -23,4 +23,7 @@ struct qie_comm {
     // recv = [world][bytes], rank r's send at offset r * bytes
     virtual int allgather(const void* send, void* recv, int64_t bytes, hipStream_t st) = 0;
     virtual bool graph_capturable() const = 0;
+    // x (bf16 [n]) = bf16(x + bf16(all-reduced sum of part)): the row-parallel exchange; the
+    // peer backend does it in one kernel, the others all-reduce `part` in place and add
+    virtual int allreduce_residual_bf16(const float* part, uint16_t* x, int64_t n, hipStream_t st);
 };

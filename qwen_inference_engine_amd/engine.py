@@ -92,6 +92,33 @@ class Comm:
         return Comm(h.value, lib)
 
     @staticmethod
+    def peer(world: int, rank: int, device: int, exchange) -> "Comm":
+        """Peer backend across processes: `exchange(handle_bytes) -> [handle of rank r for r
+        in range(world)]` is the host channel (e.g. dist.FileGroup.allgather)."""
+        lib = _lib.load()
+        h = C.c_void_p()
+        buf = C.create_string_buffer(_lib.QIE_COMM_PEER_HANDLE_BYTES)
+        _lib.check(lib.qie_comm_create_peer(world, rank, device, C.byref(h), buf), "qie_comm_create_peer")
+        comm = Comm(h.value, lib)
+        hs = exchange(buf.raw)
+        allh = C.create_string_buffer(b"".join(hs), _lib.QIE_COMM_PEER_HANDLE_BYTES * world)
+        _lib.check(lib.qie_comm_peer_connect(h, allh), "qie_comm_peer_connect")
+        return comm
+
+    @staticmethod
+    def peer_local(world: int) -> List["Comm"]:
+        """Peer backend for `world` ranks of this process on one device (graph-capturable)."""
+        lib = _lib.load()
+        hs = (C.c_void_p * world)()
+        _lib.check(lib.qie_comm_create_peer_local(world, hs), "qie_comm_create_peer_local")
+        return [Comm(hs[r], lib) for r in range(world)]
+
+    def peer_error(self) -> int:
+        e = C.c_int32()
+        _lib.check(self.lib.qie_comm_peer_error(self.h, C.byref(e)), "qie_comm_peer_error")
+        return e.value
+
+    @staticmethod
     def local(world: int) -> List["Comm"]:
         lib = _lib.load()
         hs = (C.c_void_p * world)()

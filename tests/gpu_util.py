@@ -89,6 +89,32 @@ def host(t: DBuf) -> np.ndarray:
     return t.numpy()
 
 
+def to_bf16(a: np.ndarray) -> np.ndarray:
+    """fp32 -> bf16 bits, round to nearest even (finite values)."""
+    u = np.ascontiguousarray(a, np.float32).view(np.uint32).astype(np.uint64)
+    return ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+
+
+def stream() -> int:
+    """A new non-blocking stream (qie_stream_create), kept alive with the test's buffers."""
+    import ctypes as C
+    h = C.c_void_p()
+    check(L().qie_stream_create(C.byref(h)), "stream")
+    _LIVE.append(_Stream(h.value))
+    return h.value
+
+
+class _Stream:
+    def __init__(self, h):
+        self.h = h
+
+    def __del__(self):
+        try:
+            L().qie_stream_destroy(self.h)
+        except Exception:
+            pass
+
+
 def p(t) -> int:
     return None if t is None else t.ptr
 

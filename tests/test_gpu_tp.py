@@ -45,9 +45,11 @@ def logit_tol(want):
     return LOGIT_ULPS * 2.0 ** -7 * max(1.0, float(np.abs(G.bf(want)).max()))
 
 
-def run_ranks(world, fn, timeout=300):
-    """fn(rank, comm) on `world` threads; returns the per-rank results, re-raises failures."""
-    comms = Q.Comm.local(world)
+def run_ranks(world, fn, timeout=300, backend="local"):
+    """fn(rank, comm) on `world` threads; returns the per-rank results, re-raises failures.
+    backend "local" (host barriers, engines eager) or "peer" (qie_comm_create_peer_local:
+    one-kernel exchanges, engines capture their decode graphs)."""
+    comms = Q.Comm.local(world) if backend == "local" else Q.Comm.peer_local(world)
     out, err = [None] * world, [None] * world
 
     def body(r):
@@ -70,7 +72,7 @@ def run_ranks(world, fn, timeout=300):
     return out
 
 
-def greedy_trace(spec, world, prompt, n_new, forced=None):
+def greedy_trace(spec, world, prompt, n_new, forced=None, backend="local"):
     """Per-rank (ids, per-step logits); `forced` = ids to teacher-force after each step."""
     def fn(rank, comm):
         eng = Q.Engine(spec, max_ctx=128, comm=comm).init_synthetic(SYN)
@@ -82,8 +84,10 @@ def greedy_trace(spec, world, prompt, n_new, forced=None):
                 b.set_position(0, len(prompt) + i, forced[i])
             if i + 1 < n_new:
                 raw.append(b.decode_step()[0])
+        if backend == "peer":
+            assert comm.peer_error() == 0, "a peer exchange timed out"
         return raw, np.stack(lgs)
-    return run_ranks(world, fn)
+    return run_ranks(world, fn, backend=backend)
 
 
 @pytest.mark.parametrize("name", list(CONFIGS))
@@ -114,6 +118,105 @@ def test_tp_matches_single_gpu(name):
             assert gap <= logit_tol(ref_lgs[i]), f"step {i}: tp {t_tp} vs {ref_ids[i]} gap {gap}"
             flips += 1
     assert flips <= 2
+
+
+@pytest.mark.parametrize("name", ["qwen2-bias-hd64", "tied-tp4", "q28kv4-tp8"])
+def test_peer_backend_equals_local(name):
+    """The peer backend (one kernel per exchange: push into every rank's buffer, per-block
+    generation flags, rank-ordered reduce with the residual add fused; decode steps CAPTURED
+    in each rank's hipGraph and replayed concurrently on one GPU) produces the local
+    backend's ids and logits bit for bit: both sum the ranks in order 0..world-1."""
+    spec, world = CONFIGS[name]
+    prompt = list(rng(3).integers(0, spec.vocab, 13))
+    loc = greedy_trace(spec, world, prompt, 10)
+    peer = greedy_trace(spec, world, prompt, 10, backend="peer")
+    for r in range(world):
+        assert peer[r][0] == loc[r][0]
+        assert np.array_equal(peer[r][1], loc[r][1])
+
+
+def test_peer_comm_collectives():
+    """qie_comm peer collectives on 3 in-process ranks: the fused all-reduce + residual add
+    equals the rank-ordered fp32 sum then bf16(x + bf16(sum)) bit for bit, across the
+    2-MiB slot (chunked: several generations in one call), and so does the plain fp32
+    all-reduce; each rank runs on its own stream (a shared stream would serialise them)."""
+    lib = Q._lib.load()
+    world, n = 3, (2 << 20) // 4 + 4104        # one full slot + a remainder (multiple of 8)
+    parts = [np.random.default_rng(10 + r).standard_normal(n).astype(np.float32) for r in range(world)]
+    x0 = G.to_bf16(np.random.default_rng(5).standard_normal(n).astype(np.float32))
+    want_sum = parts[0].copy()
+    for r in range(1, world):
+        want_sum = (want_sum + parts[r]).astype(np.float32)
+    want_x = G.to_bf16(G.bf(x0) + G.bf(G.to_bf16(want_sum)))
+    comms = Q.Comm.peer_local(world)
+    bufs = [(G.dev(parts[r]), G.dev(x0), G.dev(parts[r])) for r in range(world)]
+    errs = [None] * world
+
+    def body(r):
+        try:
+            st = G.stream()
+            pb, xb, sb = bufs[r]
+            G.check(lib.qie_comm_allreduce_residual_bf16(comms[r].h, G.p(pb), G.p(xb), n, st))
+            G.check(lib.qie_comm_allreduce_sum_f32(comms[r].h, G.p(sb), n, st))
+            G.check(lib.qie_stream_synchronize(st))
+        except BaseException as ex:  # noqa: BLE001
+            errs[r] = ex
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(120)
+        assert not t.is_alive(), "peer rank hung"
+    for e in errs:
+        if e is not None:
+            raise e
+    for r in range(world):
+        assert comms[r].peer_error() == 0
+        assert np.array_equal(G.host_bf16(bufs[r][1]), want_x), f"rank {r} residual"
+        assert np.array_equal(G.host(bufs[r][2]), want_sum), f"rank {r} sum"
+    for c in comms:
+        c.close()
+
+
+def test_peer_two_processes_one_gpu(tmp_path):
+    """The peer backend ACROSS PROCESSES: two ranks as two processes on this box's one GPU,
+    each exporting its exchange buffer as a HIP IPC handle and mapping the other's
+    (tests/peer_worker.py); the fused all-reduce + residual add and the fp32 all-reduce give
+    both processes the rank-ordered result bit for bit.  Skipped (with the runtime's
+    message) where the IPC mapping of a same-device buffer is refused."""
+    import os
+    import subprocess
+    import sys
+    world, n = 2, 60000
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    worker = os.path.join(os.path.dirname(__file__), "peer_worker.py")
+    ps = [subprocess.Popen([sys.executable, worker, str(r), str(world), str(tmp_path), str(n)], env=env,
+                           stderr=subprocess.PIPE, text=True) for r in range(world)]
+    rcs, errs = [], []
+    for p in ps:
+        try:
+            _, e = p.communicate(timeout=180)
+        except subprocess.TimeoutExpired:
+            for q in ps:
+                q.kill()
+            raise AssertionError("peer worker hung")
+        rcs.append(p.returncode)
+        errs.append(e)
+    if any(rc == 5 for rc in rcs):
+        pytest.skip("IPC mapping refused: " + " | ".join(e.strip()[-300:] for e in errs if e))
+    assert rcs == [0] * world, errs
+    parts = [np.random.default_rng(10 + r).standard_normal(n).astype(np.float32) for r in range(world)]
+    want_sum = parts[0].copy()
+    for r in range(1, world):
+        want_sum = (want_sum + parts[r]).astype(np.float32)
+    x0 = G.to_bf16(np.random.default_rng(5).standard_normal(n).astype(np.float32))
+    want_x = G.to_bf16(G.bf(x0) + G.bf(G.to_bf16(want_sum)))
+    for r in range(world):
+        out = np.load(tmp_path / f"out{r}.npz")
+        assert int(out["err"]) == 0, f"rank {r}: a peer exchange timed out"
+        assert np.array_equal(out["x"], want_x), f"rank {r} residual"
+        assert np.array_equal(out["s"], want_sum), f"rank {r} sum"
 
 
 def test_tp_sampling_ranks_agree():

@@ -6,6 +6,7 @@
 #   BENCH=1    bench.py headline line without the CPU leg (BENCH_ARGS appended)
 #   AB_VARIANTS='[{}, {"QIE_X": "1"}]'  tools/ab_decode.py on the development library
 #              (AB_MODEL / AB_P / AB_STEPS / AB_ROUNDS / AB_BATCH / AB_FP8 / AB_PREFILL)
+#   AB_GEMM_VARIANTS='[{}, {"QIE_GEMM8": "1"}]'  tools/ab_gemm.py (prefill GEMMs, bit-equality + time)
 #   UB_SET     tools/ubench.py kernel variants (development library)
 #   PROFILE=1  rocprofv3 kernel trace of a short bench (PROF_ARGS appended)
 set -u
@@ -21,6 +22,10 @@ if [ "$T" != "none" ]; then
       --timeout-method thread > gpurun_out/pytest_quick.log 2>&1
   rc=$?; tail -4 gpurun_out/pytest_quick.log; echo "pytest rc=$rc"; [ $rc -eq 0 ] || exit $rc
   if [ -n "${TEST_ENV:-}" ]; then unset QIE_LIB; for kv in $TEST_ENV; do unset "${kv%%=*}"; done; fi
+fi
+if [ -n "${AB_GEMM_VARIANTS:-}" ]; then
+  QIE_LIB=$DEVLIB timeout -k 10 300 python -u tools/ab_gemm.py > gpurun_out/ab_gemm.log 2> gpurun_out/ab_gemm.err
+  rc=$?; cat gpurun_out/ab_gemm.log | cut -c1-400; tail -3 gpurun_out/ab_gemm.err; echo "ab_gemm rc=$rc"; [ $rc -eq 0 ] || exit $rc
 fi
 if [ -n "${AB_VARIANTS:-}" ]; then
   QIE_LIB=$DEVLIB timeout -k 10 ${AB_TIMEOUT:-600} python -u tools/ab_decode.py > gpurun_out/ab_decode.log 2> gpurun_out/ab_decode.err

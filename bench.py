@@ -67,6 +67,9 @@ def parse(argv=None):
     ap.add_argument("--parallel", choices=["tp", "replicas"], default="tp",
                     help="N > 1: one tensor-parallel sequence (RCCL) or N independent replicas")
     ap.add_argument("--tp", action="store_true", help="(compat) same as --parallel tp")
+    ap.add_argument("--comm", choices=["rccl", "peer"], default="rccl",
+                    help="tensor-parallel exchange: RCCL (default) or the peer backend (HIP IPC buffers, "
+                         "one kernel per exchange with the residual add fused; DESIGN.md §6)")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the other single-GPU BASELINE configs (2 and 4) in the default line")
     ap.add_argument("--dry-run", action="store_true",
@@ -146,12 +149,17 @@ def run(a):
         ok, why = S.tp_shardable(spec, world)
         if not ok:
             tp_note = f"tp{world} not possible for {spec.name} ({why}): replicas"
-        else:   # one RCCL communicator over all ranks; the unique id travels through the group
-            uid = Q.Comm.unique_id().hex() if rank == 0 else None
-            uid = group.allgather(uid)[0]
+        else:   # one communicator over all ranks; ids / IPC handles travel through the group
             err = None
+            if a.comm == "rccl":
+                uid = Q.Comm.unique_id().hex() if rank == 0 else None
+                uid = group.allgather(uid)[0]
             try:
-                comm = Q.Comm.rccl(bytes.fromhex(uid), world, rank, local)
+                if a.comm == "rccl":
+                    comm = Q.Comm.rccl(bytes.fromhex(uid), world, rank, local)
+                else:
+                    comm = Q.Comm.peer(world, rank, local,
+                                       lambda h: [bytes.fromhex(x) for x in group.allgather(h.hex())])
             except Exception as ex:   # reported in the JSON line, never silently
                 err = str(ex)
             errs = [e for e in group.allgather(err) if e]
@@ -251,6 +259,7 @@ def run(a):
         "config": {"workload": f"{spec.name} {'fp8' if a.fp8 else 'bf16'} decode, batch={B}, prompt={P}, gen={a.gen}",
                    "batch_per_gpu": B if not comm else None, "batch": B, "prompt": P, "gen": a.gen,
                    "ctx_timed": [P + 1, P + a.steps], "parallelism": par,
+                   "tp_comm": a.comm if comm else None,
                    "graph": not a.no_graph, "kv": f"paged{a.page_tokens}" if a.page_tokens else "contiguous"},
         "prefill_tok_s": round(prefill_tok_s, 1),
         "prefill_ms": round(t_prefill * 1e3, 3),

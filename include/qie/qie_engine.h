@@ -67,8 +67,9 @@ int qie_comm_create_local(int32_t world, qie_comm** out);
  * residual add fused into the row-parallel all-reduce); graph-capturable.  Across
  * processes: qie_comm_create_peer() returns this rank's QIE_COMM_PEER_HANDLE_BYTES IPC
  * handle, the host ships all handles to every rank (handles[r] = rank r's), then
- * qie_comm_peer_connect().  Ranks of one process on one device:
- * qie_comm_create_peer_local(world, out[world]).  A rank that waited ~2 s for a peer
+ * qie_comm_peer_connect().  Ranks of one process on one device (world <= 2: the
+ * process's hardware queues must give every rank its own):
+ * qie_comm_create_peer_local(world, out[world]).  A rank that waited ~10 s for a peer
  * sets the error word qie_comm_peer_error() reads (no kernel waits forever). */
 #define QIE_COMM_PEER_HANDLE_BYTES 128
 int qie_comm_create_peer(int32_t world, int32_t rank, int32_t device, qie_comm** out, void* handle_out);

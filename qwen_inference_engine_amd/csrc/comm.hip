@@ -189,8 +189,11 @@ struct LocalComm : qie_comm {
 //     first, the last block to finish (ticket) stores e + 1; data and flags alternate
 //     between two parities, and a rank can only reach generation e + 2 after every peer
 //     raised its e + 1 flags, i.e. after every peer finished reading generation e;
-//   * the wait is bounded (~2 s of s_memrealtime): a peer that never arrives sets the error
-//     word and the kernel ends (no hang); qie_comm_peer_error() reports it.
+//   * the wait is bounded (~10 s of s_memrealtime): a peer that never arrives sets the error
+//     word and the kernel ends (no hang); qie_comm_peer_error() reports it.  Every rank's
+//     collective must be able to run while another waits: one process per GPU, or (ranks of
+//     one process on one device) at most 2 ranks — a process gets 4 hardware queues, and two
+//     ranks' streams sharing one queue would serialise a waiting kernel before its peer.
 constexpr int kPeerMaxWorld = 8;
 constexpr int kPeerBlocks = 16;
 constexpr int64_t kPeerFlagBytes = 4096;             // [2][8][16] uint32 flags, padded
@@ -202,7 +205,7 @@ struct PeerArgs {
     unsigned* ctl;              // this rank's [0] generation, [1] ticket, [2] error
 };
 
-enum { kPeerSumF32 = 0, kPeerSumResid = 1, kPeerMaxU64 = 2, kPeerGather = 3 };
+enum { kPeerSumF32 = 0, kPeerSumResid = 1, kPeerMaxU64 = 2, kPeerGather = 3, kPeerGatherB = 4 };
 
 __device__ __forceinline__ unsigned* peer_flag(char* b, int par, int src, int blk) {
     return reinterpret_cast<unsigned*>(b) + (par * kPeerMaxWorld + src) * kPeerBlocks + blk;
@@ -215,7 +218,8 @@ __device__ __forceinline__ char* peer_slot(char* b, int par, int src) {
 // words [world][n], or (kPeerSumResid) the bf16 residual stream x updated in place
 template <int OP>
 __global__ __launch_bounds__(256) void peer_kernel(PeerArgs A, const void* src, void* dst, int64_t n) {
-    using T = typename std::conditional<OP == kPeerMaxU64, uint64_t, uint32_t>::type;
+    using T = typename std::conditional<OP == kPeerMaxU64, uint64_t,
+                                        typename std::conditional<OP == kPeerGatherB, uint8_t, uint32_t>::type>::type;
     __shared__ unsigned e_s;
     const int blk = blockIdx.x, tid = threadIdx.x;
     if (tid == 0) e_s = __hip_atomic_load(A.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -241,7 +245,7 @@ __global__ __launch_bounds__(256) void peer_kernel(PeerArgs A, const void* src, 
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != e + 1) {
             __builtin_amdgcn_s_sleep(2);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {   // ~2 s at 100 MHz
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull) {   // ~10 s at 100 MHz
                 __hip_atomic_store(A.ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 break;
             }
@@ -250,7 +254,7 @@ __global__ __launch_bounds__(256) void peer_kernel(PeerArgs A, const void* src, 
     __syncthreads();
     __threadfence_system();
     char* mine = A.buf[A.rank];
-    if constexpr (OP == kPeerGather) {
+    if constexpr (OP == kPeerGather || OP == kPeerGatherB) {
         for (int q = 0; q < A.world; q++) {
             const T* sl = reinterpret_cast<const T*>(peer_slot(mine, par, q));
             T* out = reinterpret_cast<T*>(dst) + (int64_t)q * n;
@@ -336,7 +340,12 @@ struct PeerComm : qie_comm {
         return 0;
     }
     int allgather(const void* send, void* recv, int64_t bytes, hipStream_t st) override {
-        QIE_REQUIRE(bytes % 4 == 0, "peer allgather: bytes must be a multiple of 4");
+        // byte-granular form for odd sizes (a vocab shard of 777 bf16 logits), small by construction
+        if (bytes % 4 != 0) {
+            QIE_REQUIRE(bytes <= kPeerCap, "peer allgather: %lld bytes (not a multiple of 4) exceed a slot",
+                        (long long)bytes);
+            return run<kPeerGatherB>(send, recv, bytes, st);
+        }
         const int64_t words = bytes / 4, per = kPeerCap / 4;
         if (words <= per) return run<kPeerGather>(send, recv, words, st);
         // chunked: gather each chunk into tmp [world][chunk], then scatter into recv rows
@@ -471,8 +480,9 @@ int qie_comm_peer_connect(qie_comm* comm, const void* handles) {
 }
 
 int qie_comm_create_peer_local(int32_t world, qie_comm** out) {
-    QIE_REQUIRE(out && world >= 1 && world <= kPeerMaxWorld, "qie_comm_create_peer_local: world must be 1..%d",
-                kPeerMaxWorld);
+    // ranks of one process share its hardware queues (4): beyond 2 ranks two of them can land
+    // on one queue, where a waiting exchange kernel blocks its own peer (see the kernel's notes)
+    QIE_REQUIRE(out && world >= 1 && world <= 2, "qie_comm_create_peer_local: world must be 1 or 2");
     std::vector<PeerComm*> cs;
     for (int r = 0; r < world; r++) {
         auto* c = new PeerComm();

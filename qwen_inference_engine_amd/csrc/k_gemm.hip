@@ -755,10 +755,13 @@ static int g8_workspace(hipStream_t st, int tiles, int splitk, G8Split* out) {
 
 // parts per tile: the fewest rounds of (tile, part) items over the CUs, in units of a tile
 // (112 tiles: 2 parts = one round of half tiles; 144 tiles: 3 parts, two rounds of thirds)
+// (short parts lose: QKV at 3 x 19 and O at 2 x 28 k-tiles measured 108 -> 112 and 71 -> 69 us,
+// the last arriver's serial slab read and the per-part pipeline fill eat the gain; down at
+// 2 x 148: 309 -> 247 us), so a part keeps >= 64 k-tiles
 static int g8_splitk(int64_t tiles, int64_t cus, int nk) {
     int best = 1;
     double best_t = 1e30;
-    for (int s = 1; s <= 4 && nk / s >= 4; s++) {
+    for (int s = 1; s <= 4 && nk / s >= 64; s++) {
         const double t = (double)((tiles * s + cus - 1) / cus) / s;
         if (t < best_t - 1e-9) {
             best_t = t;
@@ -842,9 +845,10 @@ int gemm(const qie_linear_args* a, hipStream_t st) {
         const int64_t cus = device_cu_count();
         const int force = (a->flags & QIE_LINEAR_TILE256) ? 1 : (a->flags & QIE_LINEAR_TILE128) ? 2
                                                                                             : dev_env("QIE_GEMM_BIG", -1);
-        // phase-interleaved 256x256 kernel (QIE_GEMM8, dev A/B; K a multiple of 64, >= 4 k-tiles)
+        // phase-interleaved 256x256 kernel (K a multiple of 64, >= 4 k-tiles): Qwen2-7B gate/up at 2,048
+        // rows 612 -> 488 us, bit-identical to gemm_big; down split-K 2: 309 -> 247 us
         const bool g8ok = a->K % g8::BK == 0 && a->K >= 4 * g8::BK;
-        const int g8mode = dev_env("QIE_GEMM8", 0);   // 1: full-chip grids only, 2: also split-K below
+        const int g8mode = dev_env("QIE_GEMM8", 2);   // 2 (default): + split-K below; 1: full-chip grids only; 0: off
         if (g8ok && g8mode != 0 && force != 2 && (force == 1 || (force < 0 && a->M >= big::BM && t256 >= cus))) {
             G8Split sk{1, nullptr, nullptr};
             return launch_gemm8(a->epilogue, p, (int)n_mt, (int)t256, sk, st);

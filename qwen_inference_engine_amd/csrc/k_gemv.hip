@@ -1120,7 +1120,21 @@ static int launch_gemv_t(const GemvParams& p, hipStream_t st, int blocks_per_cu)
     const int64_t n_blocks_needed = (p.n_tasks + 3) / 4;
     int64_t cap = (int64_t)device_cu_count() * blocks_per_cu;
     int64_t grid64 = std::max<int64_t>(1, std::min(n_blocks_needed, cap));
-    if (blocks_per_cu <= 0) {
+    if (blocks_per_cu == -2) {
+        // Full-residency grid-stride grid (the SwiGLU default): every CU holds the same number
+        // of blocks for the whole launch.  The balanced grid below gives every WAVE the same
+        // task count but leaves CUs with 3 and 4 blocks (948 blocks at 4 per CU for Qwen2-7B
+        // gate/up): in-graph gate/up 43.0 -> 42.2 us, 358.9 -> 361.5 tok/s (same box, A/B)
+        static size_t cached_shm2 = 0;
+        static int cached_nb2 = 0;
+        int nb = cached_shm2 == shm ? cached_nb2 : 0;
+        if (nb == 0) {
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 256, shm) != hipSuccess || nb < 1) nb = 2;
+            cached_shm2 = shm;
+            cached_nb2 = nb;
+        }
+        grid64 = std::max<int64_t>(1, std::min(n_blocks_needed, (int64_t)device_cu_count() * nb));
+    } else if (blocks_per_cu <= 0) {
         // Balanced persistent grid (default): the grid is what fits on the chip at once, and
         // the task count per wave is made (nearly) equal — e.g. gate/up (18,944 tasks) on
         // 768 resident blocks: 7 rounds over 677 blocks instead of 4.6 rounds over 1024
@@ -1432,19 +1446,19 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
         env_int("QIE_GEMV_XREG", vocab_rows ? 1 : 0) != 0) {
         xch = 3;
     }
-    // Normalised x in every wave's registers (XCH 4): no LDS image, no barrier (A/B knobs
-    // QIE_GEMV_XREG4 for the STORE projections (QKV, lm_head) and QIE_GEMV_XREG4_SW for gate/up)
+    // Normalised x in every wave's registers (XCH 4): no LDS image, no barrier.  Default for
+    // gate/up (5 row tasks per wave reuse it): 361.5 -> 362.7 tok/s at Qwen2-7B; the QKV
+    // projection (one task per wave) pays the per-wave divisions on its critical path:
+    // 9.98 -> 14.6 us (dev knobs QIE_GEMV_XREG4 / _LM / _SW)
     if (MT == 1 && p.M == 1 && p.norm_w && a->K % 8 == 0 && a->K <= 4096 &&
         env_int(a->epilogue == QIE_EPI_SWIGLU ? "QIE_GEMV_XREG4_SW" : (vocab_rows ? "QIE_GEMV_XREG4_LM" : "QIE_GEMV_XREG4"),
-                0) != 0) {
+                a->epilogue == QIE_EPI_SWIGLU ? 1 : 0) != 0) {
         xch = 4;
         p.xlds = 0;
     }
-    // gate/up grid override (A/B): blocks per CU for the SwiGLU launch only
-    if (a->epilogue == QIE_EPI_SWIGLU && MT == 1) {
-        const int sb = env_int("QIE_GEMV_SWIGLU_BPC", -1);
-        if (sb >= 0) bpc = sb;
-    }
+    // gate/up grid: full residency, grid-stride (-2, launch_gemv_t); QIE_GEMV_SWIGLU_BPC = N > 0
+    // caps N blocks per CU, -1 the balanced grid (dev A/B)
+    if (a->epilogue == QIE_EPI_SWIGLU && MT == 1 && bpc < 0) bpc = env_int("QIE_GEMV_SWIGLU_BPC", -2);
     // Batch-1 GEMVs without a fused norm on the one-block-per-CU grid (one row task per
     // wave: Qwen2-7B O, down) read x from L2 beside each weight chunk (XCH = 1) instead of
     // staging it in LDS behind a barrier: Qwen2-7B decode 355 -> 358 tok/s (two A/B rounds),

@@ -120,7 +120,7 @@ def test_tp_matches_single_gpu(name):
     assert flips <= 2
 
 
-@pytest.mark.parametrize("name", ["qwen2-bias-hd64", "tied-tp4", "q28kv4-tp8"])
+@pytest.mark.parametrize("name", ["qwen2-bias-hd64", "qwen3-qknorm-hd128", "g7-kvrep-tp2"])
 def test_peer_backend_equals_local(name):
     """The peer backend (one kernel per exchange: push into every rank's buffer, per-block
     generation flags, rank-ordered reduce with the residual add fused; decode steps CAPTURED
@@ -136,12 +136,12 @@ def test_peer_backend_equals_local(name):
 
 
 def test_peer_comm_collectives():
-    """qie_comm peer collectives on 3 in-process ranks: the fused all-reduce + residual add
+    """qie_comm peer collectives on 2 in-process ranks: the fused all-reduce + residual add
     equals the rank-ordered fp32 sum then bf16(x + bf16(sum)) bit for bit, across the
     2-MiB slot (chunked: several generations in one call), and so does the plain fp32
     all-reduce; each rank runs on its own stream (a shared stream would serialise them)."""
     lib = Q._lib.load()
-    world, n = 3, (2 << 20) // 4 + 4104        # one full slot + a remainder (multiple of 8)
+    world, n = 2, (2 << 20) // 4 + 4104        # one full slot + a remainder (multiple of 8)
     parts = [np.random.default_rng(10 + r).standard_normal(n).astype(np.float32) for r in range(world)]
     x0 = G.to_bf16(np.random.default_rng(5).standard_normal(n).astype(np.float32))
     want_sum = parts[0].copy()

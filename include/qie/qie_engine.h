@@ -190,11 +190,6 @@ int qie_engine_rope_tables(const qie_engine* e, const float** rope_cos, const fl
  * microseconds per launch and the algorithmic bytes per launch. */
 int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* avg_us,
                           double* bytes);
-/* In-graph kernel durations: n_steps greedy decode steps (they advance the batch like
- * qie_decode) replayed from a separate capture of the step with a hipEvent pair around
- * every launch role; avg_us[6] (roles as above) = the mean event-to-event time over layers
- * 1..L-1 (lm_head: the head) and the steps, -1 where nothing was timed. */
-int qie_batch_graph_kernel_times(qie_batch* b, int32_t n_steps, double* avg_us);
 
 #ifdef __cplusplus
 }

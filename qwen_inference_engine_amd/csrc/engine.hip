@@ -140,10 +140,6 @@ struct qie_batch {
     hipGraphExec_t gexec = nullptr;
     qie_sampling gs{};
     bool graph_ok = false;
-    // in-graph kernel probe (qie_batch_graph_kernel_times): while `probe` is set, the
-    // enqueue records an event pair around every launch role of layers 1..L-1 and the head
-    bool probe = false;
-    std::vector<hipEvent_t> pev;   // [(layer, role)][2], roles as qie_batch_time_kernel
 };
 
 namespace qie {
@@ -454,13 +450,6 @@ static bool rope_in_projection(const qie_batch* b) {
     return b->B == 1 && !s.qk_norm && s.numerics == QIE_NUMERICS_REF && dev_env("QIE_ROPE_IN_PROJ", 0) != 0;
 }
 
-// in-graph probe: event `edge` (0 before, 1 after) of launch role `role` of layer l (l = L: the head)
-static int probe_mark(qie_batch* b, int l, int role, int edge) {
-    if (!b->probe || l == 0) return 0;
-    QIE_HIP(hipEventRecord(b->pev[((size_t)l * 6 + role) * 2 + edge], b->e->stream));
-    return 0;
-}
-
 static int enqueue_layer_decode(qie_batch* b, int l) {
     qie_engine* e = b->e;
     const qie_model_spec& s = e->spec;
@@ -481,27 +470,21 @@ static int enqueue_layer_decode(qie_batch* b, int l) {
     a.norm_w = L.attn_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
     QIE_TRY(prenorm(b, a, B));
     const bool rope_in_proj = rope_in_projection(b);
-    QIE_TRY(probe_mark(b, l, 2, 0));
     if (rope_in_proj) QIE_TRY(gemv_rope(&a, b->d_pos, e->rope_cos, e->rope_sin, (int)hd, QD + KD, st));
     else QIE_TRY(gemv(&a, st));
-    QIE_TRY(probe_mark(b, l, 2, 1));
 
     set_decode_rope_cur(b->d_rope_cur);
-    QIE_TRY(probe_mark(b, l, 5, 0));
     const int arc = qie_attention_decode(b->qkv, B, b->d_pos, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, e->sh.nq,
                                          &cache, l, s.rms_eps, s.numerics | (rope_in_proj ? QIE_ATTN_PREROPED : 0),
                                          b->att, b->dec_ws, st);
     set_decode_rope_cur(nullptr);
     QIE_TRY(arc);
-    QIE_TRY(probe_mark(b, l, 5, 1));
     a = lin_base(e);
     a.x = b->att; a.ldx = QD;
     a.w[0] = L.wo; a.seg_rows[0] = H;
     a.M = B; a.K = QD; a.N = H;
     a.ldy = H;
-    QIE_TRY(probe_mark(b, l, 3, 0));
     QIE_TRY(row_parallel(b, a, b->x_res, b->part, B));
-    QIE_TRY(probe_mark(b, l, 3, 1));
 
     a = lin_base(e);
     a.x = b->x_res; a.ldx = H;
@@ -511,18 +494,15 @@ static int enqueue_layer_decode(qie_batch* b, int l) {
     a.epilogue = QIE_EPI_SWIGLU;
     a.norm_w = L.ffn_norm; a.norm_eps = s.rms_eps; a.numerics = s.numerics;
     QIE_TRY(prenorm(b, a, B));
-    QIE_TRY(probe_mark(b, l, 0, 0));
     QIE_TRY(gemv(&a, st));
-    QIE_TRY(probe_mark(b, l, 0, 1));
 
     a = lin_base(e);
     a.x = b->h; a.ldx = I;
     a.w[0] = L.w_down; a.seg_rows[0] = H;
     a.M = B; a.K = I; a.N = H;
     a.ldy = H;
-    QIE_TRY(probe_mark(b, l, 1, 0));
     QIE_TRY(row_parallel(b, a, b->x_res, b->part, B));
-    return probe_mark(b, l, 1, 1);
+    return 0;
 }
 
 static bool is_greedy(const qie_sampling* s) { return !s || s->top_k <= 1 || !(s->temperature > 0.f); }
@@ -569,9 +549,7 @@ static int enqueue_head(qie_batch* b, const uint16_t* x, int64_t ldx, int m0, in
         a.argmax_keys = (uint64_t*)(b->d_keys + m0);
         a.key_col0 = e->sh.vocab0;   // keys carry global vocab ids
     }
-    QIE_TRY(probe_mark(b, s.n_layers, 4, 0));
     QIE_TRY(gemv(&a, st));
-    QIE_TRY(probe_mark(b, s.n_layers, 4, 1));
     if (greedy && use_comm(e)) QIE_TRY(e->comm->allreduce_max_u64((uint64_t*)(b->d_keys + m0), M, st));
     if (!greedy) {
         const uint16_t* lg = b->logits + (int64_t)m0 * Vl;
@@ -1117,8 +1095,6 @@ void qie_batch_destroy(qie_batch* b) {
     if (!b) return;
     if (b->e && b->e->stream) hipStreamSynchronize(b->e->stream);
     if (b->gexec) hipGraphExecDestroy(b->gexec);
-    for (hipEvent_t ev : b->pev)
-        if (ev) hipEventDestroy(ev);
     void* ps[] = {b->kc, b->vc, b->d_table, b->d_pos, b->d_rope_cur, b->d_step, b->d_hist, b->d_ids, b->d_keys, b->x_res, b->qkv, b->q,
                   b->att, b->h, b->logits, b->attn_ws, b->dec_ws, b->samp_ws, b->pf_x, b->pf_hn, b->pf_qkv, b->pf_q,
                   b->pf_att, b->pf_h, b->pf_pos, b->pf_ids, b->pf_attn_ws, b->part, b->logits_full,
@@ -1510,62 +1486,6 @@ int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* av
     *avg_us = ms * 1000.0 / iters;
     *bytes = by;
     return 0;
-}
-
-int qie_batch_graph_kernel_times(qie_batch* b, int32_t n_steps, double* avg_us) {
-    QIE_REQUIRE(b && n_steps > 0 && avg_us, "qie_batch_graph_kernel_times: bad arguments");
-    qie_engine* e = b->e;
-    const int L = e->spec.n_layers;
-    QIE_REQUIRE(e->opts.use_graph && L >= 2, "qie_batch_graph_kernel_times: needs the graph path and >= 2 layers");
-    const size_t nev = (size_t)(L + 1) * 6 * 2;
-    if (b->pev.size() != nev) {
-        for (hipEvent_t ev : b->pev)
-            if (ev) hipEventDestroy(ev);
-        b->pev.assign(nev, nullptr);
-        for (auto& ev : b->pev) QIE_HIP(hipEventCreate(&ev));
-    }
-    QIE_TRY(prepare_steps(b, n_steps, "qie_batch_graph_kernel_times"));
-    // a separate capture of the greedy step with the event pairs in it (the cached graph is kept)
-    hipGraph_t g = nullptr;
-    hipGraphExec_t gx = nullptr;
-    QIE_HIP(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
-    b->probe = true;
-    const int rc = enqueue_decode(b, nullptr);
-    b->probe = false;
-    hipError_t he = hipStreamEndCapture(e->stream, &g);
-    if (rc) {
-        if (g) hipGraphDestroy(g);
-        return rc;
-    }
-    if (he != hipSuccess) return fail((int)he, "probe capture: %s", hipGetErrorString(he));
-    he = hipGraphInstantiate(&gx, g, nullptr, nullptr, 0);
-    hipGraphDestroy(g);
-    if (he != hipSuccess) return fail((int)he, "probe instantiate: %s", hipGetErrorString(he));
-    double sum[6] = {0, 0, 0, 0, 0, 0};
-    int cnt[6] = {0, 0, 0, 0, 0, 0};
-    int err = 0;
-    for (int i = 0; i < n_steps && !err; i++) {
-        he = hipGraphLaunch(gx, e->stream);
-        if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
-        if (he != hipSuccess) {
-            err = fail((int)he, "probe replay: %s", hipGetErrorString(he));
-            break;
-        }
-        for (int m = 0; m < b->B; m++) b->h_pos[m] += 1;
-        for (int l = 1; l <= L; l++)
-            for (int r = 0; r < 6; r++) {
-                if ((l == L) != (r == 4)) continue;   // the head row holds lm_head only
-                float ms = 0.f;
-                if (hipEventElapsedTime(&ms, b->pev[((size_t)l * 6 + r) * 2], b->pev[((size_t)l * 6 + r) * 2 + 1]) ==
-                    hipSuccess) {
-                    sum[r] += ms * 1e3;
-                    cnt[r] += 1;
-                }
-            }
-    }
-    hipGraphExecDestroy(gx);
-    for (int r = 0; r < 6; r++) avg_us[r] = cnt[r] ? sum[r] / cnt[r] : -1.0;
-    return err;
 }
 
 int qie_linear(const qie_linear_args* a, void* stream) {

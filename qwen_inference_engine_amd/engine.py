@@ -330,16 +330,6 @@ class Batch:
                    "qie_batch_time_kernel")
         return us.value, by.value
 
-    GRAPH_ROLES = ("gate_up", "down", "qkv", "o", "lm_head", "attn")
-
-    def graph_kernel_times(self, n_steps: int = 8) -> dict:
-        """In-graph durations (us) of the decode step's launch roles: n_steps greedy steps
-        (they advance the batch) replayed from a capture with hipEvent pairs around every
-        launch (qie_batch_graph_kernel_times), averaged over layers 1..L-1."""
-        out = (C.c_double * 6)()
-        _lib.check(self.lib.qie_batch_graph_kernel_times(self.h, n_steps, out), "qie_batch_graph_kernel_times")
-        return {r: round(out[i], 3) for i, r in enumerate(self.GRAPH_ROLES) if out[i] >= 0}
-
     def close(self) -> None:
         if getattr(self, "h", None):
             self.lib.qie_batch_destroy(self.h)

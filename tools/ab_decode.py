@@ -10,9 +10,8 @@ only reorders work must reproduce them bit for bit; one that changes numerics ma
       python tools/ab_decode.py
 
 Env: AB_MODEL (Qwen2-7B), AB_P (2048), AB_STEPS (256), AB_ROUNDS (3), AB_BATCH (1),
-AB_FP8 (0), AB_KERNELS (1: also the live per-kernel timings), AB_GRAPH (1: also the in-graph
-per-kernel durations, qie_batch_graph_kernel_times), AB_PREFILL (0: also time one prefill per
-variant)."""
+AB_FP8 (0), AB_KERNELS (1: also the live per-kernel timings), AB_PREFILL (0: also time one
+prefill per variant)."""
 import json
 import os
 import sys
@@ -71,11 +70,6 @@ def main():
                         ids_ref = ids
                     res[i]["ids_equal"] = bool(np.array_equal(ids, ids_ref))
                     res[i]["ids_diff_steps"] = int(np.sum(np.any(ids != ids_ref, axis=1)))
-                if os.environ.get("AB_GRAPH", "1") == "1":   # in-graph durations (event pairs in a probe capture)
-                    for s in range(B):
-                        b.set_position(s, P, first[s])
-                    for k, v in b.graph_kernel_times(8).items():
-                        res[i].setdefault("graph", {}).setdefault(k, []).append(v)
                 if kern:
                     for w, name in KNAMES.items():
                         us, _ = b.time_kernel(w, 54)
@@ -97,8 +91,6 @@ def main():
             out["prefill_ms_median"] = round(float(np.median(r["prefill_ms"])), 3)
         if r["kern"]:
             out["kern_us"] = {k: round(float(np.median(v)), 3) for k, v in r["kern"].items()}
-        if r.get("graph"):
-            out["graph_us"] = {k: round(float(np.median(v)), 3) for k, v in r["graph"].items()}
         print(json.dumps(out), flush=True)
 
 

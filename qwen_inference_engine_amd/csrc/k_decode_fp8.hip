@@ -315,6 +315,274 @@ __global__ __launch_bounds__(KS * 64) void dec8_kernel(Dec8Params p) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// dec8r (round 4): dec8 with the A fragments in LDS and a 4-deep register ring of weight
+// steps.  In dec8 the A fragments (16 rows x the wave's K slice, rows >= M padding) held 64
+// VGPRs per wave for the whole launch, leaving room for only two half-tile steps in flight
+// (~112 KB per CU at config 4's gate/up, 4.0 TB/s, where the bf16 GEMV keeps ~200 KB in
+// flight per CU and streams at 6.3 TB/s).  Here the normalised fragments go to LDS once
+// (only the AR = 8 or 16 real row slots; a lane's own slice, so no barrier), each unit reads
+// its two 16-B fragments back with ds_read_b128, and the freed registers hold FOUR
+// half-tile steps, three in flight while one is computed.  Steps past the block's last
+// tile load through a zero-sized buffer range (no memory traffic, no branch).  Numerics,
+// tiles, the epilogue and the fused norm are dec8's.
+template <int EPI, int KU, int KS, int AR>
+__global__ __launch_bounds__(KS * 64) void dec8r_kernel(Dec8Params p) {
+#pragma clang fp contract(off)
+    constexpr int NB = EPI == QIE_EPI_SWIGLU ? 2 : 1;
+    constexpr int kNT = 2;
+    __shared__ __attribute__((aligned(16))) float red[2][KS][NB][256];
+    __shared__ float ssq[KS][16];
+    __shared__ __attribute__((aligned(16))) d8_u32x4 nw_s[KS][KU * 8];
+    __shared__ __attribute__((aligned(16))) d8_u32x4 a_s[KS][KU][2][AR * 4];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int fr = lane & 15, g = lane >> 4;
+    const int M = p.M, K = p.K, T = p.n_tiles;
+    if ((int)blockIdx.x >= T) return;
+    const int my = (T - 1 - (int)blockIdx.x) / (int)gridDim.x + 1;
+    const int arow = fr < M ? fr : M - 1;
+    const int kw = wave * (KU * 64);
+    const int aidx = (fr & (AR - 1)) * 4 + g;   // this lane's A slot (rows >= M: any real row)
+
+    d8_u32x4 av[KU][2];
+    {
+        const d8_u32x4* xp = reinterpret_cast<const d8_u32x4*>(p.x + (int64_t)arow * p.ldx + kw + 16 * g);
+#pragma unroll
+        for (int u = 0; u < KU; u++) {
+            av[u][0] = xp[8 * u];
+            av[u][1] = xp[8 * u + 1];
+        }
+    }
+    const bool nrm = p.norm_w != nullptr && !QIE_DBG(p.dbg & 2);
+    const d8_u32x4 nwv = *reinterpret_cast<const d8_u32x4*>((nrm ? p.norm_w : p.x) + kw + 8 * (lane < KU * 8 ? lane : 0));
+
+    constexpr int KH = KU / 2;
+    struct Step {
+        d8_u32x4 wv[NB][KH];
+        float sc[NB];
+        float ep[4];
+    };
+    auto issue = [&](Step& t, int it, int hf) {
+        const bool live = it < my;                                   // past the last tile: no traffic
+        const int itc = live ? it : my - 1;
+        const int tile = (int)blockIdx.x + itc * (int)gridDim.x;
+        const int sg = NB == 2 ? 0 : (tile < p.t01[0] ? 0 : (tile < p.t01[1] ? 1 : 2));
+        const int tb0 = sg == 0 ? 0 : (sg == 1 ? p.t01[0] : p.t01[1]);
+        const int rows = p.seg_rows[sg];
+        int r = (tile - tb0) * 16 + fr;
+        r = r < rows ? r : rows - 1;
+        const int voff = r * K + kw + 16 * g + hf * (KH * 64);
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+            const uint8_t* base = p.w[NB == 2 ? b : sg];
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), (short)0,
+                                                              live ? (int)((int64_t)rows * (K + 4)) : 0, 0x00020000);
+#pragma unroll
+            for (int u = 0; u < KH; u++) t.wv[b][u] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, u * 64, kNT);
+            if (hf) t.sc[b] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, rows * K + r * 4, 0, 0));
+        }
+        if (!hf) return;
+        const int n = tile * 16 + fr;
+        const int nc = n < p.N ? n : p.N - 1;
+        if constexpr (EPI == QIE_EPI_RESIDUAL) {
+#pragma unroll
+            for (int rr = 0; rr < 4; rr++) {
+                const int i = 4 * g + rr < M ? 4 * g + rr : M - 1;
+                t.ep[rr] = bf2f(p.y[(int64_t)i * p.ldy + nc]);
+            }
+        } else if constexpr (EPI == QIE_EPI_STORE) {
+            const uint16_t* bp = p.bias[sg];
+            const float v = bf2f((bp ? bp : p.x)[bp ? r : 0]);
+            t.ep[0] = bp ? v : 0.f;
+        }
+    };
+
+    Step s0, s1, s2, s3;
+    issue(s0, 0, 0);
+    issue(s1, 0, 1);
+    __builtin_amdgcn_sched_barrier(0);
+
+    if (nrm) {
+        float ss = 0.f;
+#pragma unroll
+        for (int u = 0; u < KU; u++)
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const uint32_t e4[4] = {av[u][h].x, av[u][h].y, av[u][h].z, av[u][h].w};
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const float l = bf_lo(e4[j]), hh = bf_hi(e4[j]);
+                    ss += l * l + hh * hh;
+                }
+            }
+        ss = xor32_sum(xor16_sum(ss));
+        // opaque: the apply below re-unpacks the fragments instead of keeping the 128 unpacked
+        // floats of the sum of squares alive across the exchange (they spilled)
+#pragma unroll
+        for (int u = 0; u < KU; u++) asm volatile("" : "+v"(av[u][0]), "+v"(av[u][1]));
+        if (g == 0) ssq[wave][fr] = ss;
+        if (lane < KU * 8) nw_s[wave][lane] = nwv;
+        __syncthreads();
+        float tot = 0.f;
+#pragma unroll
+        for (int w = 0; w < KS; w++) tot += ssq[w][fr];
+        const float rms = sqrtf((tot / (float)K) + p.eps);
+        const float inv = 1.0f / rms;
+        const float rr = rms < INFINITY ? rms : 0.f;
+        auto apply = [&](auto hf) {
+            constexpr bool HF = decltype(hf)::value;
+#pragma unroll
+            for (int u = 0; u < KU; u++)
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const d8_u32x4 nv = nw_s[wave][8 * u + 2 * g + h];
+                    av[u][h].x = d8_rms_pair<HF>(av[u][h].x, nv.x, rr, inv);
+                    av[u][h].y = d8_rms_pair<HF>(av[u][h].y, nv.y, rr, inv);
+                    av[u][h].z = d8_rms_pair<HF>(av[u][h].z, nv.z, rr, inv);
+                    av[u][h].w = d8_rms_pair<HF>(av[u][h].w, nv.w, rr, inv);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+        };
+        __builtin_amdgcn_sched_barrier(0);
+        if (p.numerics == QIE_NUMERICS_HF) apply(std::true_type{});
+        else apply(std::false_type{});
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    // the fragments to LDS: each lane's own slot (row slots >= AR are never stored: rows >= M)
+    if (fr < AR) {
+#pragma unroll
+        for (int u = 0; u < KU; u++) {
+            a_s[wave][u][0][aidx] = av[u][0];
+            a_s[wave][u][1][aidx] = av[u][1];
+        }
+    }
+    // a wave reads back only its own slots: its LDS ops retire in order, no barrier
+    __builtin_amdgcn_sched_barrier(0);
+    issue(s2, 1, 0);   // after the prologue: its registers were the fragments'
+    __builtin_amdgcn_sched_barrier(0);
+
+    unsigned long long kbest[4] = {0ull, 0ull, 0ull, 0ull};
+    d8_f32x4 acc[NB];
+    auto mma = [&](const Step& t, int hf) {
+        if (hf == 0) {
+#pragma unroll
+            for (int b = 0; b < NB; b++) acc[b] = d8_f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int u = 0; u < KH; u++) {
+            const int ua = hf * KH + u;
+            const d8_bf16x8 a0 = __builtin_bit_cast(d8_bf16x8, a_s[wave][ua][0][aidx]);
+            const d8_bf16x8 a1 = __builtin_bit_cast(d8_bf16x8, a_s[wave][ua][1][aidx]);
+#pragma unroll
+            for (int b = 0; b < NB; b++) {
+                const uint2 c0 = fp8x4_to_bf16x4(t.wv[b][u].x), c1 = fp8x4_to_bf16x4(t.wv[b][u].y);
+                const uint2 c2 = fp8x4_to_bf16x4(t.wv[b][u].z), c3 = fp8x4_to_bf16x4(t.wv[b][u].w);
+                const d8_u32x4 lo = d8_u32x4{c0.x, c0.y, c1.x, c1.y};
+                const d8_u32x4 hi = d8_u32x4{c2.x, c2.y, c3.x, c3.y};
+                acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, __builtin_bit_cast(d8_bf16x8, lo), acc[b], 0, 0, 0);
+                acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, __builtin_bit_cast(d8_bf16x8, hi), acc[b], 0, 0, 0);
+            }
+            // one unit at a time: hoisting every unit's reads and conversions would spill
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    auto finish = [&](const Step& t, int it) {
+        const int buf = it & 1;
+#pragma unroll
+        for (int b = 0; b < NB; b++)
+            *reinterpret_cast<float4*>(&red[buf][wave][b][lane * 4]) = make_float4(acc[b][0], acc[b][1], acc[b][2], acc[b][3]);
+        __syncthreads();
+        if (wave != it % KS) return;
+        const int tile = (int)blockIdx.x + it * (int)gridDim.x;
+        const int n = tile * 16 + fr;
+        float c[NB][4];
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+            float4 s = *reinterpret_cast<const float4*>(&red[buf][0][b][lane * 4]);
+#pragma unroll
+            for (int w = 1; w < KS; w++) {
+                const float4 v = *reinterpret_cast<const float4*>(&red[buf][w][b][lane * 4]);
+                s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+            }
+            c[b][0] = s.x * t.sc[b];
+            c[b][1] = s.y * t.sc[b];
+            c[b][2] = s.z * t.sc[b];
+            c[b][3] = s.w * t.sc[b];
+        }
+        if (n >= p.N) return;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int i = 4 * g + r;
+            if (i >= M) continue;
+            uint16_t* yr = p.y + (int64_t)i * p.ldy;
+            if constexpr (EPI == QIE_EPI_SWIGLU) {
+                const float gg = rbf(c[0][r]);
+                const float uu = rbf(c[1][r]);
+                const float a = rbf(gg * (1.0f / (1.0f + expf(-gg))));
+                yr[n] = f2bf(uu * a);
+            } else if constexpr (EPI == QIE_EPI_RESIDUAL) {
+                yr[n] = f2bf(t.ep[r] + rbf(c[0][r]));
+            } else if constexpr (EPI == QIE_EPI_F32) {
+                reinterpret_cast<float*>(p.y)[(int64_t)i * p.ldy + n] = c[0][r];
+            } else {
+                const uint16_t o = f2bf(c[0][r] + t.ep[0]);
+                yr[n] = o;
+                if (p.keys) {
+                    const unsigned long long kk = sel_key(bf2f(o), (uint32_t)(n + p.key_col0));
+                    kbest[r] = kk > kbest[r] ? kk : kbest[r];
+                }
+            }
+        }
+    };
+
+    // ring of four half-tile steps: step 2 it + hf of tile it sits in s[(2 it + hf) & 3];
+    // every step issues the one three steps ahead before computing
+    __builtin_amdgcn_sched_barrier(0);
+    for (int it = 0; it < my; it += 2) {
+        issue(s3, it + 1, 1);
+        mma(s0, 0);
+        issue(s0, it + 2, 0);
+        mma(s1, 1);
+        finish(s1, it);
+        if (it + 1 >= my) break;   // block-uniform
+        issue(s1, it + 2, 1);
+        mma(s2, 0);
+        issue(s2, it + 3, 0);
+        mma(s3, 1);
+        finish(s3, it + 1);
+    }
+    if constexpr (EPI == QIE_EPI_STORE) {
+        if (p.keys) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                unsigned long long v = kbest[r];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    const unsigned long long s = __shfl_xor(v, o, 64);
+                    v = s > v ? s : v;
+                }
+                if (fr == 0 && 4 * g + r < M && v) atomicMax(p.keys + 4 * g + r, v);
+            }
+        }
+    }
+}
+
+template <int EPI, int KU, int KS, int AR>
+static int dec8r_launch(const Dec8Params& p, hipStream_t st) {
+    const void* fn = (const void*)dec8r_kernel<EPI, KU, KS, AR>;
+    static int per_cu = 0;
+    if (per_cu == 0) {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, KS * 64, 0) != hipSuccess || nb < 1) nb = 1;
+        per_cu = nb;
+    }
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(p.n_tiles, (int64_t)device_cu_count() * per_cu));
+    hipLaunchKernelGGL((dec8r_kernel<EPI, KU, KS, AR>), dim3(grid), dim3(KS * 64), 0, st, p);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+
 template <int EPI, int KU, int KS>
 static int dec8_launch(const Dec8Params& p, hipStream_t st) {
     const void* fn = (const void*)dec8_kernel<EPI, KU, KS>;
@@ -332,6 +600,16 @@ static int dec8_launch(const Dec8Params& p, hipStream_t st) {
 
 template <int KU, int KS>
 static int dec8_epi(const Dec8Params& p, int epi, hipStream_t st) {
+    if constexpr (KU == 8 && KS == 7) {   // the ring form (config 4's K = 3,584), M <= 8 (dev A/B QIE_DEC8R)
+        if (p.M <= 8 && dev_env("QIE_DEC8R", 0) != 0) {
+            switch (epi) {
+                case QIE_EPI_SWIGLU: return dec8r_launch<QIE_EPI_SWIGLU, KU, KS, 8>(p, st);
+                case QIE_EPI_RESIDUAL: return dec8r_launch<QIE_EPI_RESIDUAL, KU, KS, 8>(p, st);
+                case QIE_EPI_F32: return dec8r_launch<QIE_EPI_F32, KU, KS, 8>(p, st);
+                default: return dec8r_launch<QIE_EPI_STORE, KU, KS, 8>(p, st);
+            }
+        }
+    }
     switch (epi) {
         case QIE_EPI_SWIGLU: return dec8_launch<QIE_EPI_SWIGLU, KU, KS>(p, st);
         case QIE_EPI_RESIDUAL: return dec8_launch<QIE_EPI_RESIDUAL, KU, KS>(p, st);

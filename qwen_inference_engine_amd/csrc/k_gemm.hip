@@ -856,7 +856,9 @@ int gemm(const qie_linear_args* a, hipStream_t st) {
         if (g8ok && g8mode == 2 && force < 0 && a->M >= big::BM && t256 < cus) {
             const int s = g8_splitk(t256, cus, (int)(a->K / g8::BK));
             G8Split sk{1, nullptr, nullptr};
-            if (s == 1 || g8_workspace(st, (int)t256, s, &sk) == 0)
+            // unsplit, 256x256 tiles must still cover half the chip: QKV at 144 tiles 101.7 ->
+            // 87.8 us, but O at 112 tiles 78 -> 103 us (its 256x128 kernel fills 224 CUs)
+            if ((s == 1 && 2 * t256 >= cus) || (s > 1 && g8_workspace(st, (int)t256, s, &sk) == 0))
                 return launch_gemm8(a->epilogue, p, (int)n_mt, (int)t256, sk, st);
         }
         if (force == 1 || (force < 0 && a->M >= big::BM && t256 >= cus))

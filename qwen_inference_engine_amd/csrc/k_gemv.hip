@@ -199,7 +199,11 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
     // Unconditional buffer loads (a missing bias reads element 0 of x; the epilogue ignores it).
     constexpr bool EPRE = MT == 1 && (EPI == QIE_EPI_RESIDUAL || EPI == QIE_EPI_STORE);
     uint32_t epre_v[EPRE ? RPW : 1];
-    const bool epre_on = EPRE && XCH > 0 && p.epre != 0 && p.M == 1;   // uniform; the XCH > 0 prologues issue them
+    // the loads are issued WITHOUT a branch: a load under a (even uniform) condition makes the
+    // waitcnt pass fall back to vmcnt(0) at every later wait, and the weight stream stops
+    // pipelining (the first, branched form measured QKV 10.0 -> 10.7, O 6.4 -> 6.9 us)
+    constexpr bool EPRE_ON = EPRE && XCH > 0;
+    const bool epre_on = EPRE_ON && p.M == 1 && p.epre != 0;   // uniform; p.epre = 0 (dev A/B): reload
     auto epre_issue = [&](int64_t task) {
         if constexpr (EPRE) {
 #pragma unroll
@@ -288,7 +292,7 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
     constexpr bool PF = XCH > 0;
 
     if constexpr (XCH == 1) {
-        if (epre_on) epre_issue(task0 < p.n_tasks ? task0 : p.n_tasks - 1);
+        if constexpr (EPRE_ON) epre_issue(task0 < p.n_tasks ? task0 : p.n_tasks - 1);
         task_ptrs(task0 < p.n_tasks ? task0 : p.n_tasks - 1, wr);
         load_chunk(wr, (int64_t)lane * EL, wv);
     } else if constexpr (XCH == 3) {
@@ -310,7 +314,7 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
             nvw[c] = __builtin_amdgcn_raw_buffer_load_b128(rn, lane * 16, (u < U ? u : 0) * 1024, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (epre_on) epre_issue(task0 < p.n_tasks ? task0 : p.n_tasks - 1);
+        if constexpr (EPRE_ON) epre_issue(task0 < p.n_tasks ? task0 : p.n_tasks - 1);
         task_ptrs(task0 < p.n_tasks ? task0 : p.n_tasks - 1, wr);
         load_chunk(wr, (int64_t)lane * EL, wv);
         __builtin_amdgcn_sched_barrier(0);
@@ -369,7 +373,7 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
             na[u] = __builtin_amdgcn_raw_buffer_load_b128(rn, lane * 16, u * 1024, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (epre_on) epre_issue(task0 < p.n_tasks ? task0 : p.n_tasks - 1);
+        if constexpr (EPRE_ON) epre_issue(task0 < p.n_tasks ? task0 : p.n_tasks - 1);
         task_ptrs(task0 < p.n_tasks ? task0 : p.n_tasks - 1, wr);
         load_chunk(wr, (int64_t)lane * EL, wv);
         __builtin_amdgcn_sched_barrier(0);
@@ -430,7 +434,7 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
         __builtin_amdgcn_sched_barrier(0);
         // unconditional (a wave without a task re-reads the last row): a load under a
         // branch makes the vmcnt bookkeeping at the join wait for everything
-        if (epre_on) epre_issue(task0 < p.n_tasks ? task0 : p.n_tasks - 1);
+        if constexpr (EPRE_ON) epre_issue(task0 < p.n_tasks ? task0 : p.n_tasks - 1);
         task_ptrs(task0 < p.n_tasks ? task0 : p.n_tasks - 1, wr);
         load_chunk(wr, (int64_t)lane * EL, wv);
         __builtin_amdgcn_sched_barrier(0);
@@ -1366,7 +1370,7 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
     p.rope_sn = g_rope.sn;
     p.rope_hd = g_rope.hd;
     p.rope_rows = g_rope.rows;
-    p.epre = env_int("QIE_GEMV_EPRE", 0);
+    p.epre = env_int("QIE_GEMV_EPRE", 1);
     p.mkdiv = env_int("QIE_GEMV_MKDIV", 0);
     if (a->M >= 2 && a->M <= 16 && env_int("QIE_SKINNY_MFMA", 1) != 0) {
         const bool fp8w = (a->flags & QIE_LINEAR_FP8) != 0;

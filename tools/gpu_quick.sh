@@ -9,6 +9,7 @@
 #   AB_GEMM_VARIANTS='[{}, {"QIE_GEMM8": "1"}]'  tools/ab_gemm.py (prefill GEMMs, bit-equality + time)
 #   UB_SET     tools/ubench.py kernel variants (development library)
 #   PROFILE=1  rocprofv3 kernel trace of a short bench (PROF_ARGS appended)
+#   PMC=1      tools/pmc_traffic.sh (FETCH_SIZE / WRITE_SIZE per decode launch; PMC_CONFIG=fp8b8)
 set -u
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd "$R"; mkdir -p gpurun_out
@@ -42,8 +43,12 @@ fi
 if [ "${PROFILE:-0}" = "1" ]; then
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run \
-      -- python3 "$R/bench.py" --steps 64 --warmup 4 --prefill-iters 1 --no-cpu-baseline ${PROF_ARGS:-} \
+      -- python3 "$R/bench.py" --steps 64 --warmup 4 --prefill-iters 1 --no-cpu-baseline --no-configs ${PROF_ARGS:-} \
       > "$R/gpurun_out/prof.log" 2>&1
   rc=$?; echo "rocprof rc=$rc"; cd "$R"; [ $rc -eq 0 ] || exit $rc
+fi
+if [ "${PMC:-0}" = "1" ]; then   # HBM traffic per launch (FETCH_SIZE, WRITE_SIZE passes)
+  PMC_CONFIG=${PMC_CONFIG:-} bash tools/pmc_traffic.sh
+  rc=$?; [ $rc -eq 0 ] || exit $rc
 fi
 exit 0

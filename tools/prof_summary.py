@@ -28,7 +28,14 @@ ROLE = {
     "gemm_big_kernel<2, 256>": "prefill gate/up GEMM (256x256 LDS-DMA, SwiGLU)",
     "gemm_big_kernel<1, 128>": "prefill O / down GEMM (256x128 LDS-DMA, +residual)",
     "gemm_big_kernel<0, 256>": "prefill QKV GEMM (256x256 LDS-DMA, one round, +bias)",
-    "finalize_kernel": "token -> history, position++, next embedding row",
+    "finalize_kernel": "token -> history, position++, next embedding row, RoPE row of the new position",
+    # round 4
+    "gemv_kernel<1, 2, 2, 7, 4, 0, 256> [g 512 x 256]": "decode gate/up GEMV (+RMSNorm in registers, SwiGLU), full-residency grid  [dominant]",
+    "gemm8_kernel<2>": "prefill gate/up GEMM (phase-interleaved 256x256, SwiGLU)",
+    "gemm8_kernel<1>": "prefill down GEMM (phase-interleaved 256x256, split-K 2, +residual)",
+    "dec8r_kernel<2, 8, 7, 8>": "fp8 decode gate/up, A in LDS + 4-step ring  [dominant]",
+    "dec8r_kernel<0, 8, 7, 8>": "fp8 decode QKV, A in LDS + 4-step ring",
+    "dec8r_kernel<1, 8, 7, 8>": "fp8 decode O-proj, A in LDS + 4-step ring",
     "gemv_kernel<1, 2, 0, 8, 1, 0, 576> [g 256 x 448]": "bench live timing of down (store epilogue)",
     "gemv_kernel<1, 2, 0, 7, 1, 0, 576> [g 256 x 448]": "bench live timing of O-proj (store epilogue)",
     "synth_kernel": "synthetic weight fill (setup)",
@@ -107,8 +114,8 @@ def in_graph_decode(trace):
 
 
 HEADLINE = ("`rocprofv3 --kernel-trace --stats --output-format csv -- python3 bench.py --steps 64 --warmup 4 "
-            "--prefill-iters 1 --no-cpu-baseline` (Qwen2-7B bf16, batch 1, prompt 2048; prefill x2 + 4 warm-up + "
-            "64 timed hipGraph decode steps + bench's live kernel timings).")
+            "--prefill-iters 1 --no-cpu-baseline --no-configs` (Qwen2-7B bf16, batch 1, prompt 2048; prefill x2 + 4 "
+            "warm-up + 64 timed hipGraph decode steps + bench's live kernel timings).")
 
 
 def main(tag="r01", src="gpurun_out/prof", desc=HEADLINE, how="tools/gpu_check.sh PROFILE=1"):

@@ -190,6 +190,11 @@ int qie_engine_rope_tables(const qie_engine* e, const float** rope_cos, const fl
  * microseconds per launch and the algorithmic bytes per launch. */
 int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* avg_us,
                           double* bytes);
+/* One decode step run eagerly (as qie_decode_step) that also copies the residual stream
+ * into host_x: bf16 [2 n_layers + 1][batch][hidden], slot 0 = the step's input row, slot
+ * 2l + 1 = after layer l's attention block (O-proj + residual), 2l + 2 = after its MLP
+ * block (down-proj + residual).  Parity diagnostics (tools/flip_attrib.py). */
+int qie_batch_debug_step(qie_batch* b, const qie_sampling* smp, int32_t* next_ids, void* host_x);
 
 #ifdef __cplusplus
 }

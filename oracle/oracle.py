@@ -51,6 +51,7 @@ def lib():
             "or_sample_ref": (C.c_int, [P, I64, C.c_int, F, F, C.c_uint64]),
             "or_curand_uniform_first": (F, [C.c_uint64]),
             "or_set_sum_order": (None, [C.c_int]),
+            "or_set_layer_dump": (None, [P]),
             "or_forward": (C.c_int, [C.POINTER(qlib.ModelSpecC), C.POINTER(qlib.ModelWeightsC), P, P,
                                      C.c_int, P, C.c_int, C.c_int, P, P, C.c_int]),
         }
@@ -200,6 +201,17 @@ class Model:
         self.pos = sp + ids.size
         self.last_hidden = hidden
         return logits
+
+    def forward_dump(self, ids, start_pos=None):
+        """forward() that also returns the last token's residual rows bf16 [2L + 1][H] (slot 0
+        after the embedding, 2l + 1 / 2l + 2 after layer l's attention / MLP residual adds)."""
+        buf = np.zeros((2 * self.spec.n_layers + 1, self.spec.hidden), np.uint16)
+        lib().or_set_layer_dump(_p(buf))
+        try:
+            lg = self.forward(ids, start_pos)
+        finally:
+            lib().or_set_layer_dump(None)
+        return lg, buf
 
     def generate_greedy(self, prompt, n_new):
         """Prefill + (n_new - 1) decode steps; returns (ids, per-step logits)."""

@@ -589,6 +589,12 @@ int or_sample_ref(const bf16_t* logits, int64_t V, int k, float temperature, flo
  * bf16 logits of the LAST token.  Optional final_hidden receives the normed
  * hidden row fed to lm_head.
  */
+/* Parity diagnostics (tools/flip_attrib.py): when set, or_forward copies the LAST token's
+ * residual row into dump[slot][H] — slot 0 after the embedding, 2l + 1 after layer l's
+ * attention residual, 2l + 2 after its MLP residual (the engine's qie_batch_debug_step). */
+static bf16_t* g_layer_dump = nullptr;
+void or_set_layer_dump(bf16_t* dump) { g_layer_dump = dump; }
+
 int or_forward(const qie_model_spec* s, const qie_model_weights* w, bf16_t* kcache,
                bf16_t* vcache, int max_ctx, const int32_t* ids, int n, int start_pos,
                bf16_t* logits_out, bf16_t* final_hidden, int nthreads) {
@@ -610,6 +616,10 @@ int or_forward(const qie_model_spec* s, const qie_model_weights* w, bf16_t* kcac
         v((size_t)n * KD), att((size_t)n * QD), tmp((size_t)n * H), up((size_t)n * I),
         gate((size_t)n * I), hm((size_t)n * I);
     or_embedding((const bf16_t*)w->embed, ids, x.data(), n, H);
+    auto dump = [&](int64_t slot) {
+        if (g_layer_dump) std::memcpy(g_layer_dump + slot * H, x.data() + (int64_t)(n - 1) * H, H * 2);
+    };
+    dump(0);
     const int64_t head_stride = (int64_t)max_ctx * hd;
     for (int64_t l = 0; l < L; l++) {
         const qie_layer_weights& lw = w->layers[l];
@@ -636,12 +646,14 @@ int or_forward(const qie_model_spec* s, const qie_model_weights* w, bf16_t* kcac
                      /*causal=*/1, start_pos, head_stride, nthreads);
         or_matmul(att.data(), (const bf16_t*)lw.wo, nullptr, tmp.data(), n, QD, H, nthreads);
         or_resadd(x.data(), tmp.data(), (int64_t)n * H);
+        dump(2 * l + 1);
         or_rmsnorm(x.data(), (const bf16_t*)lw.ffn_norm, hn.data(), n, H, s->rms_eps, num);
         or_matmul(hn.data(), (const bf16_t*)lw.w_up, nullptr, up.data(), n, H, I, nthreads);
         or_matmul(hn.data(), (const bf16_t*)lw.w_gate, nullptr, gate.data(), n, H, I, nthreads);
         or_silu_mul(gate.data(), up.data(), hm.data(), (int64_t)n * I);
         or_matmul(hm.data(), (const bf16_t*)lw.w_down, nullptr, tmp.data(), n, I, H, nthreads);
         or_resadd(x.data(), tmp.data(), (int64_t)n * H);
+        dump(2 * l + 2);
     }
     /* final norm of the last token only (qwen_main.cu:226-236 norms every row
      * then copies row P-1; identical values for the last row). */

@@ -183,6 +183,7 @@ SIGNATURES = [
     ("qie_engine_arena", C.c_int, [_P, C.POINTER(_P), _PI64]),
     ("qie_engine_rope_tables", C.c_int, [_P, C.POINTER(_P), C.POINTER(_P), _PI32]),
     ("qie_batch_time_kernel", C.c_int, [_P, _I32, _I32, _PD, _PD]),
+    ("qie_batch_debug_step", C.c_int, [_P, _P, _PI32, _P]),
 ]
 
 _lib = None

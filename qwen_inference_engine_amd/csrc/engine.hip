@@ -140,6 +140,9 @@ struct qie_batch {
     hipGraphExec_t gexec = nullptr;
     qie_sampling gs{};
     bool graph_ok = false;
+    // qie_batch_debug_step: while set, the decode enqueue copies the residual stream after every
+    // attention block and every MLP block into dbg_x ([2L + 1][B][H] bf16; slot 0 = the input)
+    uint16_t* dbg_x = nullptr;
 };
 
 namespace qie {
@@ -450,6 +453,14 @@ static bool rope_in_projection(const qie_batch* b) {
     return b->B == 1 && !s.qk_norm && s.numerics == QIE_NUMERICS_REF && dev_env("QIE_ROPE_IN_PROJ", 0) != 0;
 }
 
+// qie_batch_debug_step: residual stream snapshot `slot` (eager step only, never captured)
+static int dbg_snap(qie_batch* b, int slot) {
+    if (!b->dbg_x) return 0;
+    const int64_t n = (int64_t)b->B * b->e->spec.hidden;
+    QIE_HIP(hipMemcpyAsync(b->dbg_x + slot * n, b->x_res, (size_t)n * 2, hipMemcpyDeviceToDevice, b->e->stream));
+    return 0;
+}
+
 static int enqueue_layer_decode(qie_batch* b, int l) {
     qie_engine* e = b->e;
     const qie_model_spec& s = e->spec;
@@ -485,6 +496,7 @@ static int enqueue_layer_decode(qie_batch* b, int l) {
     a.M = B; a.K = QD; a.N = H;
     a.ldy = H;
     QIE_TRY(row_parallel(b, a, b->x_res, b->part, B));
+    QIE_TRY(dbg_snap(b, 2 * l + 1));
 
     a = lin_base(e);
     a.x = b->x_res; a.ldx = H;
@@ -502,7 +514,7 @@ static int enqueue_layer_decode(qie_batch* b, int l) {
     a.M = B; a.K = I; a.N = H;
     a.ldy = H;
     QIE_TRY(row_parallel(b, a, b->x_res, b->part, B));
-    return 0;
+    return dbg_snap(b, 2 * l + 2);
 }
 
 static bool is_greedy(const qie_sampling* s) { return !s || s->top_k <= 1 || !(s->temperature > 0.f); }
@@ -1486,6 +1498,24 @@ int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* av
     *avg_us = ms * 1000.0 / iters;
     *bytes = by;
     return 0;
+}
+
+int qie_batch_debug_step(qie_batch* b, const qie_sampling* smp, int32_t* next_ids, void* host_x) {
+    QIE_REQUIRE(b && host_x, "qie_batch_debug_step: bad arguments");
+    qie_engine* e = b->e;
+    const int64_t n = (int64_t)b->B * e->spec.hidden, slots = 2 * (int64_t)e->spec.n_layers + 1;
+    QIE_TRY(prepare_steps(b, 1, "qie_batch_debug_step"));
+    QIE_TRY(dmalloc((void**)&b->dbg_x, (size_t)(slots * n * 2)));
+    int rc = dbg_snap(b, 0);
+    if (!rc) rc = enqueue_decode(b, smp);   // eager: the graph (if any) is left as it is
+    hipError_t he = hipStreamSynchronize(e->stream);
+    if (!rc && he == hipSuccess) he = hipMemcpy(host_x, b->dbg_x, (size_t)(slots * n * 2), hipMemcpyDeviceToHost);
+    hipFree(b->dbg_x);
+    b->dbg_x = nullptr;
+    QIE_TRY(rc);
+    QIE_HIP(he);
+    for (int m = 0; m < b->B; m++) b->h_pos[m] += 1;
+    return sync_ids(b, next_ids);
 }
 
 int qie_linear(const qie_linear_args* a, void* stream) {

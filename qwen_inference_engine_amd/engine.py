@@ -324,6 +324,16 @@ class Batch:
                     out[which][g, t0:t1] = buf
         return out
 
+    def debug_step(self, sampling: Sampling = GREEDY):
+        """One eager decode step; returns (ids, residual snapshots bf16 [2L + 1][B][H]):
+        slot 0 the input row, 2l + 1 after layer l's attention block, 2l + 2 after its MLP."""
+        L, H = self.e.spec.n_layers, self.e.spec.hidden
+        xs = np.zeros((2 * L + 1, self.B, H), np.uint16)
+        out = (C.c_int32 * self.B)()
+        sc = sampling.to_c()
+        _lib.check(self.lib.qie_batch_debug_step(self.h, C.byref(sc), out, xs.ctypes.data), "qie_batch_debug_step")
+        return list(out), xs
+
     def time_kernel(self, which: int = 0, iters: int = 20):
         us, by = C.c_double(), C.c_double()
         _lib.check(self.lib.qie_batch_time_kernel(self.h, which, iters, C.byref(us), C.byref(by)),

@@ -136,7 +136,11 @@ static int g_sum_order = 0;
  *       split / tiled kernel computes: exp2((s - m) log2 e) (the -use_fast_math
  *       __expf of the reference build, flags.make:10), softmax denominator and P.V
  *       accumulated per 128-key block, P.V divided by the denominator AFTER the sum;
- *       SiLU's exponent in the same fast-math form.
+ *       SiLU's exponent in the same fast-math form;
+ *   3 = order 0 except the attention softmax in 2's online form;
+ *   4 = order 0 except SiLU's exponent in 2's fast-math form;
+ *   5 = order 0 except the RMSNorm sum of squares in 2's order;
+ *   6 = order 0 except the attention q.k dot products in 2's order (3..6: tools/flip_attrib.py).
  * The logit spread between variant 0 and 1 / 2 at a given depth is the reference
  * algorithm's own order sensitivity, which sizes the end-to-end parity tolerance
  * (bench.py cpu_baseline, tests/test_gpu_headline.py, DESIGN.md "Parity"). */
@@ -154,7 +158,7 @@ void or_rmsnorm(const bf16_t* x, const bf16_t* w, bf16_t* y, int64_t rows, int64
         const bf16_t* xr = x + r * H;
         bf16_t* yr = y + r * H;
         float sum = 0.f;
-        if (g_sum_order == 2) {
+        if (g_sum_order == 2 || g_sum_order == 5) {
             float part[256];
             for (int j = 0; j < 256; j++) part[j] = 0.f;
             for (int64_t i = 0; i < H; i++) {
@@ -342,7 +346,7 @@ void or_silu_mul(const bf16_t* gate, const bf16_t* up, bf16_t* h, int64_t n) {
         float g = bf2f(gate[i]);
         // order 2: the reference build's -use_fast_math exponent (flags.make:10), which a
         // GPU libm need not match to the last ulp either
-        const float ex = g_sum_order == 2 ? exp2f(-g * 1.44269504088896341f) : expf(-g);
+        const float ex = g_sum_order == 2 || g_sum_order == 4 ? exp2f(-g * 1.44269504088896341f) : expf(-g);
         float a = rbf(g * (1.0f / (1.0f + ex)));
         h[i] = f2bf(bf2f(up[i]) * a);
     }
@@ -387,7 +391,7 @@ void or_attention(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, bf16_t* o
                 for (int t = 0; t < mkv; t++) {
                     const bf16_t* kr = kh + (int64_t)t * hd;
                     for (int d = 0; d < hd; d++) buf[d] = bf2f(qr[d]) * bf2f(kr[d]);
-                    if (g_sum_order == 2) {
+                    if (g_sum_order == 2 || g_sum_order == 6) {
                         float part[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
                         for (int d = 0; d < hd; d++) part[d & 7] += buf[d];
                         for (int w = 4; w > 0; w >>= 1)
@@ -406,7 +410,7 @@ void or_attention(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, bf16_t* o
                 float mx = -1e9f;
                 for (int t = 0; t < mkv; t++) mx = fmaxf(mx, score[t]);
                 float sum = 0.f;
-                if (g_sum_order == 2) {
+                if (g_sum_order == 2 || g_sum_order == 3) {
                     // the online-softmax (flash) formulation every split / tiled kernel uses:
                     // exponent as exp2((s - m) * log2 e) (the reference build's -use_fast_math
                     // __expf), per-128-key block sums, and P.V normalised AFTER the

@@ -30,6 +30,7 @@ int gemv_rope(const qie_linear_args* a, const int32_t* pos, const float* cs, con
               hipStream_t st);
 int gemm(const qie_linear_args* a, hipStream_t st);
 bool dec8_applies(const qie_linear_args* a);
+int dec8_reserve(hipStream_t st);
 }  // namespace qie
 
 
@@ -1050,6 +1051,8 @@ static int batch_create(qie_engine* e, int32_t batch, int32_t max_ctx, int32_t p
     }
     b->h_pos.assign(batch, 0);
     if (!rc) rc = flush_table(b);
+    // the fp8 batched-decode split-K workspace of this stream, before any graph capture
+    if (!rc && e->fp8 && batch >= 2) rc = dec8_reserve(e->stream);
     if (rc) {
         qie_batch_destroy(b);
         return rc;

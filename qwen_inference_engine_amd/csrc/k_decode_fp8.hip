@@ -30,6 +30,8 @@
 #include "../../include/qie/qie_ops.h"
 
 #include <algorithm>
+#include <map>
+#include <mutex>
 #include <type_traits>
 
 namespace qie {
@@ -55,6 +57,13 @@ struct Dec8Params {
     unsigned long long* keys;  // arg-max keys per row (STORE), may be null
     int64_t key_col0;
     int dbg;                   // development build only (QIE_DEC8_DBG): 2 skips the fused norm
+    // split-K (SPL instantiations only; long K such as the down projection's 18,944): the K
+    // units are cut into `parts` slices of KS * KU units (the last one ragged), block b serves
+    // part b % parts; each part's reduced 16 x 16 fp32 tile goes write-through to slab
+    // [tile][part] and the last arriving part (ticket cnt[tile]) sums them in part order
+    int parts;
+    float* slab;
+    unsigned* cnt;
 };
 
 // One bf16 pair of qie_rmsnorm's rms_apply8 (k_misc.hip, normalization.cu:18-23).
@@ -78,9 +87,10 @@ __device__ __forceinline__ uint32_t d8_rms_pair(uint32_t xv, uint32_t wv, float 
     return pack2(y[0], y[1]);
 }
 
-template <int EPI, int KU, int KS>
+template <int EPI, int KU, int KS, bool SPL = false>
 __global__ __launch_bounds__(KS * 64) void dec8_kernel(Dec8Params p) {
 #pragma clang fp contract(off)
+    static_assert(!SPL || EPI != QIE_EPI_SWIGLU, "split-K: single-segment epilogues");
     constexpr int NB = EPI == QIE_EPI_SWIGLU ? 2 : 1;   // B tiles per column tile (gate, up)
     constexpr int kNT = 2;                               // buffer-load policy: nt (streamed once)
     __shared__ __attribute__((aligned(16))) float red[2][KS][NB][256];
@@ -89,19 +99,35 @@ __global__ __launch_bounds__(KS * 64) void dec8_kernel(Dec8Params p) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int fr = lane & 15, g = lane >> 4;
     const int M = p.M, K = p.K, T = p.n_tiles;
-    if ((int)blockIdx.x >= T) return;   // block-uniform, before any barrier
-    const int my = (T - 1 - (int)blockIdx.x) / (int)gridDim.x + 1;
+    // block -> (first tile bi, tile stride G, K part); without split: part 0, G = grid
+    const int part = SPL ? (int)blockIdx.x % p.parts : 0;
+    const int bi = SPL ? (int)blockIdx.x / p.parts : (int)blockIdx.x;
+    const int G = SPL ? (int)gridDim.x / p.parts : (int)gridDim.x;
+    if (bi >= T || bi >= G) return;   // block-uniform, before any barrier
+    const int my = (T - 1 - bi) / G + 1;
     const int arow = fr < M ? fr : M - 1;
-    const int kw = wave * (KU * 64);
+    const int kw = (part * KS + wave) * (KU * 64);
+    // units of this wave past K (the ragged last part): A fragments 0, weight loads out of
+    // the buffer range (0) — wave-uniform, and no load sits under a branch
+    const int kval = SPL ? (K - kw) / 64 : KU;   // valid units (may be <= 0 or > KU)
 
     // ---- A fragments of this wave's K slice: row arow, k = kw + 64 u + 16 g + [0, 16)
     d8_u32x4 av[KU][2];
     {
-        const d8_u32x4* xp = reinterpret_cast<const d8_u32x4*>(p.x + (int64_t)arow * p.ldx + kw + 16 * g);
+        const d8_u32x4* xp = reinterpret_cast<const d8_u32x4*>(p.x + (int64_t)arow * p.ldx + (SPL ? 0 : kw) + 16 * g);
 #pragma unroll
         for (int u = 0; u < KU; u++) {
-            av[u][0] = xp[8 * u];
-            av[u][1] = xp[8 * u + 1];
+            if constexpr (SPL) {
+                const int ok = u < kval;
+                const int o = ok ? (kw / 8 + 8 * u) : 0;
+                const d8_u32x4 z = d8_u32x4{0u, 0u, 0u, 0u};
+                const d8_u32x4 v0 = xp[o], v1 = xp[o + 1];
+                av[u][0] = ok ? v0 : z;
+                av[u][1] = ok ? v1 : z;
+            } else {
+                av[u][0] = xp[8 * u];
+                av[u][1] = xp[8 * u + 1];
+            }
         }
     }
     // this wave's slice of the norm weights: one 16-B load per lane (k = kw + 8 lane), staged
@@ -124,7 +150,7 @@ __global__ __launch_bounds__(KS * 64) void dec8_kernel(Dec8Params p) {
     // hf (which half of the tile) is a constant at every call site: the epilogue operands
     // ride with the second half only
     auto issue = [&](Step& t, int it, int hf) {
-        const int tile = (int)blockIdx.x + it * (int)gridDim.x;
+        const int tile = bi + it * G;
         const int sg = NB == 2 ? 0 : (tile < p.t01[0] ? 0 : (tile < p.t01[1] ? 1 : 2));
         const int tb0 = sg == 0 ? 0 : (sg == 1 ? p.t01[0] : p.t01[1]);
         const int rows = p.seg_rows[sg];
@@ -137,7 +163,13 @@ __global__ __launch_bounds__(KS * 64) void dec8_kernel(Dec8Params p) {
             const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), (short)0,
                                                               (int)((int64_t)rows * (K + 4)), 0x00020000);
 #pragma unroll
-            for (int u = 0; u < KH; u++) t.wv[b][u] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, u * 64, kNT);
+            for (int u = 0; u < KH; u++) {
+                if constexpr (SPL)
+                    t.wv[b][u] = __builtin_amdgcn_raw_buffer_load_b128(
+                        rs, hf * KH + u < kval ? voff + u * 64 : 0x7ffffff0, 0, kNT);
+                else
+                    t.wv[b][u] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, u * 64, kNT);
+            }
             if (hf) t.sc[b] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, rows * K + r * 4, 0, 0));
         }
         if (!hf) return;
@@ -242,7 +274,7 @@ __global__ __launch_bounds__(KS * 64) void dec8_kernel(Dec8Params p) {
         // next tile's barrier, which the epilogue wave reaches only after its reads
         __syncthreads();
         if (wave != it % KS) return;   // wave-uniform
-        const int tile = (int)blockIdx.x + it * (int)gridDim.x;
+        const int tile = bi + it * G;
         const int n = tile * 16 + fr;
         float c[NB][4];
 #pragma unroll
@@ -252,6 +284,28 @@ __global__ __launch_bounds__(KS * 64) void dec8_kernel(Dec8Params p) {
             for (int w = 1; w < KS; w++) {
                 const float4 v = *reinterpret_cast<const float4*>(&red[buf][w][b][lane * 4]);
                 s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+            }
+            if constexpr (SPL) {
+                // publish this part's tile write-through, drain, take the ticket; the last
+                // arriver sums every part in part order (independent of arrival order)
+                float* tb = p.slab + (int64_t)tile * p.parts * 256;
+                const auto rs = __builtin_amdgcn_make_buffer_rsrc(tb, (short)0, p.parts * 1024, 0x00020000);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(d8_u32x4, d8_f32x4{s.x, s.y, s.z, s.w}), rs,
+                                                       part * 1024 + lane * 16, 0, 16);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                unsigned old = 0;
+                if (lane == 0) old = __hip_atomic_fetch_add(p.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                old = __shfl(old, 0, 64);
+                if (old != (unsigned)p.parts - 1) return;   // wave-uniform
+                for (int q = 0; q < p.parts; q++) {
+                    const d8_f32x4 v = __builtin_bit_cast(d8_f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, q * 1024 + lane * 16, 0, 16));
+                    if (q == 0) {
+                        s = make_float4(v[0], v[1], v[2], v[3]);
+                    } else {
+                        s.x += v[0]; s.y += v[1]; s.z += v[2]; s.w += v[3];
+                    }
+                }
+                if (lane == 0) __hip_atomic_store(p.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             c[b][0] = s.x * t.sc[b];
             c[b][1] = s.y * t.sc[b];
@@ -583,19 +637,71 @@ static int dec8r_launch(const Dec8Params& p, hipStream_t st) {
     return 0;
 }
 
-template <int EPI, int KU, int KS>
+template <int EPI, int KU, int KS, bool SPL = false>
 static int dec8_launch(const Dec8Params& p, hipStream_t st) {
-    const void* fn = (const void*)dec8_kernel<EPI, KU, KS>;
+    const void* fn = (const void*)dec8_kernel<EPI, KU, KS, SPL>;
     static int per_cu = 0;   // resident blocks per CU (one per instantiation, cached)
     if (per_cu == 0) {
         int nb = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, KS * 64, 0) != hipSuccess || nb < 1) nb = 1;
         per_cu = nb;
     }
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(p.n_tiles, (int64_t)device_cu_count() * per_cu));
-    hipLaunchKernelGGL((dec8_kernel<EPI, KU, KS>), dim3(grid), dim3(KS * 64), 0, st, p);
+    const int64_t slots = (int64_t)device_cu_count() * per_cu;
+    int grid;
+    if constexpr (SPL) {   // parts x G blocks, G tiles in flight per part (one round if they fit)
+        const int64_t g = std::max<int64_t>(1, std::min<int64_t>(p.n_tiles, slots / p.parts));
+        grid = (int)(g * p.parts);
+    } else {
+        grid = (int)std::max<int64_t>(1, std::min<int64_t>(p.n_tiles, slots));
+    }
+    hipLaunchKernelGGL((dec8_kernel<EPI, KU, KS, SPL>), dim3(grid), dim3(KS * 64), 0, st, p);
     QIE_LAUNCH_CHECK();
     return 0;
+}
+
+// Split-K workspace (slabs + tickets), one per stream — streams of one device may run
+// projections at the same time (tensor-parallel ranks on one GPU in the tests) — reserved by
+// qie_batch_create (dec8_reserve) so that the captured decode step finds it; tickets are
+// zero at rest (the last arriver resets its tile's).
+namespace {
+constexpr int kDec8MaxTiles = 2048, kDec8MaxParts = 8;   // N <= 32,768 (dec8_applies)
+struct Dec8Ws {
+    float* slab = nullptr;
+    unsigned* cnt = nullptr;
+};
+std::mutex g_d8_mu;
+std::map<hipStream_t, Dec8Ws> g_d8_ws;
+}  // namespace
+
+int dec8_reserve(hipStream_t st) {
+    std::lock_guard<std::mutex> lk(g_d8_mu);
+    Dec8Ws& w = g_d8_ws[st];
+    if (w.slab) return 0;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return 1;
+    QIE_HIP(hipMalloc((void**)&w.slab, (size_t)kDec8MaxTiles * kDec8MaxParts * 1024));
+    QIE_HIP(hipMalloc((void**)&w.cnt, (size_t)kDec8MaxTiles * 4));
+    QIE_HIP(hipMemsetAsync(w.cnt, 0, (size_t)kDec8MaxTiles * 4, st));
+    QIE_HIP(hipStreamSynchronize(st));
+    return 0;
+}
+
+static bool dec8_workspace(hipStream_t st, Dec8Params* p) {
+    if (dec8_reserve(st) != 0) return false;
+    std::lock_guard<std::mutex> lk(g_d8_mu);
+    const Dec8Ws& w = g_d8_ws[st];
+    p->slab = w.slab;
+    p->cnt = w.cnt;
+    return true;
+}
+
+template <int KU, int KS>
+static int dec8_epi_split(const Dec8Params& p, int epi, hipStream_t st) {
+    switch (epi) {
+        case QIE_EPI_RESIDUAL: return dec8_launch<QIE_EPI_RESIDUAL, KU, KS, true>(p, st);
+        case QIE_EPI_F32: return dec8_launch<QIE_EPI_F32, KU, KS, true>(p, st);
+        default: return dec8_launch<QIE_EPI_STORE, KU, KS, true>(p, st);
+    }
 }
 
 template <int KU, int KS>
@@ -620,6 +726,9 @@ static int dec8_epi(const Dec8Params& p, int epi, hipStream_t st) {
 
 // K slice shapes: (units per wave KU, waves KS) with KU * KS * 64 = K.  7 waves x 8 units at
 // K = 3,584 (14 x 4 measured the same for QKV and 0.45 µs slower for O at config 4).
+// Long K without such a shape (the down projection's 18,944 = 296 units): split-K over
+// parts of 8 waves x KU units (QIE_DEC8_SPLIT_KU, 8 or 4; the last part ragged), single-
+// segment epilogues without a fused norm only (a norm needs the whole row in one block).
 static bool dec8_shape(int64_t K, int* ku, int* ks) {
     if (K % 64 != 0) return false;
     const int64_t units = K / 64;
@@ -632,13 +741,21 @@ static bool dec8_shape(int64_t K, int* ku, int* ks) {
         }
     return false;
 }
+static int dec8_split_parts(const qie_linear_args* a, int* ku) {
+    if (a->K % 64 != 0 || a->norm_w || a->epilogue == QIE_EPI_SWIGLU || a->seg_rows[1] > 0) return 0;
+    if (dev_env("QIE_DEC8_SPLIT", 1) == 0) return 0;
+    const int64_t units = a->K / 64;
+    *ku = dev_env("QIE_DEC8_SPLIT_KU", 8) == 4 ? 4 : 8;
+    const int64_t parts = (units + 8 * *ku - 1) / (8 * *ku);
+    return parts >= 2 && parts <= kDec8MaxParts ? (int)parts : 0;
+}
 
 // true when dec8_linear takes this projection (the engine then skips its separate norm)
 bool dec8_applies(const qie_linear_args* a) {
     if (!(a->flags & QIE_LINEAR_FP8) || a->M < 2 || a->M > 16) return false;
     if (dev_env("QIE_DEC8", 1) == 0) return false;
     int ku, ks;
-    if (!dec8_shape(a->K, &ku, &ks)) return false;
+    if (!dec8_shape(a->K, &ku, &ks) && dec8_split_parts(a, &ku) == 0) return false;
     // vocabulary-sized projections (tens of tiles per block) keep the general skinny kernel:
     // its 16 waves per CU keep more bytes in flight than one 7-wave block (lm_head 119 vs 194 µs)
     if (a->N <= 0 || a->N > 32768 || a->ldx % 8 != 0 || a->K >= (1 << 20)) return false;
@@ -654,7 +771,10 @@ bool dec8_applies(const qie_linear_args* a) {
     return true;
 }
 
-int dec8_linear(const qie_linear_args* a, hipStream_t st) {
+// *done = false: not taken (a split-K projection whose workspace cannot be made during a
+// graph capture); the caller runs its general kernel
+int dec8_linear(const qie_linear_args* a, hipStream_t st, bool* done) {
+    *done = true;
     QIE_REQUIRE(dec8_applies(a), "qie_linear: internal: fp8 batched-decode path does not apply");
     Dec8Params p;
     p.x = (const uint16_t*)a->x;
@@ -670,6 +790,9 @@ int dec8_linear(const qie_linear_args* a, hipStream_t st) {
     p.keys = (unsigned long long*)a->argmax_keys;
     p.key_col0 = a->key_col0;
     p.dbg = dev_env("QIE_DEC8_DBG", 0);
+    p.parts = 1;
+    p.slab = nullptr;
+    p.cnt = nullptr;
     p.n_tiles = (int32_t)((a->N + 15) / 16);
     for (int s = 0; s < 3; s++) {
         p.w[s] = (const uint8_t*)a->w[s];
@@ -690,7 +813,14 @@ int dec8_linear(const qie_linear_args* a, hipStream_t st) {
                     "qie_linear: segment rows do not match the weights");
     }
     int ku = 0, ks = 0;
-    dec8_shape(a->K, &ku, &ks);
+    if (!dec8_shape(a->K, &ku, &ks)) {
+        p.parts = dec8_split_parts(a, &ku);
+        if (!dec8_workspace(st, &p)) {
+            *done = false;
+            return 0;
+        }
+        return ku == 4 ? dec8_epi_split<4, 8>(p, a->epilogue, st) : dec8_epi_split<8, 8>(p, a->epilogue, st);
+    }
     if (ku == 8 && ks == 7) return dec8_epi<8, 7>(p, a->epilogue, st);
     if (ku == 8 && ks == 8) return dec8_epi<8, 8>(p, a->epilogue, st);
     if (ku == 2 && ks == 7) return dec8_epi<2, 7>(p, a->epilogue, st);

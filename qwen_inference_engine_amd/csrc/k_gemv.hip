@@ -1338,11 +1338,15 @@ int gemv_rope(const qie_linear_args* a, const int32_t* pos, const float* cs, con
 }
 
 bool dec8_applies(const qie_linear_args* a);
-int dec8_linear(const qie_linear_args* a, hipStream_t st);
+int dec8_linear(const qie_linear_args* a, hipStream_t st, bool* done);
 
 int gemv(const qie_linear_args* a, hipStream_t st) {
-    // fp8 weights, 2..16 rows, K a whole number of per-wave slices: k_decode_fp8.hip
-    if (dec8_applies(a)) return dec8_linear(a, st);
+    // fp8 weights, 2..16 rows, K a whole number of per-wave slices (or split-K): k_decode_fp8.hip
+    if (dec8_applies(a)) {
+        bool done = false;
+        const int rc = dec8_linear(a, st, &done);
+        if (done) return rc;
+    }
     GemvParams p;
     p.x = (const uint16_t*)a->x;
     p.ldx = a->ldx;

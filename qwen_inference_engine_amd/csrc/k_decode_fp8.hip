@@ -265,53 +265,14 @@ __global__ __launch_bounds__(KS * 64) void dec8_kernel(Dec8Params p) {
         }
     };
     // tile end (after its second step): partial tiles -> LDS, one barrier, epilogue
-    auto finish = [&](const Step& t, int it) {
-        const int buf = it & 1;
-#pragma unroll
-        for (int b = 0; b < NB; b++)
-            *reinterpret_cast<float4*>(&red[buf][wave][b][lane * 4]) = make_float4(acc[b][0], acc[b][1], acc[b][2], acc[b][3]);
-        // one barrier per tile: the next write of red[buf] is two tiles away, behind the
-        // next tile's barrier, which the epilogue wave reaches only after its reads
-        __syncthreads();
-        if (wave != it % KS) return;   // wave-uniform
-        const int tile = bi + it * G;
+    // the epilogue of one output tile from its fp32 sums (before the row scale)
+    auto emit = [&](int tile, const float (&sum)[NB][4], const float* scv, const float* epv) {
         const int n = tile * 16 + fr;
         float c[NB][4];
 #pragma unroll
-        for (int b = 0; b < NB; b++) {
-            float4 s = *reinterpret_cast<const float4*>(&red[buf][0][b][lane * 4]);
+        for (int b = 0; b < NB; b++)
 #pragma unroll
-            for (int w = 1; w < KS; w++) {
-                const float4 v = *reinterpret_cast<const float4*>(&red[buf][w][b][lane * 4]);
-                s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-            }
-            if constexpr (SPL) {
-                // publish this part's tile write-through, drain, take the ticket; the last
-                // arriver sums every part in part order (independent of arrival order)
-                float* tb = p.slab + (int64_t)tile * p.parts * 256;
-                const auto rs = __builtin_amdgcn_make_buffer_rsrc(tb, (short)0, p.parts * 1024, 0x00020000);
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(d8_u32x4, d8_f32x4{s.x, s.y, s.z, s.w}), rs,
-                                                       part * 1024 + lane * 16, 0, 16);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                unsigned old = 0;
-                if (lane == 0) old = __hip_atomic_fetch_add(p.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                old = __shfl(old, 0, 64);
-                if (old != (unsigned)p.parts - 1) return;   // wave-uniform
-                for (int q = 0; q < p.parts; q++) {
-                    const d8_f32x4 v = __builtin_bit_cast(d8_f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, q * 1024 + lane * 16, 0, 16));
-                    if (q == 0) {
-                        s = make_float4(v[0], v[1], v[2], v[3]);
-                    } else {
-                        s.x += v[0]; s.y += v[1]; s.z += v[2]; s.w += v[3];
-                    }
-                }
-                if (lane == 0) __hip_atomic_store(p.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            c[b][0] = s.x * t.sc[b];
-            c[b][1] = s.y * t.sc[b];
-            c[b][2] = s.z * t.sc[b];
-            c[b][3] = s.w * t.sc[b];
-        }
+            for (int r = 0; r < 4; r++) c[b][r] = sum[b][r] * scv[b];
         if (n >= p.N) return;
 #pragma unroll
         for (int r = 0; r < 4; r++) {
@@ -324,11 +285,11 @@ __global__ __launch_bounds__(KS * 64) void dec8_kernel(Dec8Params p) {
                 const float a = rbf(gg * (1.0f / (1.0f + expf(-gg))));
                 yr[n] = f2bf(uu * a);
             } else if constexpr (EPI == QIE_EPI_RESIDUAL) {
-                yr[n] = f2bf(t.ep[r] + rbf(c[0][r]));
+                yr[n] = f2bf(epv[r] + rbf(c[0][r]));
             } else if constexpr (EPI == QIE_EPI_F32) {
                 reinterpret_cast<float*>(p.y)[(int64_t)i * p.ldy + n] = c[0][r];
             } else {
-                const uint16_t o = f2bf(c[0][r] + t.ep[0]);
+                const uint16_t o = f2bf(c[0][r] + epv[0]);
                 yr[n] = o;
                 if (p.keys) {
                     const unsigned long long kk = sel_key(bf2f(o), (uint32_t)(n + p.key_col0));
@@ -336,6 +297,81 @@ __global__ __launch_bounds__(KS * 64) void dec8_kernel(Dec8Params p) {
                 }
             }
         }
+    };
+    // split-K: each tile's reduced part sums wait in LDS until the block's last tile, then
+    // every wave publishes one tile (so the publish / ticket round trips of all the block's
+    // tiles overlap, and none stalls the weight stream)
+    constexpr int kKeep = SPL ? 8 : 1;
+    __shared__ __attribute__((aligned(16))) float keep[kKeep][256];
+    // tile end (after its second step): partial tiles -> LDS, one barrier, epilogue
+    auto finish = [&](const Step& t, int it) {
+        const int buf = it & 1;
+#pragma unroll
+        for (int b = 0; b < NB; b++)
+            *reinterpret_cast<float4*>(&red[buf][wave][b][lane * 4]) = make_float4(acc[b][0], acc[b][1], acc[b][2], acc[b][3]);
+        // one barrier per tile: the next write of red[buf] is two tiles away, behind the
+        // next tile's barrier, which the epilogue wave reaches only after its reads
+        __syncthreads();
+        if (wave != it % KS) return;   // wave-uniform
+        float sum[NB][4];
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+            float4 v4 = *reinterpret_cast<const float4*>(&red[buf][0][b][lane * 4]);
+#pragma unroll
+            for (int w = 1; w < KS; w++) {
+                const float4 v = *reinterpret_cast<const float4*>(&red[buf][w][b][lane * 4]);
+                v4.x += v.x; v4.y += v.y; v4.z += v.z; v4.w += v.w;
+            }
+            sum[b][0] = v4.x; sum[b][1] = v4.y; sum[b][2] = v4.z; sum[b][3] = v4.w;
+        }
+        if constexpr (SPL) {
+            *reinterpret_cast<float4*>(&keep[it][lane * 4]) = make_float4(sum[0][0], sum[0][1], sum[0][2], sum[0][3]);
+            return;
+        }
+        emit(bi + it * G, sum, t.sc, t.ep);
+    };
+    // split-K tail of tile it (wave it % KS... any wave): publish this part's sums
+    // write-through, drain, take the ticket; the last arriver sums every part in part order
+    // (independent of arrival order), reloads the row scale and epilogue operands, emits
+    auto split_tail = [&](int it) {
+        const int tile = bi + it * G;
+        float* tb = p.slab + (int64_t)tile * p.parts * 256;
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(tb, (short)0, p.parts * 1024, 0x00020000);
+        const float4 k4 = *reinterpret_cast<const float4*>(&keep[it][lane * 4]);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(d8_u32x4, d8_f32x4{k4.x, k4.y, k4.z, k4.w}), rs,
+                                               part * 1024 + lane * 16, 0, 16);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned old = 0;
+        if (lane == 0) old = __hip_atomic_fetch_add(p.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        old = __shfl(old, 0, 64);
+        if (old != (unsigned)p.parts - 1) return;   // wave-uniform
+        const int rows = p.seg_rows[0];
+        int r = tile * 16 + fr;
+        r = r < rows ? r : rows - 1;
+        const auto rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p.w[0]), (short)0,
+                                                          (int)((int64_t)rows * (K + 4)), 0x00020000);
+        float scv[NB], epv[4] = {0.f, 0.f, 0.f, 0.f};
+        scv[0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw, rows * K + r * 4, 0, 0));
+        const int n = tile * 16 + fr;
+        const int nc = n < p.N ? n : p.N - 1;
+        if constexpr (EPI == QIE_EPI_RESIDUAL) {
+#pragma unroll
+            for (int rr = 0; rr < 4; rr++) {
+                const int i = 4 * g + rr < M ? 4 * g + rr : M - 1;
+                epv[rr] = bf2f(p.y[(int64_t)i * p.ldy + nc]);
+            }
+        } else if constexpr (EPI == QIE_EPI_STORE) {
+            const uint16_t* bp = p.bias[0];
+            epv[0] = bp ? bf2f(bp[r]) : 0.f;
+        }
+        float sum[NB][4];
+        for (int q = 0; q < p.parts; q++) {
+            const d8_f32x4 v = __builtin_bit_cast(d8_f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, q * 1024 + lane * 16, 0, 16));
+#pragma unroll
+            for (int j = 0; j < 4; j++) sum[0][j] = q == 0 ? v[j] : sum[0][j] + v[j];
+        }
+        if (lane == 0) __hip_atomic_store(p.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        emit(tile, sum, scv, epv);
     };
 
     // steps alternate sa (first half of a tile) / sb (second half); the next step is
@@ -353,6 +389,10 @@ __global__ __launch_bounds__(KS * 64) void dec8_kernel(Dec8Params p) {
     mma(sa, 0);
     mma(sb, 1);
     finish(sb, it);
+    if constexpr (SPL) {
+        __syncthreads();   // every tile's sums are in keep[]
+        for (int t2 = wave; t2 < my; t2 += KS) split_tail(t2);
+    }
     if constexpr (EPI == QIE_EPI_STORE) {
         if (p.keys) {
 #pragma unroll
@@ -649,7 +689,8 @@ static int dec8_launch(const Dec8Params& p, hipStream_t st) {
     const int64_t slots = (int64_t)device_cu_count() * per_cu;
     int grid;
     if constexpr (SPL) {   // parts x G blocks, G tiles in flight per part (one round if they fit)
-        const int64_t g = std::max<int64_t>(1, std::min<int64_t>(p.n_tiles, slots / p.parts));
+        // and at most 8 tiles per block (the kernel keeps each tile's part sums in LDS)
+        const int64_t g = std::max<int64_t>((p.n_tiles + 7) / 8, std::min<int64_t>(p.n_tiles, slots / p.parts));
         grid = (int)(g * p.parts);
     } else {
         grid = (int)std::max<int64_t>(1, std::min<int64_t>(p.n_tiles, slots));
@@ -664,7 +705,7 @@ static int dec8_launch(const Dec8Params& p, hipStream_t st) {
 // qie_batch_create (dec8_reserve) so that the captured decode step finds it; tickets are
 // zero at rest (the last arriver resets its tile's).
 namespace {
-constexpr int kDec8MaxTiles = 2048, kDec8MaxParts = 8;   // N <= 32,768 (dec8_applies)
+constexpr int kDec8MaxTiles = 2048, kDec8MaxParts = 16;   // N <= 32,768 (dec8_applies)
 struct Dec8Ws {
     float* slab = nullptr;
     unsigned* cnt = nullptr;
@@ -727,8 +768,12 @@ static int dec8_epi(const Dec8Params& p, int epi, hipStream_t st) {
 // K slice shapes: (units per wave KU, waves KS) with KU * KS * 64 = K.  7 waves x 8 units at
 // K = 3,584 (14 x 4 measured the same for QKV and 0.45 µs slower for O at config 4).
 // Long K without such a shape (the down projection's 18,944 = 296 units): split-K over
-// parts of 8 waves x KU units (QIE_DEC8_SPLIT_KU, 8 or 4; the last part ragged), single-
-// segment epilogues without a fused norm only (a norm needs the whole row in one block).
+// parts of 8 waves x 4 units (10 parts at 18,944, the last one ragged; 128 VGPRs, two blocks
+// per CU), single-segment epilogues without a fused norm only (a norm needs the whole row in
+// one block).  Config 4 (fp8, B = 8), same box: the general skinny kernel 2,895 tok/s (down
+// 24.9 µs live), split 8 x 8 units 2,990 (23.4), 8 x 4 units 3,010 (23.0); the first form,
+// which published each tile's parts as it finished it, stalled every wave on its ticket
+// round trip behind the per-tile barrier: 2,760 (31.5).
 static bool dec8_shape(int64_t K, int* ku, int* ks) {
     if (K % 64 != 0) return false;
     const int64_t units = K / 64;
@@ -745,7 +790,7 @@ static int dec8_split_parts(const qie_linear_args* a, int* ku) {
     if (a->K % 64 != 0 || a->norm_w || a->epilogue == QIE_EPI_SWIGLU || a->seg_rows[1] > 0) return 0;
     if (dev_env("QIE_DEC8_SPLIT", 1) == 0) return 0;
     const int64_t units = a->K / 64;
-    *ku = dev_env("QIE_DEC8_SPLIT_KU", 8) == 4 ? 4 : 8;
+    *ku = dev_env("QIE_DEC8_SPLIT_KU", 4) == 8 ? 8 : 4;
     const int64_t parts = (units + 8 * *ku - 1) / (8 * *ku);
     return parts >= 2 && parts <= kDec8MaxParts ? (int)parts : 0;
 }

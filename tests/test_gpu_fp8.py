@@ -258,9 +258,11 @@ def test_fp8_batched_decode_kernel(oracle, qlib, M, K, num):
 @pytest.mark.parametrize("M", [2, 8, 16])
 @pytest.mark.parametrize("K,N", [(4864, 896), (18944, 3584)])
 def test_fp8_batched_decode_long_k(oracle, qlib, M, K, N):
-    """fp8, 2..16 rows, long K without a norm (the down projection; the skinny MFMA kernel,
-    k_gemv.hip — a long-K form of k_decode_fp8.hip measured no faster and was dropped):
-    residual, STORE + bias and fp32 against the oracle on the dequantised weights."""
+    """fp8, 2..16 rows, long K without a norm (the down projection): k_decode_fp8.hip's
+    split-K form (parts of 8 waves x 4 units, the last one ragged: 3 parts at K = 4,864, 10 at
+    18,944; the last arriving part sums them in part order): residual, STORE + bias and fp32
+    against the oracle on the dequantised weights; a second launch reproduces the first bit
+    for bit (the tickets are back at zero, the part order does not depend on arrival)."""
     h = rand_bf16(oracle, (M, K), seed=K + M)
     dw, qw = _fp8_dev(qlib, rand_bf16(oracle, (N, K), 0.02, seed=4))
     res = rand_bf16(oracle, (M, N), seed=5)
@@ -272,6 +274,9 @@ def test_fp8_batched_decode_long_k(oracle, qlib, M, K, N):
     got = G.host_bf16(yr)
     assert (np.abs(G.bf(got).astype(np.float64) - G.bf(want)) <= tol).all()
     assert (G.ulp_diff(got, want) == 0).mean() > 0.99
+    yr2 = G.dev(res)
+    _linear(qlib, G.dev(h), [(dw, N)], [], M, K, N, yr2, _lib.QIE_EPI_RESIDUAL, flags=_lib.QIE_LINEAR_FP8)
+    assert np.array_equal(G.host_bf16(yr2), got)
     # STORE + bias (the bench's live timing of this launch uses it)
     b = rand_bf16(oracle, (N,), 0.1, seed=6)
     ys = G.zeros_bf16(M, N)

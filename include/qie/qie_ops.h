@@ -245,6 +245,9 @@ int qie_synthetic_fill_host(void* host, int64_t n, uint32_t tensor_id, uint64_t 
  * with 256x256 (TILE256) or 256x128 (TILE128) block tiles instead of the tile-count choice. */
 #define QIE_LINEAR_TILE256 2
 #define QIE_LINEAR_TILE128 4
+/* ... or the stream-K form of the 256x256 kernel (K % 64 == 0, K >= 256): one workgroup
+ * per CU, (tile, k-tile) units in contiguous ranges, shared tiles summed in k order. */
+#define QIE_LINEAR_STREAMK 8
 int64_t qie_fp8_weight_bytes(int64_t rows, int64_t cols);
 int qie_quantize_fp8(const void* w_bf16, int64_t rows, int64_t cols, void* out, void* stream);
 int qie_quantize_fp8_host(const void* w_bf16, int64_t rows, int64_t cols, void* out);
@@ -253,6 +256,17 @@ int qie_quantize_fp8_host(const void* w_bf16, int64_t rows, int64_t cols, void* 
  * runs the bf16 LDS-DMA GEMM: at prefill sizes the GEMM is MFMA-bound and the expansion
  * (1 + 2 bytes per weight) is ~2 % of it. */
 int qie_dequantize_fp8(const void* w_fp8, int64_t rows, int64_t cols, void* out_bf16, void* stream);
+/* 16-row tiled fp8 layout (QIE_LINEAR_FP8_T16): the codes of rows [16t, 16t + 16) are stored
+ * as K/64 consecutive 1-KiB blocks, block j holding row 16t + (l % 16), columns
+ * 64j + 16(l / 16) + [0, 16) at bytes [16 l, 16 l + 16) (l = 0..63) — exactly the B fragments
+ * of one 64-column unit of the batched-decode MFMA kernel, so each of its 1-KiB wave loads
+ * is contiguous (8 whole 128-B lines instead of 16 rows x 64 B); the row scales follow the
+ * codes as in the plain layout.  rows % 16 == 0, cols % 64 == 0.  qie_linear reads such
+ * weights with args.flags QIE_LINEAR_FP8 | QIE_LINEAR_FP8_T16 (the batched-decode kernel
+ * only: M <= 16 rows; the engine tiles its own decode projections, tiled weights are not
+ * read by the prefill GEMMs, which take the dequantised bf16 copy). */
+#define QIE_LINEAR_FP8_T16 16
+int qie_fp8_tile16(const void* w_fp8, int64_t rows, int64_t cols, void* out, void* stream);
 /* Test probe: out_dev[i] = the device decode of e4m3 code i (i < 256). */
 int qie_debug_fp8_decode(float* out_dev);
 /* Test probe: out_dev[i] = the bf16 bits the fp8 MFMA GEMV decodes e4m3 code i to (i < 256). */

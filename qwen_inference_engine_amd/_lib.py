@@ -23,6 +23,8 @@ QIE_EPI_F32 = 3
 QIE_LINEAR_FP8 = 1
 QIE_LINEAR_TILE256 = 2
 QIE_LINEAR_TILE128 = 4
+QIE_LINEAR_STREAMK = 8
+QIE_LINEAR_FP8_T16 = 16
 QIE_ATTN_PREROPED = 0x100   # qie_attention_decode numerics flag: q / new k arrive rotated
 QIE_COMM_ID_BYTES = 128
 QIE_COMM_PEER_HANDLE_BYTES = 128
@@ -133,6 +135,7 @@ SIGNATURES = [
     ("qie_quantize_fp8", C.c_int, [_P, _I64, _I64, _P, _P]),
     ("qie_quantize_fp8_host", C.c_int, [_P, _I64, _I64, _P]),
     ("qie_dequantize_fp8", C.c_int, [_P, _I64, _I64, _P, _P]),
+    ("qie_fp8_tile16", C.c_int, [_P, _I64, _I64, _P, _P]),
     ("qie_debug_fp8_decode", C.c_int, [_P]),
     ("qie_debug_fp8_decode_bf16", C.c_int, [_P]),
     # qie_engine.h

@@ -85,6 +85,8 @@ struct qie_engine {
     qie_model_weights w{};
     bool have_weights = false;
     bool fp8 = false;            // linear weights are e4m3 + row scales (fp8_arena)
+    bool fp8_t16 = false;        // ... and the decode projections in the 16-row tiled layout
+    bool fp8_t16_head = false;   // ... and the lm_head too
     // fp8 engines: the same (dequantised) layer weights as bf16, in place in the arena —
     // prefill's MFMA GEMMs read these (compute-bound: the LDS-DMA bf16 kernel), decode's
     // bandwidth-bound GEMVs the fp8 codes; both compute the one dequantised model
@@ -355,6 +357,52 @@ static int quantize_weights_fp8(qie_engine* e, bool own_arena) {
     QIE_HIP(hipStreamSynchronize(e->stream));
     e->w.layers = e->layers.data();
     e->fp8 = true;
+    e->fp8_t16 = e->fp8_t16_head = false;
+    // The decode projections go to the 16-row tiled layout (qie_fp8_tile16: every 1-KiB wave
+    // load of the batched-decode kernel contiguous) when that kernel takes every one of them
+    // at any batch (it is then their only reader; prefill reads the dequantised bf16 copy, so
+    // the engine must own its arena).  QIE_FP8_T16=0 (dev) keeps the plain layout.
+    if (own_arena && dev_env("QIE_FP8_T16", 1) != 0) {
+        auto ok = [&](int64_t K, int64_t N, int64_t s0, int64_t s1, int64_t s2, bool norm, int epi) {
+            qie_linear_args a;
+            std::memset(&a, 0, sizeof(a));
+            a.flags = QIE_LINEAR_FP8 | QIE_LINEAR_FP8_T16;
+            a.M = 1; a.K = K; a.N = N; a.ldx = K;
+            a.seg_rows[0] = s0; a.seg_rows[1] = s1; a.seg_rows[2] = s2;
+            a.norm_w = norm ? (const void*)e : nullptr;   // (only tested for presence)
+            a.epilogue = epi;
+            return dec8_applies(&a);
+        };
+        const bool all = ok(H, QD + 2 * KD, QD, KD, KD, true, QIE_EPI_STORE) && ok(QD, H, H, 0, 0, false, QIE_EPI_RESIDUAL) &&
+                         ok(H, I, I, I, 0, true, QIE_EPI_SWIGLU) && ok(I, H, H, 0, 0, false, QIE_EPI_RESIDUAL);
+        // the vocabulary projection stays plain for the general skinny kernel: tiled, through
+        // this kernel (one 7-wave block per CU, ~37 tiles each), config 4's lm_head took 168.9
+        // vs 119-120 µs (dev QIE_FP8_T16_HEAD=1 tiles it; its readers are <= 8-row heads)
+        const bool head = all && dev_env("QIE_FP8_T16_HEAD", 0) != 0 && ok(H, V, V, 0, 0, true, QIE_EPI_STORE);
+        if (all) {
+            size_t big = 0;
+            for (auto& t : ts)
+                if (t.p != &e->w.lm_head || head) big = std::max<size_t>(big, (size_t)qie_fp8_weight_bytes(t.rows, t.cols));
+            void* tmp = nullptr;
+            QIE_TRY(dmalloc(&tmp, big));
+            int rc = 0;
+            for (auto& t : ts) {
+                if (t.p == &e->w.lm_head && !head) continue;
+                const size_t nb = (size_t)qie_fp8_weight_bytes(t.rows, t.cols);
+                rc = qie_fp8_tile16(*t.p, t.rows, t.cols, tmp, e->stream);
+                if (rc) break;
+                if (hipMemcpyAsync(const_cast<void*>(*t.p), tmp, nb, hipMemcpyDeviceToDevice, e->stream) != hipSuccess) {
+                    rc = fail(-5, "fp8 tiling: copy failed");
+                    break;
+                }
+            }
+            if (!rc && hipStreamSynchronize(e->stream) != hipSuccess) rc = fail(-5, "fp8 tiling: synchronize failed");
+            hipFree(tmp);
+            if (rc) return rc;
+            e->fp8_t16 = true;
+            e->fp8_t16_head = head;
+        }
+    }
     return 0;
 }
 
@@ -407,6 +455,12 @@ static qie_linear_args lin_base(const qie_engine* e) {
     qie_linear_args a;
     std::memset(&a, 0, sizeof(a));
     a.flags = e->fp8 ? QIE_LINEAR_FP8 : 0;
+    return a;
+}
+// the layer projections (QKV, O, gate/up, down): + the tiled-layout flag where they are tiled
+static qie_linear_args lin_proj(const qie_engine* e) {
+    qie_linear_args a = lin_base(e);
+    if (e->fp8_t16) a.flags |= QIE_LINEAR_FP8_T16;
     return a;
 }
 
@@ -471,7 +525,7 @@ static int enqueue_layer_decode(qie_batch* b, int l) {
     const int64_t QKVD = QD + 2 * KD, I = e->sh.ffn, B = b->B;
     const qie_kv_cache cache = batch_cache(b, 0);
 
-    qie_linear_args a = lin_base(e);
+    qie_linear_args a = lin_proj(e);
     a.x = b->x_res; a.ldx = H;
     a.w[0] = L.wq; a.w[1] = L.wk; a.w[2] = L.wv;
     a.bias[0] = L.bq; a.bias[1] = L.bk; a.bias[2] = L.bv;
@@ -491,7 +545,7 @@ static int enqueue_layer_decode(qie_batch* b, int l) {
                                          b->att, b->dec_ws, st);
     set_decode_rope_cur(nullptr);
     QIE_TRY(arc);
-    a = lin_base(e);
+    a = lin_proj(e);
     a.x = b->att; a.ldx = QD;
     a.w[0] = L.wo; a.seg_rows[0] = H;
     a.M = B; a.K = QD; a.N = H;
@@ -499,7 +553,7 @@ static int enqueue_layer_decode(qie_batch* b, int l) {
     QIE_TRY(row_parallel(b, a, b->x_res, b->part, B));
     QIE_TRY(dbg_snap(b, 2 * l + 1));
 
-    a = lin_base(e);
+    a = lin_proj(e);
     a.x = b->x_res; a.ldx = H;
     a.w[0] = L.w_gate; a.w[1] = L.w_up; a.seg_rows[0] = I; a.seg_rows[1] = I;
     a.M = B; a.K = H; a.N = I;
@@ -509,7 +563,7 @@ static int enqueue_layer_decode(qie_batch* b, int l) {
     QIE_TRY(prenorm(b, a, B));
     QIE_TRY(gemv(&a, st));
 
-    a = lin_base(e);
+    a = lin_proj(e);
     a.x = b->h; a.ldx = I;
     a.w[0] = L.w_down; a.seg_rows[0] = H;
     a.M = B; a.K = I; a.N = H;
@@ -550,6 +604,7 @@ static int enqueue_head(qie_batch* b, const uint16_t* x, int64_t ldx, int m0, in
     hipStream_t st = e->stream;
     const int64_t Vl = e->sh.vocab;
     qie_linear_args a = lin_base(e);
+    if (e->fp8_t16_head) a.flags |= QIE_LINEAR_FP8_T16;
     a.x = x; a.ldx = ldx;
     a.w[0] = e->w.lm_head; a.seg_rows[0] = Vl;
     a.M = M; a.K = s.hidden; a.N = Vl;
@@ -1052,7 +1107,7 @@ static int batch_create(qie_engine* e, int32_t batch, int32_t max_ctx, int32_t p
     b->h_pos.assign(batch, 0);
     if (!rc) rc = flush_table(b);
     // the fp8 batched-decode split-K workspace of this stream, before any graph capture
-    if (!rc && e->fp8 && batch >= 2) rc = dec8_reserve(e->stream);
+    if (!rc && e->fp8 && (batch >= 2 || e->fp8_t16)) rc = dec8_reserve(e->stream);
     if (rc) {
         qie_batch_destroy(b);
         return rc;
@@ -1161,11 +1216,13 @@ static int prefill_rows(qie_batch* b, int seq0, int n_seqs, const int32_t* ids, 
                        b->d_hist + (int64_t)seq0 * b->max_ctx, len, (int64_t)b->max_ctx);
     QIE_TRY(qie_embedding(e->w.embed, b->pf_ids, b->pf_x, n, H, st));
     const qie_kv_cache cache = batch_cache(b, seq0);
-    // fp8 engine, >= 256 rows: the GEMMs run on the dequantised bf16 copy (layers_pf)
-    const bool pf16 = e->fp8 && n >= 256 && !e->layers_pf.empty();
+    // fp8 engine, >= 256 rows: the GEMMs run on the dequantised bf16 copy (layers_pf); with
+    // tiled fp8 projections (readable by the batched-decode kernel only) every prefill of more
+    // than 16 rows does
+    const bool pf16 = e->fp8 && !e->layers_pf.empty() && (n >= 256 || (e->fp8_t16 && n > 16));
     auto pf_base = [&]() {
-        qie_linear_args a = lin_base(e);
-        if (pf16) a.flags &= ~QIE_LINEAR_FP8;
+        qie_linear_args a = lin_proj(e);
+        if (pf16) a.flags &= ~(QIE_LINEAR_FP8 | QIE_LINEAR_FP8_T16);
         return a;
     };
     for (int l = 0; l < s.n_layers; l++) {
@@ -1419,7 +1476,8 @@ int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* av
     const bool batched_norm = B >= 2 && dev_env("QIE_PRENORM", 1) != 0;
     auto args_for = [&](int l, double* by) {
         const qie_layer_weights& L = e->layers[l];
-        qie_linear_args a = lin_base(e);
+        qie_linear_args a = which == 4 ? lin_base(e) : lin_proj(e);
+        if (which == 4 && e->fp8_t16_head) a.flags |= QIE_LINEAR_FP8_T16;
         if (which == 0) {
             a.x = b->x_res; a.ldx = H; a.w[0] = L.w_gate; a.w[1] = L.w_up; a.seg_rows[0] = I; a.seg_rows[1] = I;
             a.M = B; a.K = H; a.N = I; a.y = scratch; a.ldy = I; a.epilogue = QIE_EPI_SWIGLU;
@@ -1540,6 +1598,9 @@ int qie_linear(const qie_linear_args* a, void* stream) {
     QIE_REQUIRE(a->epilogue != QIE_EPI_F32 || (a->bias[0] == nullptr && a->bias[1] == nullptr && a->bias[2] == nullptr),
                 "qie_linear: F32 (partial-sum) epilogue takes no bias");
     QIE_REQUIRE(a->argmax_keys == nullptr || a->epilogue == QIE_EPI_STORE, "qie_linear: arg-max needs STORE");
+    QIE_REQUIRE(!(a->flags & QIE_LINEAR_FP8_T16) || ((a->flags & QIE_LINEAR_FP8) && dec8_applies(a)),
+                "qie_linear: 16-row tiled fp8 weights are read by the batched-decode kernel only (M <= 16, K %% 64 == 0, "
+                "segments of whole 16-row tiles, N <= 32768)");
     hipStream_t st = (hipStream_t)stream;
     if (a->M <= 16) return gemv(a, st);   // GEMV (M = 1..8) or the skinny MFMA kernel (2..16)
     return gemm(a, st);

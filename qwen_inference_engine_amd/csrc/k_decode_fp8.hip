@@ -87,7 +87,7 @@ __device__ __forceinline__ uint32_t d8_rms_pair(uint32_t xv, uint32_t wv, float 
     return pack2(y[0], y[1]);
 }
 
-template <int EPI, int KU, int KS, bool SPL = false>
+template <int EPI, int KU, int KS, bool SPL = false, bool T16 = false>
 __global__ __launch_bounds__(KS * 64) void dec8_kernel(Dec8Params p) {
 #pragma clang fp contract(off)
     static_assert(!SPL || EPI != QIE_EPI_SWIGLU, "split-K: single-segment epilogues");
@@ -156,7 +156,12 @@ __global__ __launch_bounds__(KS * 64) void dec8_kernel(Dec8Params p) {
         const int rows = p.seg_rows[sg];
         int r = (tile - tb0) * 16 + fr;
         r = r < rows ? r : rows - 1;
-        const int voff = r * K + kw + 16 * g + hf * (KH * 64);
+        // plain layout: lane (fr, g) reads row r, columns kw + 64 u + 16 g + [0, 16) — one load
+        // instruction touches 16 rows x 64 B; 16-row tiled layout (T16, qie_fp8_tile16): the
+        // same fragment is bytes 16 lane of the unit's 1-KiB block — 8 whole 128-B lines
+        constexpr int UST = T16 ? 1024 : 64;
+        const int voff = T16 ? (tile - tb0) * 16 * K + kw * 16 + hf * (KH * 1024) + lane * 16
+                             : r * K + kw + 16 * g + hf * (KH * 64);
 #pragma unroll
         for (int b = 0; b < NB; b++) {
             const uint8_t* base = p.w[NB == 2 ? b : sg];
@@ -166,9 +171,9 @@ __global__ __launch_bounds__(KS * 64) void dec8_kernel(Dec8Params p) {
             for (int u = 0; u < KH; u++) {
                 if constexpr (SPL)
                     t.wv[b][u] = __builtin_amdgcn_raw_buffer_load_b128(
-                        rs, hf * KH + u < kval ? voff + u * 64 : 0x7ffffff0, 0, kNT);
+                        rs, hf * KH + u < kval ? voff + u * UST : 0x7ffffff0, 0, kNT);
                 else
-                    t.wv[b][u] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, u * 64, kNT);
+                    t.wv[b][u] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, u * UST, kNT);
             }
             if (hf) t.sc[b] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, rows * K + r * 4, 0, 0));
         }
@@ -677,9 +682,9 @@ static int dec8r_launch(const Dec8Params& p, hipStream_t st) {
     return 0;
 }
 
-template <int EPI, int KU, int KS, bool SPL = false>
+template <int EPI, int KU, int KS, bool SPL = false, bool T16 = false>
 static int dec8_launch(const Dec8Params& p, hipStream_t st) {
-    const void* fn = (const void*)dec8_kernel<EPI, KU, KS, SPL>;
+    const void* fn = (const void*)dec8_kernel<EPI, KU, KS, SPL, T16>;
     static int per_cu = 0;   // resident blocks per CU (one per instantiation, cached)
     if (per_cu == 0) {
         int nb = 0;
@@ -695,7 +700,7 @@ static int dec8_launch(const Dec8Params& p, hipStream_t st) {
     } else {
         grid = (int)std::max<int64_t>(1, std::min<int64_t>(p.n_tiles, slots));
     }
-    hipLaunchKernelGGL((dec8_kernel<EPI, KU, KS, SPL>), dim3(grid), dim3(KS * 64), 0, st, p);
+    hipLaunchKernelGGL((dec8_kernel<EPI, KU, KS, SPL, T16>), dim3(grid), dim3(KS * 64), 0, st, p);
     QIE_LAUNCH_CHECK();
     return 0;
 }
@@ -736,18 +741,18 @@ static bool dec8_workspace(hipStream_t st, Dec8Params* p) {
     return true;
 }
 
-template <int KU, int KS>
+template <int KU, int KS, bool T16>
 static int dec8_epi_split(const Dec8Params& p, int epi, hipStream_t st) {
     switch (epi) {
-        case QIE_EPI_RESIDUAL: return dec8_launch<QIE_EPI_RESIDUAL, KU, KS, true>(p, st);
-        case QIE_EPI_F32: return dec8_launch<QIE_EPI_F32, KU, KS, true>(p, st);
-        default: return dec8_launch<QIE_EPI_STORE, KU, KS, true>(p, st);
+        case QIE_EPI_RESIDUAL: return dec8_launch<QIE_EPI_RESIDUAL, KU, KS, true, T16>(p, st);
+        case QIE_EPI_F32: return dec8_launch<QIE_EPI_F32, KU, KS, true, T16>(p, st);
+        default: return dec8_launch<QIE_EPI_STORE, KU, KS, true, T16>(p, st);
     }
 }
 
-template <int KU, int KS>
+template <int KU, int KS, bool T16>
 static int dec8_epi(const Dec8Params& p, int epi, hipStream_t st) {
-    if constexpr (KU == 8 && KS == 7) {   // the ring form (config 4's K = 3,584), M <= 8 (dev A/B QIE_DEC8R)
+    if constexpr (KU == 8 && KS == 7 && !T16) {   // the ring form (config 4's K = 3,584), M <= 8 (dev A/B QIE_DEC8R)
         if (p.M <= 8 && dev_env("QIE_DEC8R", 0) != 0) {
             switch (epi) {
                 case QIE_EPI_SWIGLU: return dec8r_launch<QIE_EPI_SWIGLU, KU, KS, 8>(p, st);
@@ -758,10 +763,10 @@ static int dec8_epi(const Dec8Params& p, int epi, hipStream_t st) {
         }
     }
     switch (epi) {
-        case QIE_EPI_SWIGLU: return dec8_launch<QIE_EPI_SWIGLU, KU, KS>(p, st);
-        case QIE_EPI_RESIDUAL: return dec8_launch<QIE_EPI_RESIDUAL, KU, KS>(p, st);
-        case QIE_EPI_F32: return dec8_launch<QIE_EPI_F32, KU, KS>(p, st);
-        default: return dec8_launch<QIE_EPI_STORE, KU, KS>(p, st);
+        case QIE_EPI_SWIGLU: return dec8_launch<QIE_EPI_SWIGLU, KU, KS, false, T16>(p, st);
+        case QIE_EPI_RESIDUAL: return dec8_launch<QIE_EPI_RESIDUAL, KU, KS, false, T16>(p, st);
+        case QIE_EPI_F32: return dec8_launch<QIE_EPI_F32, KU, KS, false, T16>(p, st);
+        default: return dec8_launch<QIE_EPI_STORE, KU, KS, false, T16>(p, st);
     }
 }
 
@@ -788,7 +793,9 @@ static bool dec8_shape(int64_t K, int* ku, int* ks) {
 }
 static int dec8_split_parts(const qie_linear_args* a, int* ku) {
     if (a->K % 64 != 0 || a->norm_w || a->epilogue == QIE_EPI_SWIGLU || a->seg_rows[1] > 0) return 0;
-    if (dev_env("QIE_DEC8_SPLIT", 1) == 0) return 0;
+    if (a->N > (int64_t)kDec8MaxTiles * 16) return 0;   // the ticket array
+    // (tiled weights can be read by this kernel only: the dev switch does not apply to them)
+    if (!(a->flags & QIE_LINEAR_FP8_T16) && dev_env("QIE_DEC8_SPLIT", 1) == 0) return 0;
     const int64_t units = a->K / 64;
     *ku = dev_env("QIE_DEC8_SPLIT_KU", 4) == 8 ? 8 : 4;
     const int64_t parts = (units + 8 * *ku - 1) / (8 * *ku);
@@ -797,16 +804,25 @@ static int dec8_split_parts(const qie_linear_args* a, int* ku) {
 
 // true when dec8_linear takes this projection (the engine then skips its separate norm)
 bool dec8_applies(const qie_linear_args* a) {
-    if (!(a->flags & QIE_LINEAR_FP8) || a->M < 2 || a->M > 16) return false;
-    if (dev_env("QIE_DEC8", 1) == 0) return false;
+    // tiled weights (QIE_LINEAR_FP8_T16) are read by this kernel only, at any 1 <= M <= 16
+    const bool t16 = (a->flags & QIE_LINEAR_FP8_T16) != 0;
+    if (!(a->flags & QIE_LINEAR_FP8) || a->M < (t16 ? 1 : 2) || a->M > 16) return false;
+    if (!t16 && dev_env("QIE_DEC8", 1) == 0) return false;
     int ku, ks;
     if (!dec8_shape(a->K, &ku, &ks) && dec8_split_parts(a, &ku) == 0) return false;
     // vocabulary-sized projections (tens of tiles per block) keep the general skinny kernel:
     // its 16 waves per CU keep more bytes in flight than one 7-wave block (lm_head 119 vs 194 µs)
-    if (a->N <= 0 || a->N > 32768 || a->ldx % 8 != 0 || a->K >= (1 << 20)) return false;
+    // (tiled weights, which only this kernel reads, take any N whose tiles fit the buffer range)
+    if (a->N <= 0 || (a->N > 32768 && !t16) || a->ldx % 8 != 0 || a->K >= (1 << 20)) return false;
     if (a->epilogue != QIE_EPI_SWIGLU) {
         // column tiles must not straddle segments
         if (a->seg_rows[0] % 16 != 0 || (a->seg_rows[1] > 0 && (a->seg_rows[0] + a->seg_rows[1]) % 16 != 0))
+            return false;
+    }
+    // tiled weights: whole 16-row tiles per segment
+    if (t16) {
+        if (a->epilogue == QIE_EPI_SWIGLU ? a->N % 16 != 0
+                                          : (a->seg_rows[0] % 16 != 0 || a->seg_rows[1] % 16 != 0 || a->seg_rows[2] % 16 != 0))
             return false;
     }
     // every segment's codes + scales must fit a 32-bit buffer range
@@ -821,6 +837,7 @@ bool dec8_applies(const qie_linear_args* a) {
 int dec8_linear(const qie_linear_args* a, hipStream_t st, bool* done) {
     *done = true;
     QIE_REQUIRE(dec8_applies(a), "qie_linear: internal: fp8 batched-decode path does not apply");
+    const bool t16 = (a->flags & QIE_LINEAR_FP8_T16) != 0;
     Dec8Params p;
     p.x = (const uint16_t*)a->x;
     p.ldx = a->ldx;
@@ -864,13 +881,21 @@ int dec8_linear(const qie_linear_args* a, hipStream_t st, bool* done) {
             *done = false;
             return 0;
         }
-        return ku == 4 ? dec8_epi_split<4, 8>(p, a->epilogue, st) : dec8_epi_split<8, 8>(p, a->epilogue, st);
+        if (t16) return ku == 4 ? dec8_epi_split<4, 8, true>(p, a->epilogue, st) : dec8_epi_split<8, 8, true>(p, a->epilogue, st);
+        return ku == 4 ? dec8_epi_split<4, 8, false>(p, a->epilogue, st) : dec8_epi_split<8, 8, false>(p, a->epilogue, st);
     }
-    if (ku == 8 && ks == 7) return dec8_epi<8, 7>(p, a->epilogue, st);
-    if (ku == 8 && ks == 8) return dec8_epi<8, 8>(p, a->epilogue, st);
-    if (ku == 2 && ks == 7) return dec8_epi<2, 7>(p, a->epilogue, st);
-    if (ku == 4 && ks == 8) return dec8_epi<4, 8>(p, a->epilogue, st);
-    return dec8_epi<8, 4>(p, a->epilogue, st);
+    if (t16) {
+        if (ku == 8 && ks == 7) return dec8_epi<8, 7, true>(p, a->epilogue, st);
+        if (ku == 8 && ks == 8) return dec8_epi<8, 8, true>(p, a->epilogue, st);
+        if (ku == 2 && ks == 7) return dec8_epi<2, 7, true>(p, a->epilogue, st);
+        if (ku == 4 && ks == 8) return dec8_epi<4, 8, true>(p, a->epilogue, st);
+        return dec8_epi<8, 4, true>(p, a->epilogue, st);
+    }
+    if (ku == 8 && ks == 7) return dec8_epi<8, 7, false>(p, a->epilogue, st);
+    if (ku == 8 && ks == 8) return dec8_epi<8, 8, false>(p, a->epilogue, st);
+    if (ku == 2 && ks == 7) return dec8_epi<2, 7, false>(p, a->epilogue, st);
+    if (ku == 4 && ks == 8) return dec8_epi<4, 8, false>(p, a->epilogue, st);
+    return dec8_epi<8, 4, false>(p, a->epilogue, st);
 }
 
 }  // namespace qie

@@ -700,6 +700,287 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmParams p, int n_mt, G8Sp
     }
 }
 
+// Stream-K form of gemm8 (one workgroup per CU, a fixed grid).  Tile quantisation costs the
+// one-tile-per-workgroup kernel whole rounds: gate/up at 2,048 rows has 1,184 tiles = 4.625
+// rounds of 256 (the fifth round 62 % busy), QKV 144 tiles (one round, 56 % busy), down 112
+// (split-K 2: 224 of 256 CUs).  Here the work is (tile, k-tile) units: the first
+// dp_rounds * grid tiles go whole, one per workgroup per round; the k-tile units of the
+// remaining tiles are cut into `grid` contiguous ranges of `chunk` units (tile-major, so a
+// range is a tail of one tile, whole tiles, the head of another).  A tile covered by one
+// range is finished in place; a tile shared by several ranges (its SEGMENTS) is finished by
+// the last-arriving segment (ticket), which sums every segment's fp32 slab in SEGMENT order
+// (k order; independent of arrival order) and runs the epilogue.  A workgroup's only
+// partial segments are its range's first and last: slab [workgroup][first / last].
+struct G8Stream {
+    int dp_rounds;     // whole-tile rounds: tile r * grid + w for r < dp_rounds
+    int tiles;         // all tiles; stream-K covers [dp_rounds * grid, tiles)
+    int chunk;         // k-tile units per stream-K range
+    float* slab;       // [grid][2][256 * 256] fp32
+    unsigned* cnt;     // [tiles], zero at rest
+};
+
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm8sk_kernel(GemmParams p, int n_mt, G8Stream sk) {
+#pragma clang fp contract(off)
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    const int fr = lane & 15, g = lane >> 4;
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    // XCD-major workgroup index: consecutive indices (consecutive tiles, which share a weight
+    // tile) sit on one XCD's L2
+    const int q8 = nwg >> 3, r8 = nwg & 7, xcd = orig & 7;
+    const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+    const int nk_all = (int)(p.K / g8::BK);
+
+    int64_t m0 = 0, nt = 0;
+    const uint16_t* src[4][2];
+    int dst_row[4][2];
+    auto set_tile = [&](int tile) {
+        const int64_t mt = tile % n_mt;
+        nt = tile / n_mt;
+        m0 = mt * g8::BM;
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                const int b = 2 * wave + i;
+                int row0;
+                if (u == 0 || u == 3) row0 = (b < 8 ? 8 * b : 128 + 8 * (b - 8)) + (u == 3 ? 64 : 0);
+                else row0 = 64 * (b >> 2) + 8 * (b & 3) + (u == 2 ? 32 : 0);
+                dst_row[u][i] = row0;
+                const int r = row0 + (lane >> 3);
+                const int cs = (lane & 7) ^ g8_swz(r);
+                if (u == 0 || u == 3) {
+                    int64_t ar = m0 + r;
+                    ar = ar < p.M ? ar : p.M - 1;
+                    src[u][i] = p.A + ar * p.lda + cs * 8;
+                } else {
+                    src[u][i] = big_wrow<EPI, 256>(p, nt, r) + cs * 8;
+                }
+            }
+    };
+    int kb = 0;
+    auto stage = [&](int u, int kt) {
+        unsigned char* buf = smem + (kt & 1) * g8::BUF + ((u == 0 || u == 3) ? 0 : g8::BM * 128);
+        const int64_t k0 = (int64_t)(kb + kt) * g8::BK;
+#pragma unroll
+        for (int i = 0; i < 2; i++) glds16(src[u][i] + k0, buf + dst_row[u][i] * 128);
+    };
+
+    f32x4 acc[8][4];
+    bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
+    auto read_a = [&](const unsigned char* buf, int qa) {
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; s2++) {
+                const int row = 128 * wm + 64 * qa + 16 * i + fr;
+                fa[i][s2] = *reinterpret_cast<const bf16x8*>(buf + row * 128 + (((4 * s2 + g) ^ g8_swz(row)) * 16));
+            }
+    };
+    auto read_b = [&](const unsigned char* buf, int qb, bf16x8 (&fb)[2][2]) {
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; s2++) {
+                const int row = 64 * wn + 32 * qb + 16 * j + fr;
+                fb[j][s2] = *reinterpret_cast<const bf16x8*>(buf + g8::BM * 128 + row * 128 +
+                                                             (((4 * s2 + g) ^ g8_swz(row)) * 16));
+            }
+    };
+    auto mfma_q = [&](int qa, int qb, const bf16x8 (&fb)[2][2]) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; s2++)
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < 2; j++)
+                    acc[4 * qa + i][2 * qb + j] =
+                        __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s2], fb[j][s2], acc[4 * qa + i][2 * qb + j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto bar = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto wait8 = [&](bool tail) {
+        if (tail) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    };
+
+    // k-tiles [kb_, kb_ + nk) of the current tile into acc (gemm8_kernel's main loop)
+    auto run = [&](int kb_, int nk) {
+        kb = kb_;
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        stage(0, 0); stage(1, 0); stage(2, 0); stage(3, 0);
+        if (nk > 1) {   // uniform
+            stage(0, 1); stage(1, 1);
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        bar();
+        if (wm == 1) bar();
+        for (int t = 0; t < nk; t++) {
+            const unsigned char* buf = smem + (t & 1) * g8::BUF;
+            const bool tail = t >= nk - 2;
+            read_b(buf, 0, fb0);
+            __builtin_amdgcn_sched_barrier(0);
+            read_a(buf, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (t + 1 < nk) stage(2, t + 1);
+            wait8(tail);
+            bar();
+            mfma_q(0, 0, fb0);
+            bar();
+            read_b(buf, 1, fb1);
+            __builtin_amdgcn_sched_barrier(0);
+            if (t + 1 < nk) stage(3, t + 1);
+            wait8(tail);
+            bar();
+            mfma_q(0, 1, fb1);
+            bar();
+            read_a(buf, 1);
+            __builtin_amdgcn_sched_barrier(0);
+            if (t + 2 < nk) stage(0, t + 2);
+            bar();
+            mfma_q(1, 1, fb1);
+            bar();
+            if (t + 2 < nk) stage(1, t + 2);
+            wait8(tail);
+            bar();
+            mfma_q(1, 0, fb0);
+            bar();
+        }
+        if (wm == 0) bar();
+    };
+
+    auto epilogue = [&]() {
+        constexpr int NJ = 4;
+        if constexpr (EPI == QIE_EPI_SWIGLU) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+#pragma unroll
+                for (int jj = 0; jj < NJ / 2; jj++) {
+                    const int64_t col = nt * 128 + 32 * wn + 16 * jj + fr;
+                    if (col >= p.N) continue;
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const int64_t row = m0 + wm * 128 + i * 16 + g * 4 + r;
+                        if (row >= p.M) continue;
+                        const float gg = rbf(acc[i][jj][r]);
+                        const float uu = rbf(acc[i][jj + NJ / 2][r]);
+                        const float av = rbf(gg * (1.0f / (1.0f + expf(-gg))));
+                        p.C[row * p.ldc + col] = f2bf(uu * av);
+                    }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < NJ; j++) {
+                const int64_t col = nt * 256 + wn * 64 + j * 16 + fr;
+                if (col >= p.N) continue;
+                float bias = 0.f;
+                if constexpr (EPI == QIE_EPI_STORE) {
+                    const uint16_t* b = col < p.n0 ? p.b0 : (col < p.n01 ? p.b1 : p.b2);
+                    if (b) bias = bf2f(b[col < p.n0 ? col : (col < p.n01 ? col - p.n0 : col - p.n01)]);
+                }
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const int64_t row = m0 + wm * 128 + i * 16 + g * 4 + r;
+                        if (row >= p.M) continue;
+                        if constexpr (EPI == QIE_EPI_F32) {
+                            reinterpret_cast<float*>(p.C)[row * p.ldc + col] = acc[i][j][r];
+                            continue;
+                        }
+                        uint16_t* dst = p.C + row * p.ldc + col;
+                        if constexpr (EPI == QIE_EPI_RESIDUAL)
+                            *dst = f2bf(bf2f(*dst) + rbf(acc[i][j][r]));
+                        else
+                            *dst = f2bf(acc[i][j][r] + bias);
+                    }
+                }
+            }
+        }
+    };
+
+    // ---- whole tiles
+    for (int r = 0; r < sk.dp_rounds; r++) {
+        set_tile(r * nwg + wid);
+        run(0, nk_all);
+        epilogue();
+        __syncthreads();   // the next tile's DMA reuses the buffers
+    }
+    // ---- stream-K ranges
+    const int64_t base = (int64_t)sk.dp_rounds * nwg * nk_all;
+    const int64_t total = (int64_t)sk.tiles * nk_all;
+    const int64_t ustart = base + (int64_t)wid * sk.chunk;
+    const int64_t uend = ustart + sk.chunk < total ? ustart + sk.chunk : total;
+    for (int64_t u = ustart; u < uend;) {   // uniform
+        const int tile = (int)(u / nk_all);
+        const int k0 = (int)(u % nk_all);
+        const int k1 = (int)(uend - u < (int64_t)(nk_all - k0) ? k0 + (uend - u) : nk_all);
+        set_tile(tile);
+        run(k0, k1 - k0);
+        bool emit = true;
+        if (k0 != 0 || k1 != nk_all) {   // uniform: a shared tile
+            const int slot = u == ustart ? 0 : 1;
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc(sk.slab + ((int64_t)wid * 2 + slot) * 65536, (short)0,
+                                                              65536 * 4, 0x00020000);
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_g8, acc[i][j]), rs,
+                                                           ((wave * 32 + i * 4 + j) * 64 + lane) * 16, 0, 16);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
+            __syncthreads();
+            // the tile's segments: ranges wf..wl
+            const int64_t tu0 = (int64_t)tile * nk_all - base;
+            const int wf = (int)(tu0 / sk.chunk), wl = (int)((tu0 + nk_all - 1) / sk.chunk);
+            int* flag = reinterpret_cast<int*>(smem);
+            if (tid == 0) {
+                const unsigned old = __hip_atomic_fetch_add(sk.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                *flag = old == (unsigned)(wl - wf) ? 1 : 0;
+            }
+            __syncthreads();
+            emit = *flag != 0;
+            if (emit) {
+                for (int w2 = wf; w2 <= wl; w2++) {   // segment (k) order
+                    const int64_t s2 = base + (int64_t)w2 * sk.chunk;
+                    const int slot2 = s2 / nk_all == tile ? 0 : 1;
+                    const auto rq = __builtin_amdgcn_make_buffer_rsrc(sk.slab + ((int64_t)w2 * 2 + slot2) * 65536,
+                                                                      (short)0, 65536 * 4, 0x00020000);
+#pragma unroll
+                    for (int i = 0; i < 8; i++)
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                          rq, ((wave * 32 + i * 4 + j) * 64 + lane) * 16, 0, 16));
+                            acc[i][j] = w2 == wf ? v : acc[i][j] + v;
+                        }
+                }
+                if (tid == 0) __hip_atomic_store(sk.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        if (emit) epilogue();
+        u += k1 - k0;
+        __syncthreads();
+    }
+}
+
 template <int EPI>
 static int launch_gemm8_t(const GemmParams& p, int n_mt, int n_tiles, const G8Split& sk, hipStream_t st) {
     const void* fn = (const void*)gemm8_kernel<EPI>;
@@ -730,27 +1011,64 @@ struct G8Ws {
 static std::mutex g8_mu;
 static std::map<hipStream_t, G8Ws> g8_ws;
 
-static int g8_workspace(hipStream_t st, int tiles, int splitk, G8Split* out) {
+static int g8_workspace(hipStream_t st, int slabs, int tiles, G8Split* out) {
     std::lock_guard<std::mutex> lk(g8_mu);
     G8Ws& w = g8_ws[st];
-    const size_t need = (size_t)tiles * splitk * 65536 * 4;
+    const size_t need = (size_t)slabs * 65536 * 4;
     if (need > w.slab_bytes || (size_t)tiles > w.cnt_n) {
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return 1;   // no split
         QIE_HIP(hipStreamSynchronize(st));
+        const size_t sb = std::max(need, w.slab_bytes), cn = std::max((size_t)tiles, w.cnt_n);   // never shrink
         if (w.slab) hipFree(w.slab);
         if (w.cnt) hipFree(w.cnt);
         w = G8Ws{};
-        QIE_HIP(hipMalloc((void**)&w.slab, need));
-        QIE_HIP(hipMalloc((void**)&w.cnt, (size_t)tiles * 4));
-        QIE_HIP(hipMemset(w.cnt, 0, (size_t)tiles * 4));
-        w.slab_bytes = need;
-        w.cnt_n = tiles;
+        QIE_HIP(hipMalloc((void**)&w.slab, sb));
+        QIE_HIP(hipMalloc((void**)&w.cnt, cn * 4));
+        QIE_HIP(hipMemset(w.cnt, 0, cn * 4));
+        w.slab_bytes = sb;
+        w.cnt_n = cn;
     }
     out->slab = w.slab;
     out->cnt = w.cnt;
-    out->splitk = splitk;
     return 0;
+}
+
+template <int EPI>
+static int launch_gemm8sk_t(const GemmParams& p, int n_mt, int grid, const G8Stream& sk, hipStream_t st) {
+    const void* fn = (const void*)gemm8sk_kernel<EPI>;
+    constexpr size_t shm = 2 * (size_t)g8::BUF;
+    static bool raised = false;
+    if (!raised) {
+        QIE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+        raised = true;
+    }
+    hipLaunchKernelGGL((gemm8sk_kernel<EPI>), dim3((unsigned)grid), dim3(512), shm, st, p, n_mt, sk);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+
+// Stream-K plan + workspace (the split-K one: slab [grid][2] tiles, tickets [tiles]);
+// *launched = false: a workspace would have to grow during a graph capture
+static int launch_gemm8sk(int epi, const GemmParams& p, int n_mt, int tiles, hipStream_t st, bool* launched) {
+    *launched = false;
+    const int gk = dev_env("QIE_GEMM8_SK_GRID", 0);   // dev A/B: workgroups (default one per CU)
+    const int grid = gk > 0 ? gk : (int)device_cu_count();
+    const int nk = (int)(p.K / g8::BK);
+    G8Stream sk;
+    sk.tiles = tiles;
+    sk.dp_rounds = tiles / grid;
+    const int64_t rest = (int64_t)(tiles - sk.dp_rounds * grid) * nk;
+    sk.chunk = (int)std::max<int64_t>(1, (rest + grid - 1) / grid);
+    G8Split ws{1, nullptr, nullptr};
+    if (rest > 0 && g8_workspace(st, 2 * grid, tiles, &ws) != 0) return 0;
+    sk.slab = ws.slab;
+    sk.cnt = ws.cnt;
+    *launched = true;
+    if (epi == QIE_EPI_SWIGLU) return launch_gemm8sk_t<QIE_EPI_SWIGLU>(p, n_mt, grid, sk, st);
+    if (epi == QIE_EPI_RESIDUAL) return launch_gemm8sk_t<QIE_EPI_RESIDUAL>(p, n_mt, grid, sk, st);
+    if (epi == QIE_EPI_F32) return launch_gemm8sk_t<QIE_EPI_F32>(p, n_mt, grid, sk, st);
+    return launch_gemm8sk_t<QIE_EPI_STORE>(p, n_mt, grid, sk, st);
 }
 
 // parts per tile: the fewest rounds of (tile, part) items over the CUs, in units of a tile
@@ -849,6 +1167,12 @@ int gemm(const qie_linear_args* a, hipStream_t st) {
         // rows 612 -> 488 us, bit-identical to gemm_big; down split-K 2: 309 -> 247 us
         const bool g8ok = a->K % g8::BK == 0 && a->K >= 4 * g8::BK;
         const int g8mode = dev_env("QIE_GEMM8", 2);   // 2 (default): + split-K below; 1: full-chip grids only; 0: off
+        // stream-K (QIE_GEMM8 = 3; args.flags QIE_LINEAR_STREAMK): any tile count, one workgroup per CU
+        if (g8ok && ((a->flags & QIE_LINEAR_STREAMK) || (g8mode == 3 && force < 0 && a->M >= big::BM))) {
+            bool launched = false;
+            const int rc = launch_gemm8sk(a->epilogue, p, (int)n_mt, (int)t256, st, &launched);
+            if (rc || launched) return rc;
+        }
         if (g8ok && g8mode != 0 && force != 2 && (force == 1 || (force < 0 && a->M >= big::BM && t256 >= cus))) {
             G8Split sk{1, nullptr, nullptr};
             return launch_gemm8(a->epilogue, p, (int)n_mt, (int)t256, sk, st);
@@ -858,7 +1182,7 @@ int gemm(const qie_linear_args* a, hipStream_t st) {
             G8Split sk{1, nullptr, nullptr};
             // unsplit, 256x256 tiles must still cover half the chip: QKV at 144 tiles 101.7 ->
             // 87.8 us, but O at 112 tiles 78 -> 103 us (its 256x128 kernel fills 224 CUs)
-            if ((s == 1 && 2 * t256 >= cus) || (s > 1 && g8_workspace(st, (int)t256, s, &sk) == 0))
+            if ((s == 1 && 2 * t256 >= cus) || (s > 1 && g8_workspace(st, (int)t256 * s, (int)t256, &sk) == 0 && (sk.splitk = s) > 1))
                 return launch_gemm8(a->epilogue, p, (int)n_mt, (int)t256, sk, st);
         }
         if (force == 1 || (force < 0 && a->M >= big::BM && t256 >= cus))

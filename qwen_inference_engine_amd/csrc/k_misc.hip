@@ -863,6 +863,34 @@ int qie_dequantize_fp8(const void* w_fp8, int64_t rows, int64_t cols, void* out_
     return 0;
 }
 
+// plain [rows][cols] fp8 codes -> the 16-row tiled layout (qie_ops.h); one thread per 16-B
+// piece of the output: output piece (t, j, l) <- row 16 t + l % 16, columns 64 j + 16 (l / 16)
+__global__ __launch_bounds__(256) void fp8_tile16_kernel(const uint4* in, int64_t cols16, int64_t units,
+                                                         int64_t n16, uint4* out) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256) {
+        const int64_t l = i & 63, blk = i >> 6;
+        const int64_t t = blk / units, j = blk % units;
+        const int64_t row = 16 * t + (l & 15);
+        out[i] = in[row * cols16 + 4 * j + (l >> 4)];
+    }
+}
+
+int qie_fp8_tile16(const void* w_fp8, int64_t rows, int64_t cols, void* out, void* stream) {
+    QIE_REQUIRE(w_fp8 && out && w_fp8 != out && rows > 0 && rows % 16 == 0 && cols > 0 && cols % 64 == 0 &&
+                    ((uintptr_t)w_fp8 % 16) == 0 && ((uintptr_t)out % 16) == 0,
+                "qie_fp8_tile16: bad arguments (rows %% 16 == 0, cols %% 64 == 0, distinct 16-B aligned buffers)");
+    const int64_t n16 = rows * cols / 16;
+    const unsigned grid = (unsigned)std::min<int64_t>((n16 + 255) / 256, (int64_t)device_cu_count() * 16);
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(fp8_tile16_kernel, dim3(grid), dim3(256), 0, st, (const uint4*)w_fp8, cols / 16, cols / 64, n16,
+                       (uint4*)out);
+    QIE_LAUNCH_CHECK();
+    // the row scales are unchanged
+    QIE_HIP(hipMemcpyAsync((uint8_t*)out + rows * cols, (const uint8_t*)w_fp8 + rows * cols, (size_t)rows * 4,
+                           hipMemcpyDeviceToDevice, st));
+    return 0;
+}
+
 int qie_quantize_fp8_host(const void* w_bf16, int64_t rows, int64_t cols, void* out) {
     QIE_REQUIRE(w_bf16 && out && rows > 0 && cols > 0 && cols % 16 == 0, "qie_quantize_fp8_host: bad arguments");
     const uint16_t* w = (const uint16_t*)w_bf16;

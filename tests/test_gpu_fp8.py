@@ -287,3 +287,119 @@ def test_fp8_batched_decode_long_k(oracle, qlib, M, K, N):
         _linear(qlib, G.dev(h), [(dw, N)], [], M, K, N, yf, _lib.QIE_EPI_F32, flags=_lib.QIE_LINEAR_FP8)
         want = oracle.bf16_to_f32(h).astype(np.float64) @ oracle.bf16_to_f32(qw).astype(np.float64).T
         assert np.abs(G.host(yf) - want).max() <= 1e-5 * _abs_scale(oracle, h, qw).max() + 1e-6
+
+
+def _tile16_host(codes, rows, cols):
+    """qie_ops.h's 16-row tiled layout restated on the host: block (t, j) piece l = row
+    16 t + l % 16, columns 64 j + 16 (l // 16) + [0, 16)."""
+    c = codes[:rows * cols].reshape(rows // 16, 16, cols // 64, 4, 16)   # t, fr, j, g, byte
+    tiled = c.transpose(0, 2, 3, 1, 4).reshape(-1)                       # t, j, g, fr, byte
+    return np.concatenate([tiled, codes[rows * cols:]])
+
+
+@pytest.mark.parametrize("rows,cols", [(16, 64), (48, 896), (512, 3584)])
+def test_fp8_tile16_layout(oracle, qlib, rows, cols):
+    """qie_fp8_tile16 is the documented permutation of the codes, bit for bit; the row scales
+    are copied unchanged."""
+    w = rand_bf16(oracle, (rows, cols), 0.05, seed=rows)
+    d, _ = _fp8_dev(qlib, w)
+    out = G.zeros((d.nbytes,), np.uint8)
+    G.check(qlib.qie_fp8_tile16(G.p(d), rows, cols, G.p(out), None))
+    G.check(qlib.qie_synchronize())
+    assert np.array_equal(G.host(out), _tile16_host(G.host(d), rows, cols))
+
+
+def _tiled(qlib, d, rows, cols):
+    out = G.zeros((d.nbytes,), np.uint8)
+    G.check(qlib.qie_fp8_tile16(G.p(d), rows, cols, G.p(out), None))
+    return out
+
+
+@pytest.mark.parametrize("M", [1, 2, 8, 16])
+@pytest.mark.parametrize("K", [896, 3584])
+def test_fp8_t16_decode_kernel_equals_plain(oracle, qlib, M, K):
+    """The batched-decode kernel on 16-row tiled weights (QIE_LINEAR_FP8_T16, the engine's
+    decode projections) only changes where each fragment is loaded from: its outputs equal
+    the plain-layout kernel's bit for bit (fused norm + 3-segment STORE with biases and
+    arg-max keys, SwiGLU, residual), at M = 1 too (there the plain reference runs at M = 2
+    on a duplicated row: rows are independent)."""
+    Mr = max(M, 2)
+    x = rand_bf16(oracle, (Mr, K), seed=M + K)
+    if M == 1:
+        x[1] = x[0]
+    nw = oracle.f32_to_bf16((1 + 0.2 * rng(12).standard_normal(K)).astype(np.float32))
+    fp8 = _lib.QIE_LINEAR_FP8
+    t16 = fp8 | _lib.QIE_LINEAR_FP8_T16
+    # QKV-shaped, fused norm, biases, arg-max keys
+    n = (512, 128, 128)
+    q = [_fp8_dev(qlib, rand_bf16(oracle, (r, K), 0.05, seed=30 + i))[0] for i, r in enumerate(n)]
+    qt = [_tiled(qlib, d, r, K) for d, r in zip(q, n)]
+    bs = [G.dev(rand_bf16(oracle, (r,), 0.1, seed=40 + i)) for i, r in enumerate(n)]
+    N = sum(n)
+    outs = []
+    for ws, fl, m in ((q, fp8, Mr), (qt, t16, M)):
+        y = G.zeros_bf16(m, N)
+        keys = G.dev(np.zeros(m, np.uint64))
+        _linear(qlib, G.dev(x[:m].copy()), list(zip(ws, n)), bs, m, K, N, y, _lib.QIE_EPI_STORE, norm_w=G.dev(nw),
+                eps=1e-6, num=0, keys=keys, flags=fl)
+        outs.append((G.host_bf16(y)[:M], G.host(keys)[:M]))
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+    # SwiGLU with the fused norm
+    I = 640
+    g_, u_ = (_fp8_dev(qlib, rand_bf16(oracle, (I, K), 0.08, seed=7 + i))[0] for i in range(2))
+    gt, ut = _tiled(qlib, g_, I, K), _tiled(qlib, u_, I, K)
+    outs = []
+    for (a, b), fl, m in (((g_, u_), fp8, Mr), ((gt, ut), t16, M)):
+        y = G.zeros_bf16(m, I)
+        _linear(qlib, G.dev(x[:m].copy()), [(a, I), (b, I)], [], m, K, I, y, _lib.QIE_EPI_SWIGLU, norm_w=G.dev(nw),
+                eps=1e-6, num=0, flags=fl)
+        outs.append(G.host_bf16(y)[:M])
+    assert np.array_equal(outs[0], outs[1])
+    # residual (O-shaped), no norm
+    dw = _fp8_dev(qlib, rand_bf16(oracle, (K, K), 0.02, seed=4))[0]
+    dwt = _tiled(qlib, dw, K, K)
+    res = rand_bf16(oracle, (Mr, K), seed=5)
+    outs = []
+    for w_, fl, m in ((dw, fp8, Mr), (dwt, t16, M)):
+        yr = G.dev(res[:m].copy())
+        _linear(qlib, G.dev(x[:m].copy()), [(w_, K)], [], m, K, K, yr, _lib.QIE_EPI_RESIDUAL, flags=fl)
+        outs.append(G.host_bf16(yr)[:M])
+    assert np.array_equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("M", [1, 8])
+@pytest.mark.parametrize("K,N", [(4864, 896), (18944, 3584)])
+def test_fp8_t16_long_k_equals_plain(oracle, qlib, M, K, N):
+    """Split-K form on tiled weights (the down projection) == the plain-layout split-K form,
+    bit for bit (M = 1 against M = 2 with a duplicated row)."""
+    Mr = max(M, 2)
+    h = rand_bf16(oracle, (Mr, K), seed=K + M)
+    if M == 1:
+        h[1] = h[0]
+    dw = _fp8_dev(qlib, rand_bf16(oracle, (N, K), 0.02, seed=4))[0]
+    dwt = _tiled(qlib, dw, N, K)
+    res = rand_bf16(oracle, (Mr, N), seed=5)
+    outs = []
+    for w_, fl, m in ((dw, _lib.QIE_LINEAR_FP8, Mr), (dwt, _lib.QIE_LINEAR_FP8 | _lib.QIE_LINEAR_FP8_T16, M)):
+        yr = G.dev(res[:m].copy())
+        _linear(qlib, G.dev(h[:m].copy()), [(w_, N)], [], m, K, N, yr, _lib.QIE_EPI_RESIDUAL, flags=fl)
+        outs.append(G.host_bf16(yr)[:M])
+    assert np.array_equal(outs[0], outs[1])
+
+
+def test_fp8_t16_rejected_outside_decode_kernel(qlib):
+    """Tiled weights are readable by the batched-decode kernel only: a prefill-sized call
+    (M > 16) with the flag fails loudly instead of reading them as plain rows."""
+    import ctypes as C
+    from qwen_inference_engine_amd._lib import LinearArgsC
+    K, N, M = 896, 128, 32
+    w = G.zeros((int(qlib.qie_fp8_weight_bytes(N, K)),), np.uint8)
+    a = LinearArgsC()
+    x, y = G.zeros_bf16(M, K), G.zeros_bf16(M, N)
+    a.x, a.ldx = G.p(x), K
+    a.w[0], a.seg_rows[0] = G.p(w), N
+    a.M, a.K, a.N = M, K, N
+    a.y, a.ldy = G.p(y), N
+    a.epilogue = _lib.QIE_EPI_STORE
+    a.flags = _lib.QIE_LINEAR_FP8 | _lib.QIE_LINEAR_FP8_T16
+    assert qlib.qie_linear(C.byref(a), None) != 0

@@ -175,3 +175,28 @@ def test_config4_fp8_batch8_prompt1024(oracle):
         if step + 1 < n_new:
             t_e = b.decode_step()
     assert flips <= max_flips(B * n_new)
+
+
+def test_fp8_tiled_batch1_short_prompt(oracle):
+    """Qwen2-7B widths (2 layers), e4m3 weights at batch 1 with a 12-token prompt: every
+    projection runs the batched-decode kernel on the engine's 16-row tiled weights (prefill
+    of <= 16 rows and the M = 1 decode), against the oracle on the dequantised model."""
+    spec = S.QWEN2_7B.replace(n_layers=2)
+    syn = W.SynthParams(seed=0)
+    P, n_new, max_ctx = 12, 6, 32
+    eng = Q.Engine(spec, max_ctx=max_ctx, weight_fp8=True).init_synthetic(syn)
+    b = eng.batch(1, max_ctx)
+    hw = W.HostWeights.synthetic(spec, syn).fp8_dequantized()
+    prompt = [int(t) for t in rng(77).integers(0, spec.vocab, P)]
+    om = OrderPair(oracle, hw, max_ctx)
+    ids, outs = oracle_trace(oracle, om, prompt, n_new)
+    t = b.prefill(0, prompt)
+    flips = 0
+    for step in range(n_new):
+        lg0 = outs[step][0]
+        flips += check_step(b.logits()[0], lg0, om, t, ids[step], f"step {step}")
+        if t != ids[step]:
+            b.set_position(0, P + step, ids[step])
+        if step + 1 < n_new:
+            t = b.decode_step()[0]
+    assert flips <= max_flips(n_new)

@@ -134,12 +134,14 @@ def test_linear_swiglu(oracle, qlib, M, K, I):
 
 @pytest.mark.parametrize("M,K", [(256, 896), (300, 96), (520, 32), (257, 3584)])
 @pytest.mark.parametrize("epi", ["store3", "residual", "swiglu", "f32"])
-@pytest.mark.parametrize("tile", ["1", "2"])
+@pytest.mark.parametrize("tile", ["1", "2", "sk"])
 def test_linear_big_gemm(oracle, qlib, M, K, epi, tile):
     """The LDS-DMA prefill GEMM, 256x256 (QIE_LINEAR_TILE256) and 256x128 (QIE_LINEAR_TILE128)
     tiles, forced at test sizes (the engine picks them by tile count): every epilogue, ragged
-    M and N (clamped rows never stored), K of 1, 3 and 28+ k-tiles (ring prologue / drain)."""
-    fl = _lib.QIE_LINEAR_TILE256 if tile == "1" else _lib.QIE_LINEAR_TILE128
+    M and N (clamped rows never stored), K of 1, 3 and 28+ k-tiles (ring prologue / drain);
+    "sk" the stream-K form (QIE_LINEAR_STREAMK, K % 64 == 0 and >= 256 only): at these sizes
+    every workgroup gets ONE k-tile, so each tile is summed from 14 or 56 segments."""
+    fl = {"1": _lib.QIE_LINEAR_TILE256, "2": _lib.QIE_LINEAR_TILE128, "sk": _lib.QIE_LINEAR_STREAMK}[tile]
     x = rand_bf16(oracle, (M, K), seed=M + K)
     if epi == "store3":
         n = (200, 72, 40)

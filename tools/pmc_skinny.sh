@@ -1,5 +1,5 @@
 #!/bin/bash
-# Stall counters of the batch-8 skinny MFMA GEMM (config 4, fp8): tools/ubench_b8.py under
+# Stall counters of the batch-8 decode projections (config 4, fp8: dec8 / skinny kernels): tools/ubench_b8.py under
 # two rocprofv3 --pmc passes (one run each, never combined with trace domains).
 set -u
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -22,7 +22,7 @@ cnt = collections.Counter()
 for f in glob.glob("gpurun_out/pmc_sk*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        if "skinny" not in k and "gemv_kernel" not in k:
+        if "skinny" not in k and "gemv_kernel" not in k and "dec8" not in k:
             continue
         k = k.split("(")[0][:70]
         tot[k][r["Counter_Name"]] += float(r["Counter_Value"])

@@ -11,7 +11,8 @@ only reorders work must reproduce them bit for bit; one that changes numerics ma
 
 Env: AB_MODEL (Qwen2-7B), AB_P (2048), AB_STEPS (256), AB_ROUNDS (3), AB_BATCH (1),
 AB_FP8 (0), AB_KERNELS (1: also the live per-kernel timings), AB_PREFILL (0: also time one
-prefill per variant)."""
+prefill per variant), AB_ENGINE (0; 1: a fresh engine per variant and round, for knobs read
+when the weights are loaded, e.g. QIE_FP8_T16)."""
 import json
 import os
 import sys
@@ -38,7 +39,8 @@ def main():
     do_pf = os.environ.get("AB_PREFILL", "0") == "1"
     variants = json.loads(os.environ.get("AB_VARIANTS", "[{}]"))
     max_ctx = P + steps + 64
-    eng = Q.Engine(spec, max_ctx=max_ctx, weight_fp8=fp8).init_synthetic(W.SynthParams(seed=0))
+    per_engine = os.environ.get("AB_ENGINE", "0") == "1"
+    eng = None if per_engine else Q.Engine(spec, max_ctx=max_ctx, weight_fp8=fp8).init_synthetic(W.SynthParams(seed=0))
     prompts = np.random.default_rng(1).integers(0, spec.vocab, size=(B, P), dtype=np.int32)
     res = {i: {"tok_s": [], "prefill_ms": [], "kern": {}} for i in range(len(variants))}
     ids_ref = None
@@ -48,6 +50,8 @@ def main():
             saved = {k: os.environ.get(k) for k in env}
             os.environ.update({k: str(v) for k, v in env.items()})
             try:
+                if per_engine:
+                    eng = Q.Engine(spec, max_ctx=max_ctx, weight_fp8=fp8).init_synthetic(W.SynthParams(seed=0))
                 b = eng.batch(B, max_ctx)
                 first = b.prefill_batch(0, prompts) if B > 1 else [b.prefill(0, prompts[0])]
                 if do_pf:
@@ -75,6 +79,9 @@ def main():
                         us, _ = b.time_kernel(w, 54)
                         res[i]["kern"].setdefault(name, []).append(us)
                 b.close()
+                if per_engine:
+                    eng.close()
+                    eng = None
             finally:
                 for k, v in saved.items():
                     if v is None:

@@ -33,6 +33,8 @@ ROLE = {
     "gemv_kernel<1, 2, 2, 7, 4, 0, 256> [g 512 x 256]": "decode gate/up GEMV (+RMSNorm in registers, SwiGLU), full-residency grid  [dominant]",
     "gemm8_kernel<2>": "prefill gate/up GEMM (phase-interleaved 256x256, SwiGLU)",
     "gemm8_kernel<1>": "prefill down GEMM (phase-interleaved 256x256, split-K 2, +residual)",
+    "gemm8_kernel<0>": "prefill QKV GEMM (phase-interleaved 256x256, +bias)",
+    "attn_decode_mfma2_kernel<128, false, 4, false, 128>": "decode attention (fused RoPE/KV append, speculative K/V step, split-K, in-launch combine)",
     "dec8r_kernel<2, 8, 7, 8>": "fp8 decode gate/up, A in LDS + 4-step ring  [dominant]",
     "dec8r_kernel<0, 8, 7, 8>": "fp8 decode QKV, A in LDS + 4-step ring",
     "dec8r_kernel<1, 8, 7, 8>": "fp8 decode O-proj, A in LDS + 4-step ring",
@@ -49,6 +51,14 @@ ROLE = {
     "rmsnorm_reg_kernel<2>": "final RMSNorm (batch head) / prefill RMSNorm",
     "gemm_kernel<1, 0>": "prefill O / down GEMM (128x128 tiles, +residual)",
     "quantize_fp8_kernel": "fp8 weight quantisation (setup)",
+    # round 4, config 4 on 16-row tiled fp8 weights (dec8_kernel<EPI, KU, KS, split-K, tiled>)
+    "dec8_kernel<2, 8, 7, false, true>": "fp8 decode gate/up (+fused RMSNorm, SwiGLU), tiled weights  [dominant]",
+    "dec8_kernel<0, 8, 7, false, true>": "fp8 decode QKV (+fused RMSNorm, bias), tiled; bench live timing of O (store)",
+    "dec8_kernel<1, 8, 7, false, true>": "fp8 decode O-proj (+residual), tiled weights",
+    "dec8_kernel<1, 4, 8, true, true>": "fp8 decode down (+residual), split-K 10 x (8 waves x 4 units), tiled",
+    "dec8_kernel<0, 4, 8, true, true>": "bench live timing of down (store epilogue)",
+    "fp8_tile16_kernel": "fp8 16-row tiling of the decode projections (setup)",
+    "gemm_big_kernel<1, 128> [g 224 x 512]": "prefill O GEMM (256x128 LDS-DMA, one round of 224 tiles, +residual)",
     "dequantize_fp8_kernel": "fp8 -> bf16 prefill copy (setup)",
 }
 
@@ -147,4 +157,6 @@ def main(tag="r01", src="gpurun_out/prof", desc=HEADLINE, how="tools/gpu_check.s
 
 
 if __name__ == "__main__":
+    if any(x.startswith("-") for x in sys.argv[1:]):
+        sys.exit("usage: tools/prof_summary.py TAG [SRC_DIR] [DESCRIPTION] [HOW]")
     main(*sys.argv[1:])

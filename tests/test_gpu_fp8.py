@@ -403,3 +403,57 @@ def test_fp8_t16_rejected_outside_decode_kernel(qlib):
     a.epilogue = _lib.QIE_EPI_STORE
     a.flags = _lib.QIE_LINEAR_FP8 | _lib.QIE_LINEAR_FP8_T16
     assert qlib.qie_linear(C.byref(a), None) != 0
+
+
+@pytest.mark.parametrize("M", [2, 16])
+@pytest.mark.parametrize("tiled", [False, True])
+def test_fp8_batched_decode_many_tiles_per_block(oracle, qlib, M, tiled):
+    """The batched-decode kernel with several column tiles per block (more tiles than
+    resident blocks): the multi-tile loop, the double-buffered partial-tile hand-off and the
+    rotating epilogue wave.  Config-4 shapes: SwiGLU I = 18,944 and the QKV-shaped 3-segment
+    STORE (N = 4,608) at K = 3,584 with the fused norm; the 8-wave slice shapes K = 2,048 and
+    4,096 (STORE, N = 8,192); plain and 16-row tiled weights, against the oracle on the
+    dequantised weights (test_fp8_batched_decode_kernel's bars)."""
+    fl = _lib.QIE_LINEAR_FP8 | (_lib.QIE_LINEAR_FP8_T16 if tiled else 0)
+
+    def dev_w(rows, K, scale, seed):
+        d, dq = _fp8_dev(qlib, rand_bf16(oracle, (rows, K), scale, seed=seed))
+        return (_tiled(qlib, d, rows, K) if tiled else d), dq
+
+    K = 3584
+    x = rand_bf16(oracle, (M, K), seed=90 + M)
+    nw = oracle.f32_to_bf16((1 + 0.2 * rng(13).standard_normal(K)).astype(np.float32))
+    xn = oracle.rmsnorm(x, nw, 1e-6, "ref")
+    # SwiGLU, I = 18,944 (1,184 tiles)
+    I = 18944
+    (dg, qg), (du, qu) = dev_w(I, K, 0.08, 7), dev_w(I, K, 0.08, 8)
+    y = G.zeros_bf16(M, I)
+    _linear(qlib, G.dev(x), [(dg, I), (du, I)], [], M, K, I, y, _lib.QIE_EPI_SWIGLU, norm_w=G.dev(nw), eps=1e-6,
+            num=0, flags=fl)
+    # the fused norm may round an element 1 ulp off the oracle's rows (test_fp8_batched_decode_kernel):
+    # the SwiGLU bar is the conditioning-aware one of test_linear_swiglu
+    want = oracle.silu_mul(oracle.matmul(xn, qg), oracle.matmul(xn, qu))
+    d = G.ulp_diff(G.host_bf16(y), want)
+    gs = G.bf(oracle.matmul(xn, qg)).astype(np.float64)
+    u = np.abs(G.bf(oracle.matmul(xn, qu)).astype(np.float64))
+    ill = (np.abs(gs) < 1e-2 * _abs_scale(oracle, xn, qg)) | (u < 1e-2 * _abs_scale(oracle, xn, qu)) | (gs < -4)
+    assert (d == 0).mean() > 0.9 and not ((d > 4) & ~ill).any()
+    # QKV-shaped, N = 4,608 (288 tiles), biases
+    n = (3584, 512, 512)
+    q = [dev_w(r, K, 0.05, 30 + i) for i, r in enumerate(n)]
+    bs = [rand_bf16(oracle, (r,), 0.1, seed=40 + i) for i, r in enumerate(n)]
+    N = sum(n)
+    y = G.zeros_bf16(M, N)
+    _linear(qlib, G.dev(x), [(dd, r) for (dd, _), r in zip(q, n)], [G.dev(b) for b in bs], M, K, N, y,
+            _lib.QIE_EPI_STORE, norm_w=G.dev(nw), eps=1e-6, num=0, flags=fl)
+    want = np.concatenate([oracle.matmul(xn, dq, b) for (_, dq), b in zip(q, bs)], axis=1)
+    scale = np.concatenate([_abs_scale(oracle, xn, dq) for _, dq in q], axis=1)
+    G.assert_sum_close(G.host_bf16(y), want, scale, ulps=2, what=f"fp8 dec8 qkv N={N} M={M}")
+    # 8-wave slice shapes, 512 tiles
+    for K2 in (2048, 4096):
+        x2 = rand_bf16(oracle, (M, K2), seed=K2 + M)
+        N2 = 8192
+        dw, qw = dev_w(N2, K2, 0.03, K2)
+        y = G.zeros_bf16(M, N2)
+        _linear(qlib, G.dev(x2), [(dw, N2)], [], M, K2, N2, y, _lib.QIE_EPI_STORE, flags=fl)
+        G.assert_sum_close(G.host_bf16(y), oracle.matmul(x2, qw), _abs_scale(oracle, x2, qw), what=f"fp8 dec8 K={K2}")

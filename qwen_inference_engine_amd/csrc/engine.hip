@@ -375,10 +375,13 @@ static int quantize_weights_fp8(qie_engine* e, bool own_arena) {
         };
         const bool all = ok(H, QD + 2 * KD, QD, KD, KD, true, QIE_EPI_STORE) && ok(QD, H, H, 0, 0, false, QIE_EPI_RESIDUAL) &&
                          ok(H, I, I, I, 0, true, QIE_EPI_SWIGLU) && ok(I, H, H, 0, 0, false, QIE_EPI_RESIDUAL);
-        // the vocabulary projection stays plain for the general skinny kernel: tiled, through
-        // this kernel (one 7-wave block per CU, ~37 tiles each), config 4's lm_head took 168.9
-        // vs 119-120 µs (dev QIE_FP8_T16_HEAD=1 tiles it; its readers are <= 8-row heads)
-        const bool head = all && dev_env("QIE_FP8_T16_HEAD", 0) != 0 && ok(H, V, V, 0, 0, true, QIE_EPI_STORE);
+        // the vocabulary projection too: its readers (the decode step's and the prefill's
+        // last-row heads, <= 8 rows) run the skinny kernel, which reads the tiled layout
+        // (through the batched-decode kernel instead — one 7-wave block per CU, ~37 tiles
+        // each — config 4's lm_head took 168.9 vs 119-120 µs plain); dev QIE_FP8_T16_HEAD=0
+        // keeps it plain
+        const bool head = all && dev_env("QIE_FP8_T16_HEAD", 1) != 0 && H % 64 == 0 && V % 16 == 0 &&
+                          (size_t)8 * (H + 8) * 2 <= 120 * 1024;
         if (all) {
             size_t big = 0;
             for (auto& t : ts)
@@ -1598,9 +1601,13 @@ int qie_linear(const qie_linear_args* a, void* stream) {
     QIE_REQUIRE(a->epilogue != QIE_EPI_F32 || (a->bias[0] == nullptr && a->bias[1] == nullptr && a->bias[2] == nullptr),
                 "qie_linear: F32 (partial-sum) epilogue takes no bias");
     QIE_REQUIRE(a->argmax_keys == nullptr || a->epilogue == QIE_EPI_STORE, "qie_linear: arg-max needs STORE");
-    QIE_REQUIRE(!(a->flags & QIE_LINEAR_FP8_T16) || ((a->flags & QIE_LINEAR_FP8) && dec8_applies(a)),
-                "qie_linear: 16-row tiled fp8 weights are read by the batched-decode kernel only (M <= 16, K %% 64 == 0, "
-                "segments of whole 16-row tiles, N <= 32768)");
+    QIE_REQUIRE(!(a->flags & QIE_LINEAR_FP8_T16) ||
+                    ((a->flags & QIE_LINEAR_FP8) && a->M >= 1 && a->M <= 16 && a->K % 64 == 0 &&
+                     (a->epilogue == QIE_EPI_SWIGLU ? a->N % 16 == 0
+                                                    : a->seg_rows[0] % 16 == 0 && a->seg_rows[1] % 16 == 0 &&
+                                                          a->seg_rows[2] % 16 == 0)),
+                "qie_linear: 16-row tiled fp8 weights are read by the batched-decode kernels only (M <= 16, K %% 64 == 0, "
+                "segments of whole 16-row tiles)");
     hipStream_t st = (hipStream_t)stream;
     if (a->M <= 16) return gemv(a, st);   // GEMV (M = 1..8) or the skinny MFMA kernel (2..16)
     return gemm(a, st);

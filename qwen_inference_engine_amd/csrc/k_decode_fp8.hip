@@ -812,8 +812,8 @@ bool dec8_applies(const qie_linear_args* a) {
     if (!dec8_shape(a->K, &ku, &ks) && dec8_split_parts(a, &ku) == 0) return false;
     // vocabulary-sized projections (tens of tiles per block) keep the general skinny kernel:
     // its 16 waves per CU keep more bytes in flight than one 7-wave block (lm_head 119 vs 194 µs)
-    // (tiled weights, which only this kernel reads, take any N whose tiles fit the buffer range)
-    if (a->N <= 0 || (a->N > 32768 && !t16) || a->ldx % 8 != 0 || a->K >= (1 << 20)) return false;
+    // (tiled vocabulary projections go to the skinny kernel, which reads the layout too)
+    if (a->N <= 0 || a->N > 32768 || a->ldx % 8 != 0 || a->K >= (1 << 20)) return false;
     if (a->epilogue != QIE_EPI_SWIGLU) {
         // column tiles must not straddle segments
         if (a->seg_rows[0] % 16 != 0 || (a->seg_rows[1] > 0 && (a->seg_rows[0] + a->seg_rows[1]) % 16 != 0))

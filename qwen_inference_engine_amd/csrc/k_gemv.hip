@@ -58,6 +58,7 @@ struct GemvParams {
     int64_t rope_rows;
     int epre;          // M = 1: the first task's epilogue operands (bias / residual) loaded up front
     int mkdiv;         // x-first fused norm: REF quotient by the FMA-corrected reciprocal (dev A/B)
+    int t16;           // skinny kernel, fp8: weights in the 16-row tiled layout (qie_fp8_tile16)
 };
 
 // REF RMSNorm quotient f / rms: the FMA-corrected product with the reciprocal (Markstein),
@@ -802,9 +803,12 @@ __global__ __launch_bounds__(NW * 64) void skinny_mfma_kernel(GemvParams p) {
         const int64_t n = st.tile * 16 + fr;
         const int64_t nc = n < p.N ? n : p.N - 1;
         const uint8_t* wrow[NB];
+        const uint8_t* wseg[NB];   // segment bases (the 16-row tiled fp8 layout)
         const float* scp[NB];
         int64_t r = nc;    // row within the column's segment
         if constexpr (NB == 2) {
+            wseg[0] = wbase;
+            wseg[1] = wbase + dw1;
             wrow[0] = wbase + nc * K * EB;
             wrow[1] = wbase + dw1 + nc * K * EB;
             scp[0] = reinterpret_cast<const float*>(wbase + p.N * K) + nc;
@@ -818,6 +822,7 @@ __global__ __launch_bounds__(NW * 64) void skinny_mfma_kernel(GemvParams p) {
             const uint8_t* wb = wbase + ((dw1 & m1) | (dw2 & m2));
             (void)m0;
             const int64_t rows = s0 ? p.n0 : (s1 ? p.n01 - p.n0 : p.N - p.n01);
+            wseg[0] = wb;
             wrow[0] = wb + r * K * EB;
             scp[0] = reinterpret_cast<const float*>(wb + rows * K) + r;
         }
@@ -840,15 +845,31 @@ __global__ __launch_bounds__(NW * 64) void skinny_mfma_kernel(GemvParams p) {
             const uint16_t v = *(reinterpret_cast<const uint16_t*>(bb) + (r & (int64_t)hb));
             st.ep[0] = __uint_as_float((uint32_t)hb & __float_as_uint(bf2f(v)));
         }
+        // fp8: lane (fr, g)'s 16 codes of unit uu — plain rows: bytes uu * 64 + 16 g of its row;
+        // 16-row tiled (p.t16): bytes (fr + 16 g) * 16 of the unit's 1-KiB block, so one load
+        // instruction reads 8 whole lines instead of 16 rows x 64 B (tiles start at segment
+        // starts; a clamped row past N stays inside its segment's last tile)
+        const uint8_t* lb[NB];
+        int64_t ls = KSTEP * EB;
+        if constexpr (WT != 0) {
+#pragma unroll
+            for (int b = 0; b < NB; b++)
+                lb[b] = p.t16 ? wseg[b] + (r >> 4) * 16 * K + ((r & 15) + 16 * g) * 16 : wrow[b] + 16 * g;
+            ls = p.t16 ? 1024 : KSTEP;
+        }
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int64_t uu = st.u0 + u < ue ? st.u0 + u : ue - 1;
 #pragma unroll
             for (int b = 0; b < NB; b++)   // bytes [uu * KSTEP * EB + 16 WV g, +16 WV) of the row
 #pragma unroll
-                for (int h = 0; h < WV; h++)
-                    st.wv[u][b][h] =
-                        __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wrow[b]) + uu * (4 * WV) + WV * g + h);
+                for (int h = 0; h < WV; h++) {
+                    if constexpr (WT != 0)
+                        st.wv[u][b][h] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(lb[b] + uu * ls));
+                    else
+                        st.wv[u][b][h] =
+                            __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wrow[b]) + uu * (4 * WV) + WV * g + h);
+                }
             if constexpr (!XL) {
                 const int64_t kk = uu * KSTEP + (KSTEP / 4) * g;
 #pragma unroll
@@ -1376,10 +1397,16 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
     p.rope_rows = g_rope.rows;
     p.epre = env_int("QIE_GEMV_EPRE", 1);
     p.mkdiv = env_int("QIE_GEMV_MKDIV", 0);
-    if (a->M >= 2 && a->M <= 16 && env_int("QIE_SKINNY_MFMA", 1) != 0) {
+    // 16-row tiled fp8 weights the batched-decode kernel did not take (the vocabulary
+    // projection): the skinny kernel reads them, at any 1 <= M <= 16 (qie_linear checked the shape)
+    p.t16 = (a->flags & QIE_LINEAR_FP8_T16) ? 1 : 0;
+    if ((a->M >= 2 || p.t16) && a->M <= 16 && (p.t16 || env_int("QIE_SKINNY_MFMA", 1) != 0)) {
         const bool fp8w = (a->flags & QIE_LINEAR_FP8) != 0;
         const int kstep = 64;
         const bool lds_ok = (size_t)a->M * (a->K + 8) * 2 <= kSkinnyLdsCap;
+        QIE_REQUIRE(!p.t16 || (fp8w && a->K % kstep == 0 && (lds_ok || !a->norm_w)),
+                    "qie_linear: tiled fp8 weights: the skinny kernel cannot take M=%lld K=%lld", (long long)a->M,
+                    (long long)a->K);
         if (a->K % kstep == 0 && (lds_ok || !a->norm_w)) {
             p.M = (int)a->M;
             // Stage the M rows in LDS only when the norm is fused (it needs them) or a block

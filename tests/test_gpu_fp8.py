@@ -423,21 +423,26 @@ def test_fp8_batched_decode_many_tiles_per_block(oracle, qlib, M, tiled):
     K = 3584
     x = rand_bf16(oracle, (M, K), seed=90 + M)
     nw = oracle.f32_to_bf16((1 + 0.2 * rng(13).standard_normal(K)).astype(np.float32))
-    xn = oracle.rmsnorm(x, nw, 1e-6, "ref")
+    # the kernel's own normalised rows (identity weights; they may sit 1 ulp off the oracle's,
+    # test_fp8_batched_decode_kernel): the projections are checked on them
+    de, _ = _fp8_dev(qlib, oracle.f32_to_bf16(np.eye(K, dtype=np.float32)))
+    ye = G.zeros_bf16(M, K)
+    _linear(qlib, G.dev(x), [(de, K)], [], M, K, K, ye, _lib.QIE_EPI_STORE, norm_w=G.dev(nw), eps=1e-6, num=0,
+            flags=_lib.QIE_LINEAR_FP8)
+    xn = G.host_bf16(ye)
     # SwiGLU, I = 18,944 (1,184 tiles)
     I = 18944
     (dg, qg), (du, qu) = dev_w(I, K, 0.08, 7), dev_w(I, K, 0.08, 8)
     y = G.zeros_bf16(M, I)
     _linear(qlib, G.dev(x), [(dg, I), (du, I)], [], M, K, I, y, _lib.QIE_EPI_SWIGLU, norm_w=G.dev(nw), eps=1e-6,
             num=0, flags=fl)
-    # the fused norm may round an element 1 ulp off the oracle's rows (test_fp8_batched_decode_kernel):
-    # the SwiGLU bar is the conditioning-aware one of test_linear_swiglu
+    # the SwiGLU bar of test_fp8_batched_decode_kernel / test_linear_swiglu
     want = oracle.silu_mul(oracle.matmul(xn, qg), oracle.matmul(xn, qu))
     d = G.ulp_diff(G.host_bf16(y), want)
     gs = G.bf(oracle.matmul(xn, qg)).astype(np.float64)
     u = np.abs(G.bf(oracle.matmul(xn, qu)).astype(np.float64))
     ill = (np.abs(gs) < 1e-2 * _abs_scale(oracle, xn, qg)) | (u < 1e-2 * _abs_scale(oracle, xn, qu)) | (gs < -4)
-    assert (d == 0).mean() > 0.9 and not ((d > 4) & ~ill).any()
+    assert (d == 0).mean() > 0.97 and not ((d > 2) & ~ill).any()
     # QKV-shaped, N = 4,608 (288 tiles), biases
     n = (3584, 512, 512)
     q = [dev_w(r, K, 0.05, 30 + i) for i, r in enumerate(n)]
@@ -448,7 +453,7 @@ def test_fp8_batched_decode_many_tiles_per_block(oracle, qlib, M, tiled):
             _lib.QIE_EPI_STORE, norm_w=G.dev(nw), eps=1e-6, num=0, flags=fl)
     want = np.concatenate([oracle.matmul(xn, dq, b) for (_, dq), b in zip(q, bs)], axis=1)
     scale = np.concatenate([_abs_scale(oracle, xn, dq) for _, dq in q], axis=1)
-    G.assert_sum_close(G.host_bf16(y), want, scale, ulps=2, what=f"fp8 dec8 qkv N={N} M={M}")
+    G.assert_sum_close(G.host_bf16(y), want, scale, what=f"fp8 dec8 qkv N={N} M={M}")
     # 8-wave slice shapes, 512 tiles
     for K2 in (2048, 4096):
         x2 = rand_bf16(oracle, (M, K2), seed=K2 + M)
@@ -457,3 +462,27 @@ def test_fp8_batched_decode_many_tiles_per_block(oracle, qlib, M, tiled):
         y = G.zeros_bf16(M, N2)
         _linear(qlib, G.dev(x2), [(dw, N2)], [], M, K2, N2, y, _lib.QIE_EPI_STORE, flags=fl)
         G.assert_sum_close(G.host_bf16(y), oracle.matmul(x2, qw), _abs_scale(oracle, x2, qw), what=f"fp8 dec8 K={K2}")
+
+
+@pytest.mark.parametrize("M", [1, 3, 8])
+def test_fp8_t16_vocab_projection_skinny(oracle, qlib, M):
+    """A vocabulary-sized projection (N > 32,768: the skinny MFMA kernel, not the batched-decode
+    one) on 16-row tiled weights, with the fused norm and arg-max keys: equal bit for bit to
+    the plain layout (M = 1 against M = 2 with a duplicated row), and the keys' ids equal the
+    arg-max of the plain output."""
+    K, N = 896, 40960
+    Mr = max(M, 2)
+    x = rand_bf16(oracle, (Mr, K), seed=500 + M)
+    if M == 1:
+        x[1] = x[0]
+    nw = oracle.f32_to_bf16((1 + 0.2 * rng(14).standard_normal(K)).astype(np.float32))
+    d, _ = _fp8_dev(qlib, rand_bf16(oracle, (N, K), 0.05, seed=501))
+    dt = _tiled(qlib, d, N, K)
+    outs = []
+    for w_, fl, m in ((d, _lib.QIE_LINEAR_FP8, Mr), (dt, _lib.QIE_LINEAR_FP8 | _lib.QIE_LINEAR_FP8_T16, M)):
+        y = G.zeros_bf16(m, N)
+        keys = G.dev(np.zeros(m, np.uint64))
+        _linear(qlib, G.dev(x[:m].copy()), [(w_, N)], [], m, K, N, y, _lib.QIE_EPI_STORE, norm_w=G.dev(nw), eps=1e-6,
+                num=0, keys=keys, flags=fl)
+        outs.append((G.host_bf16(y)[:M], G.host(keys)[:M]))
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])

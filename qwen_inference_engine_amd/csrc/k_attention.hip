@@ -279,6 +279,7 @@ struct PrefillAttnParams {
     int layer, nkv, nq, max_ctx;
     int64_t M;
     uint16_t* out;
+    int full_tiles;          // 1: tiles wholly at or below a group's first position skip the causal mask (dev A/B 0)
 };
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -343,7 +344,7 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
     const int kmax = a.pos[row0 + min(16 * (ngr - 1 - (int)blockIdx.x * 4) + 15, R - 1)];
     const int nkt = kmax / KT + 1;
 
-    int qpos[QG], gpos[QG];
+    int qpos[QG], gpos[QG], gmin[QG];
     bf16x8_t qf[QG][KSTEPS];
 #pragma unroll
     for (int q = 0; q < QG; q++) {
@@ -351,6 +352,9 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
         const int qrow = min(16 * gq + fr, R - 1);
         qpos[q] = a.pos[row0 + qrow];
         gpos[q] = gact[q] ? a.pos[row0 + min(16 * gq + 15, R - 1)] : -1;   // -1: no tile
+        // the group's first position (positions are non-decreasing): a key tile ending at or
+        // before it is unmasked for every row of the group
+        gmin[q] = a.full_tiles ? a.pos[row0 + min(16 * gq, R - 1)] : -1;
         const uint16_t* qp = a.q + (row0 + qrow) * (int64_t)a.nq * HD + (int64_t)h * HD;
 #pragma unroll
         for (int ks = 0; ks < KSTEPS; ks++) qf[q][ks] = *reinterpret_cast<const bf16x8_t*>(qp + ks * 32 + g * 8);
@@ -423,15 +427,29 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
                 if (!on[q]) continue;
                 float (&sv)[4][4] = pv[q];
                 float mt = -INFINITY;
+                // (an fma form, exp2(fma(s, sl2, -m)), saves 16 VALU per tile but rounds
+                // differently: config 2's 128-decision parity run then had a flip at a top-2 gap
+                // 0.34 against the oracle's own 0.31 spread — not taken)
+                if (kt * KT + KT - 1 <= gmin[q]) {   // wave-uniform: no key of the tile is masked
 #pragma unroll
-                for (int t = 0; t < 4; t++)
+                    for (int t = 0; t < 4; t++)
 #pragma unroll
-                    for (int r = 0; r < 4; r++) {
-                        const int key = kt * KT + t * 16 + g * 4 + r;
-                        const float sc = key <= qpos[q] ? sacc[q][t][r] * sl2 : -INFINITY;
-                        sv[t][r] = sc;
-                        mt = fmaxf(mt, sc);
-                    }
+                        for (int r = 0; r < 4; r++) {
+                            const float sc = sacc[q][t][r] * sl2;
+                            sv[t][r] = sc;
+                            mt = fmaxf(mt, sc);
+                        }
+                } else {
+#pragma unroll
+                    for (int t = 0; t < 4; t++)
+#pragma unroll
+                        for (int r = 0; r < 4; r++) {
+                            const int key = kt * KT + t * 16 + g * 4 + r;
+                            const float sc = key <= qpos[q] ? sacc[q][t][r] * sl2 : -INFINITY;
+                            sv[t][r] = sc;
+                            mt = fmaxf(mt, sc);
+                        }
+                }
                 mt = xor32_max(xor16_max(mt));
                 const float m_new = fmaxf(m_run[q], mt);   // finite: tile 0 holds key 0 <= every position
                 const float alpha = __builtin_amdgcn_exp2f(m_run[q] - m_new);
@@ -1119,6 +1137,7 @@ int qie_attention(const void* q, int64_t M, const int32_t* pos, int32_t rows_per
         pa.max_ctx = cache->max_ctx;
         pa.M = M;
         pa.out = (uint16_t*)out;
+        pa.full_tiles = dev_env("QIE_ATTN_PF_FULL", 1);
         const size_t shm = (size_t)2 * 2 * 64 * cache->head_dim * 2;
         const bool pg = pa.km.table != nullptr;
         // balanced causal split: ceil(ceil(R / 16) / 2) group pairs, 4 per workgroup

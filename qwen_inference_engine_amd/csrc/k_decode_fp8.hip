@@ -807,6 +807,7 @@ bool dec8_applies(const qie_linear_args* a) {
     // tiled weights (QIE_LINEAR_FP8_T16) are read by this kernel only, at any 1 <= M <= 16
     const bool t16 = (a->flags & QIE_LINEAR_FP8_T16) != 0;
     if (!(a->flags & QIE_LINEAR_FP8) || a->M < (t16 ? 1 : 2) || a->M > 16) return false;
+    if (t16 && dev_env("QIE_T16_SKINNY", 0) != 0) return false;   // dev A/B: tiled projections on the skinny kernel
     if (!t16 && dev_env("QIE_DEC8", 1) == 0) return false;
     int ku, ks;
     if (!dec8_shape(a->K, &ku, &ks) && dec8_split_parts(a, &ku) == 0) return false;

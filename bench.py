@@ -454,6 +454,12 @@ def _cpu_baseline(spec, a, batch, eng, threads):
     t0 = time.perf_counter()
     par = forced_decisions(O, hw, batch, prompt, a.parity_decisions, nthreads=threads)
     par["seconds"] = round(time.perf_counter() - t0, 1)
+    par["gpu_over_o1_spread"] = round(par["max_norm_rel"] / max(par["oracle_o1_spread"], 1e-30), 3)
+    par["gpu_over_o2_spread"] = round(par["max_norm_rel"] / max(par["oracle_o2_spread"], 1e-30), 3)
+    par["attribution"] = ("tools/flip_attrib.py on this sample (profiles/r04_flip_attrib.json, DESIGN.md section 5): the "
+                          "first op whose difference exceeds the order-1 spread is layer 0's input RMSNorm (fp32 "
+                          "sum-of-squares order; oracle variant 5 reproduces it to 1.1e-4); every flip is upstream of "
+                          "the head (a float64 re-evaluation of the engine's own final row already prefers its id)")
     par["weights"] = (f"the timed model's weights with lm_head rows r % {PEAKED['head_boost_every']} == 0 "
                       f"x 2^{PEAKED['head_boost_log2']} (exact), applied after the timed regions")
     par["rule"] = ("per step norm-relative logit error <= max(1e-3, 2 x the run's oracle order-0 vs order-2 "

@@ -87,13 +87,22 @@ __device__ __forceinline__ uint32_t d8_rms_pair(uint32_t xv, uint32_t wv, float 
     return pack2(y[0], y[1]);
 }
 
+// (split-K: two blocks per CU — at most 128 VGPRs; one block per CU ran the down projection
+// at 24.8 instead of 18.5 µs)
 template <int EPI, int KU, int KS, bool SPL = false, bool T16 = false>
-__global__ __launch_bounds__(KS * 64) void dec8_kernel(Dec8Params p) {
+__global__ __launch_bounds__(KS * 64, SPL ? 4 : 1) void dec8_kernel(Dec8Params p) {
 #pragma clang fp contract(off)
     static_assert(!SPL || EPI != QIE_EPI_SWIGLU, "split-K: single-segment epilogues");
     constexpr int NB = EPI == QIE_EPI_SWIGLU ? 2 : 1;   // B tiles per column tile (gate, up)
     constexpr int kNT = 2;                               // buffer-load policy: nt (streamed once)
-    __shared__ __attribute__((aligned(16))) float red[2][KS][NB][256];
+    // per-wave partial C tiles: RDF slots of KS x NB 16 x 16 fp32 tiles, sized so that the
+    // kernel's static LDS stays within 64 KiB.  A block whose tiles fit keeps each tile's
+    // partials until its last tile and reduces them all after ONE barrier (the per-tile
+    // barrier held every wave to the slowest at each tile: config-4 gate/up 28.7 vs 24.7 µs
+    // without it, measured with the hand-off removed); with M <= 8 only rows 0..7 (lanes
+    // 0..31) matter, so a slot holds two tiles.  More tiles: per-tile hand-off through two slots.
+    constexpr int RDF = (57344 / (KS * NB * 1024)) < 2 ? 2 : (57344 / (KS * NB * 1024));
+    __shared__ __attribute__((aligned(16))) float red[RDF][KS][NB][256];
     __shared__ float ssq[KS][16];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -303,38 +312,79 @@ __global__ __launch_bounds__(KS * 64) void dec8_kernel(Dec8Params p) {
             }
         }
     };
-    // split-K: each tile's reduced part sums wait in LDS until the block's last tile, then
-    // every wave publishes one tile (so the publish / ticket round trips of all the block's
-    // tiles overlap, and none stalls the weight stream)
-    constexpr int kKeep = SPL ? 8 : 1;
-    __shared__ __attribute__((aligned(16))) float keep[kKeep][256];
-    // tile end (after its second step): partial tiles -> LDS, one barrier, epilogue
-    auto finish = [&](const Step& t, int it) {
-        const int buf = it & 1;
-#pragma unroll
-        for (int b = 0; b < NB; b++)
-            *reinterpret_cast<float4*>(&red[buf][wave][b][lane * 4]) = make_float4(acc[b][0], acc[b][1], acc[b][2], acc[b][3]);
-        // one barrier per tile: the next write of red[buf] is two tiles away, behind the
-        // next tile's barrier, which the epilogue wave reaches only after its reads
-        __syncthreads();
-        if (wave != it % KS) return;   // wave-uniform
-        float sum[NB][4];
+    const bool half = M <= 8;                                   // rows 0..7: lanes 0..31
+    // (dev A/B QIE_DEC8_DBG & 16: the per-tile hand-off everywhere; split-K needs the deferred form)
+    // Blocks of one or two tiles keep the per-tile form: deferring saves at most one barrier
+    // there and reloads the row scales / epilogue operands the steps already hold (O, one
+    // tile per block: 5.95 -> 6.29 µs deferred)
+    const bool defer = (SPL || (my >= 3 && !QIE_DBG(p.dbg & 16))) && my <= (half ? 2 * RDF : RDF);   // block-uniform
+    // where tile it's partial of wave w, B tile b, lives (lane-indexed float4)
+    auto slot_at = [&](int it, int w, int b) -> float* {
+        if (defer && half) return &red[it >> 1][w][b][(it & 1) * 128 + lane * 4];
+        return &red[defer ? it : (it & 1)][w][b][lane * 4];
+    };
+    // the KS waves' partials of tile it, summed in wave order (the same order either way;
+    // lanes past row 7 read another tile's slot in the packed form: their rows are >= M)
+    auto reduce = [&](int it, float (&sum)[NB][4]) {
 #pragma unroll
         for (int b = 0; b < NB; b++) {
-            float4 v4 = *reinterpret_cast<const float4*>(&red[buf][0][b][lane * 4]);
+            float4 v4 = *reinterpret_cast<const float4*>(slot_at(it, 0, b));
 #pragma unroll
             for (int w = 1; w < KS; w++) {
-                const float4 v = *reinterpret_cast<const float4*>(&red[buf][w][b][lane * 4]);
+                const float4 v = *reinterpret_cast<const float4*>(slot_at(it, w, b));
                 v4.x += v.x; v4.y += v.y; v4.z += v.z; v4.w += v.w;
             }
             sum[b][0] = v4.x; sum[b][1] = v4.y; sum[b][2] = v4.z; sum[b][3] = v4.w;
         }
-        if constexpr (SPL) {
-            *reinterpret_cast<float4*>(&keep[it][lane * 4]) = make_float4(sum[0][0], sum[0][1], sum[0][2], sum[0][3]);
-            return;
-        }
-        emit(bi + it * G, sum, t.sc, t.ep);
     };
+    // the row scales and epilogue operands of a tile, reloaded (deferred epilogues; the
+    // per-tile path has them from the tile's step loads, issue())
+    auto load_epi = [&](int tile, float (&scv)[NB], float (&epv)[4]) {
+        const int sg = NB == 2 ? 0 : (tile < p.t01[0] ? 0 : (tile < p.t01[1] ? 1 : 2));
+        const int tb0 = sg == 0 ? 0 : (sg == 1 ? p.t01[0] : p.t01[1]);
+        const int rows = p.seg_rows[sg];
+        int r = (tile - tb0) * 16 + fr;
+        r = r < rows ? r : rows - 1;
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p.w[NB == 2 ? b : sg]), (short)0,
+                                                              (int)((int64_t)rows * (K + 4)), 0x00020000);
+            scv[b] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, rows * K + r * 4, 0, 0));
+        }
+        epv[0] = epv[1] = epv[2] = epv[3] = 0.f;
+        const int n = tile * 16 + fr;
+        const int nc = n < p.N ? n : p.N - 1;
+        if constexpr (EPI == QIE_EPI_RESIDUAL) {
+#pragma unroll
+            for (int rr = 0; rr < 4; rr++) {
+                const int i = 4 * g + rr < M ? 4 * g + rr : M - 1;
+                epv[rr] = bf2f(p.y[(int64_t)i * p.ldy + nc]);
+            }
+        } else if constexpr (EPI == QIE_EPI_STORE) {
+            const uint16_t* bp = p.bias[sg];
+            epv[0] = bp ? bf2f(bp[r]) : 0.f;
+        }
+    };
+    // tile end (after its second step): this wave's partial tile -> LDS; deferred: nothing
+    // else until the block's last tile; else one barrier and the rotating wave's epilogue
+    auto finish = [&](const Step& t, int it) {
+        if (!(defer && half) || lane < 32) {
+#pragma unroll
+            for (int b = 0; b < NB; b++)
+                *reinterpret_cast<float4*>(slot_at(it, wave, b)) = make_float4(acc[b][0], acc[b][1], acc[b][2], acc[b][3]);
+        }
+        if (defer) return;   // block-uniform
+        // one barrier per tile: the next write of a slot is two tiles away, behind the
+        // next tile's barrier, which the epilogue wave reaches only after its reads
+        __syncthreads();
+        if constexpr (!SPL) {   // (split-K blocks always defer: dec8_launch caps their tiles)
+            if (wave != it % KS) return;   // wave-uniform
+            float sum[NB][4];
+            reduce(it, sum);
+            emit(bi + it * G, sum, t.sc, t.ep);
+        }
+    };
+
     // split-K tail of tile it (wave it % KS... any wave): publish this part's sums
     // write-through, drain, take the ticket; the last arriver sums every part in part order
     // (independent of arrival order), reloads the row scale and epilogue operands, emits
@@ -342,8 +392,9 @@ __global__ __launch_bounds__(KS * 64) void dec8_kernel(Dec8Params p) {
         const int tile = bi + it * G;
         float* tb = p.slab + (int64_t)tile * p.parts * 256;
         const auto rs = __builtin_amdgcn_make_buffer_rsrc(tb, (short)0, p.parts * 1024, 0x00020000);
-        const float4 k4 = *reinterpret_cast<const float4*>(&keep[it][lane * 4]);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(d8_u32x4, d8_f32x4{k4.x, k4.y, k4.z, k4.w}), rs,
+        float ks[NB][4];
+        reduce(it, ks);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(d8_u32x4, d8_f32x4{ks[0][0], ks[0][1], ks[0][2], ks[0][3]}), rs,
                                                part * 1024 + lane * 16, 0, 16);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         unsigned old = 0;
@@ -394,9 +445,18 @@ __global__ __launch_bounds__(KS * 64) void dec8_kernel(Dec8Params p) {
     mma(sa, 0);
     mma(sb, 1);
     finish(sb, it);
-    if constexpr (SPL) {
-        __syncthreads();   // every tile's sums are in keep[]
-        for (int t2 = wave; t2 < my; t2 += KS) split_tail(t2);
+    if (defer) {   // block-uniform: every wave's partials of every tile are in red[]
+        __syncthreads();
+        for (int t2 = wave; t2 < my; t2 += KS) {
+            if constexpr (SPL) {
+                split_tail(t2);
+            } else {
+                float sum[NB][4], scv[NB], epv[4];
+                load_epi(bi + t2 * G, scv, epv);
+                reduce(t2, sum);
+                emit(bi + t2 * G, sum, scv, epv);
+            }
+        }
     }
     if constexpr (EPI == QIE_EPI_STORE) {
         if (p.keys) {
@@ -694,8 +754,10 @@ static int dec8_launch(const Dec8Params& p, hipStream_t st) {
     const int64_t slots = (int64_t)device_cu_count() * per_cu;
     int grid;
     if constexpr (SPL) {   // parts x G blocks, G tiles in flight per part (one round if they fit)
-        // and at most 8 tiles per block (the kernel keeps each tile's part sums in LDS)
-        const int64_t g = std::max<int64_t>((p.n_tiles + 7) / 8, std::min<int64_t>(p.n_tiles, slots / p.parts));
+        // and at most RDF tiles per block (the kernel keeps every tile's partials in LDS;
+        // RDF as in dec8_kernel, full 16-row slots)
+        constexpr int RDF = (57344 / (KS * 1024)) < 2 ? 2 : (57344 / (KS * 1024));
+        const int64_t g = std::max<int64_t>((p.n_tiles + RDF - 1) / RDF, std::min<int64_t>(p.n_tiles, slots / p.parts));
         grid = (int)(g * p.parts);
     } else {
         grid = (int)std::max<int64_t>(1, std::min<int64_t>(p.n_tiles, slots));

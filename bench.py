@@ -69,7 +69,10 @@ def parse(argv=None):
     ap.add_argument("--tp", action="store_true", help="(compat) same as --parallel tp")
     ap.add_argument("--comm", choices=["rccl", "peer"], default="rccl",
                     help="tensor-parallel exchange: RCCL (default) or the peer backend (HIP IPC buffers, "
-                         "one kernel per exchange with the residual add fused; DESIGN.md §6)")
+                         "one kernel per exchange with the residual add fused; DESIGN.md §6). The peer backend "
+                         "has run across processes on ONE GPU only; across GPUs (xGMI) it is unverified")
+    ap.add_argument("--c5-steps", type=int, default=64,
+                    help="N > 1 (tensor-parallel): timed decode steps of the Qwen2-72B config-5 line")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the other single-GPU BASELINE configs (2 and 4) in the default line")
     ap.add_argument("--dry-run", action="store_true",
@@ -270,12 +273,23 @@ def run(a):
     }
     if tp_note:
         out["note"] = tp_note
+    if comm is not None and a.comm == "peer":   # a timed-out exchange must not yield a number
+        errs = group.allgather(comm.peer_error())
+        out["config"]["peer_error_words"] = errs
+        if any(errs):
+            print(f"bench: peer exchange error words {errs}: the run is invalid", file=sys.stderr, flush=True)
+            group.close()
+            return 4
     headline = (spec.name == "Qwen2-7B" and B == 1 and P == 2048 and not a.fp8 and not a.page_tokens
                 and world == 1 and not a.no_graph)
     if rank == 0 and headline and not a.no_configs:
         out["configs"] = other_configs(Q, S, W)
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.fp8 and B == 1:
         out["cpu_baseline"] = cpu_baseline(spec, a, batch, eng)
+    if comm is not None and not a.no_configs:   # BASELINE configs[4]: the 72B curve, every rank
+        batch.close()
+        eng.close()
+        out["configs"] = {"config5": config5(Q, S, W, a, comm, group, rank, local)}
     if group:
         group.barrier()
         group.close()
@@ -355,6 +369,94 @@ def run_config(Q, S, W, c):
         if b is not None:   # the batch before its engine
             b.close()
         eng.close()
+
+
+def config5(Q, S, W, a, comm, group, rank, local):
+    """BASELINE configs[4] at TP = world: Qwen2-72B bf16, B = 1, P = 2048, over the headline's
+    communicator (every rank runs this; the max over ranks is reported).  Bounded steps
+    (--c5-steps), so a SCALE run carries the 72B curve north_star names.  Also times the
+    step's exchanges alone: 2 row-parallel all-reduces (+ residual add) of [B][H] per layer and
+    the arg-max key reduction, on the engine stream, as the graph runs them."""
+    spec = S.QWEN2_72B
+    world = comm.world
+    ok, why = S.tp_shardable(spec, world)
+    res = {"workload": f"Qwen2-72B bf16 TP={world}, batch=1, prompt={a.prompt}, gen={a.gen} (BASELINE configs[4])",
+           "tp": world, "tp_comm": a.comm}
+    if not ok:
+        res["error"] = f"not shardable at tp{world}: {why}"
+        return res
+    t_cfg = time.perf_counter()
+    P, steps, warm = a.prompt, a.c5_steps, 4
+    max_ctx = P + steps + warm + 16
+    eng = b = None
+    lib = Q._lib.load()
+    bufs = []
+    try:
+        eng = Q.Engine(spec, device=local, max_ctx=max_ctx, comm=comm).init_synthetic(W.SynthParams(seed=0))
+        b = eng.batch(1, max_ctx)
+        prompt = np.random.default_rng(1).integers(0, spec.vocab, size=P, dtype=np.int32)
+        first = b.prefill(0, prompt)           # warm
+        eng.sync()
+        group.barrier()
+        t0 = time.perf_counter()
+        first = b.prefill(0, prompt)
+        eng.sync()
+        t_pf = group.max(time.perf_counter() - t0)
+        b.decode(warm, want_ids=False)
+        b.set_position(0, P, first)
+        eng.sync()
+        group.barrier()
+        t0 = time.perf_counter()
+        b.decode(steps, want_ids=False)
+        eng.sync()
+        dt = group.max(time.perf_counter() - t0)
+        ms = dt * 1e3 / steps
+        # the exchanges alone: the same sizes, order and stream as one decode step's
+        H, L = spec.hidden, spec.n_layers
+        import ctypes as C
+        part, x, keys = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        for p_, n_ in ((part, H * 4), (x, H * 2), (keys, 64)):
+            Q._lib.check(lib.qie_malloc(C.byref(p_), n_), "qie_malloc")
+            Q._lib.check(lib.qie_memset(p_, 0, n_), "qie_memset")
+            bufs.append(p_)
+        st = eng.stream
+        reps = 8
+
+        def exchanges():
+            for _ in range(2 * L):
+                Q._lib.check(lib.qie_comm_allreduce_residual_bf16(comm.h, part, x, H, st), "exchange")
+            Q._lib.check(lib.qie_comm_allreduce_max_u64(comm.h, keys, 1, st), "exchange")
+        exchanges()
+        eng.sync()
+        group.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            exchanges()
+        eng.sync()
+        ex_ms = group.max(time.perf_counter() - t0) * 1e3 / reps
+        step_bytes = spec.decode_weight_bytes() + spec.kv_bytes_per_position() * (P + (steps + 1) / 2.0)
+        per_gpu = step_bytes / world / (ms * 1e-3) / 1e9
+        res.update({"value": round(steps / dt, 3), "unit": "tokens/s", "ms_per_step": round(ms, 4), "steps": steps,
+                    "ctx_timed": [P + 1, P + steps], "prefill_tok_s": round(P / t_pf, 1),
+                    "prefill_ms": round(t_pf * 1e3, 3),
+                    "prefill_tflops_job": round(spec.prefill_flops(P, 1) / t_pf / 1e12, 1),
+                    "step_roofline": {"bytes_per_step": step_bytes, "achieved_GBps_per_gpu": round(per_gpu, 1),
+                                      "frac": round(per_gpu / HBM_PEAK_GBS, 4),
+                                      "roofline_tok_s": round(HBM_PEAK_GBS * 1e9 * world / step_bytes, 1)},
+                    "exchange": {"ms_per_step": round(ex_ms, 4), "frac_of_step": round(ex_ms / ms, 4),
+                                 "per_step": f"{2 * L} all-reduce+residual of {H} fp32 + 1 max-u64 arg-max key",
+                                 "timing": "the step's exchanges alone on the engine stream, max over ranks"}})
+    except Exception as ex:   # reported, never silently dropped
+        res["error"] = str(ex)[:300]
+    finally:
+        for p_ in bufs:
+            lib.qie_free(p_)
+        if b is not None:
+            b.close()
+        if eng is not None:
+            eng.close()
+    res["wall_s"] = round(time.perf_counter() - t_cfg, 1)
+    return res
 
 
 def pmc_traffic(kernel="gate_up", tag=""):
@@ -456,10 +558,10 @@ def _cpu_baseline(spec, a, batch, eng, threads):
     par["seconds"] = round(time.perf_counter() - t0, 1)
     par["gpu_over_o1_spread"] = round(par["max_norm_rel"] / max(par["oracle_o1_spread"], 1e-30), 3)
     par["gpu_over_o2_spread"] = round(par["max_norm_rel"] / max(par["oracle_o2_spread"], 1e-30), 3)
-    par["attribution"] = ("tools/flip_attrib.py on this sample (profiles/r04_flip_attrib.json, DESIGN.md section 5): the "
-                          "first op whose difference exceeds the order-1 spread is layer 0's input RMSNorm (fp32 "
-                          "sum-of-squares order; oracle variant 5 reproduces it to 1.1e-4); every flip is upstream of "
-                          "the head (a float64 re-evaluation of the engine's own final row already prefers its id)")
+    # not computed by this run: a pointer to the one attribution study that was (its build and config)
+    par["attribution_ref"] = {"file": "profiles/r04_flip_attrib.json", "tool": "tools/flip_attrib.py",
+                              "measured_on": "round-4 build, Qwen2-7B full depth, this sample's prompt/seed/64 decisions",
+                              "note": "not re-run by this bench; see DESIGN.md section 5"}
     par["weights"] = (f"the timed model's weights with lm_head rows r % {PEAKED['head_boost_every']} == 0 "
                       f"x 2^{PEAKED['head_boost_log2']} (exact), applied after the timed regions")
     par["rule"] = ("per step norm-relative logit error <= max(1e-3, 2 x the run's oracle order-0 vs order-2 "

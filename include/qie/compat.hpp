@@ -675,12 +675,24 @@ inline Driver& driver() {
     static Driver d;
     return d;
 }
-// destroy the bound engine (before the caller frees the weight arena)
+// destroy the bound engine (before the caller frees the weight arena).  The arena the engine
+// was bound to is forgotten too: a sequence created after the caller freed it must not bind
+// a new engine to freed device memory (create_new_sequence then skips the binding and the
+// next llm() binds to the arena it is given).
 inline void release_engine() {
     Driver& d = driver();
     if (d.engine) qie_engine_destroy(d.engine);
+    if (d.base && loaded_arena_() == d.base) loaded_arena_() = nullptr;
     d.engine = nullptr;
     d.base = nullptr;
+}
+// frees an arena load_all_weights_to_gpu_chunked returned (the reference's cudaFree of
+// g_gpu_weights_buffer, iengine.cu:464-475), releasing the engine bound to it first
+inline void free_weight_arena(bf16* arena) {
+    if (!arena) return;
+    if (driver().base == arena) release_engine();
+    if (loaded_arena_() == arena) loaded_arena_() = nullptr;
+    qie_free(arena);
 }
 
 inline int bind_engine_(const TensorTable& tensors, bf16* base) {

@@ -70,7 +70,9 @@ int qie_comm_create_local(int32_t world, qie_comm** out);
  * qie_comm_peer_connect().  Ranks of one process on one device (world <= 2: the
  * process's hardware queues must give every rank its own):
  * qie_comm_create_peer_local(world, out[world]).  A rank that waited ~10 s for a peer
- * sets the error word qie_comm_peer_error() reads (no kernel waits forever). */
+ * sets the error word qie_comm_peer_error() reads (no kernel waits forever); it then stores
+ * no result, the communicator stays poisoned (later exchanges return at once) and the
+ * engine's next synchronising call fails. */
 #define QIE_COMM_PEER_HANDLE_BYTES 128
 int qie_comm_create_peer(int32_t world, int32_t rank, int32_t device, qie_comm** out, void* handle_out);
 int qie_comm_peer_connect(qie_comm* c, const void* handles);
@@ -81,6 +83,8 @@ int qie_comm_peer_error(const qie_comm* c, int32_t* err);
 int qie_comm_allreduce_residual_bf16(qie_comm* c, const float* part, void* x, int64_t n, void* stream);
 int qie_comm_rank(const qie_comm* c, int32_t* world, int32_t* rank);
 int qie_comm_allreduce_sum_f32(qie_comm* c, float* buf, int64_t n, void* stream);
+/* in place: element-wise max over ranks of u64 words (the greedy arg-max keys) */
+int qie_comm_allreduce_max_u64(qie_comm* c, uint64_t* buf, int64_t n, void* stream);
 void qie_comm_destroy(qie_comm* c);
 
 typedef struct qie_engine_opts {

@@ -149,6 +149,7 @@ SIGNATURES = [
     ("qie_comm_allreduce_residual_bf16", C.c_int, [_P, _P, _P, _I64, _P]),
     ("qie_comm_rank", C.c_int, [_P, _PI32, _PI32]),
     ("qie_comm_allreduce_sum_f32", C.c_int, [_P, _P, _I64, _P]),
+    ("qie_comm_allreduce_max_u64", C.c_int, [_P, _P, _I64, _P]),
     ("qie_comm_destroy", None, [_P]),
     ("qie_index_load_meta", C.c_int, [C.c_char_p, C.POINTER(_P)]),
     ("qie_index_synthetic", C.c_int, [C.POINTER(ModelSpecC), C.POINTER(_P)]),

@@ -190,7 +190,11 @@ struct LocalComm : qie_comm {
 //     between two parities, and a rank can only reach generation e + 2 after every peer
 //     raised its e + 1 flags, i.e. after every peer finished reading generation e;
 //   * the wait is bounded (~10 s of s_memrealtime): a peer that never arrives sets the error
-//     word and the kernel ends (no hang); qie_comm_peer_error() reports it.  Every rank's
+//     word and the kernel ends without storing a result or advancing the generation (no
+//     hang, no silently wrong residual); the communicator is then poisoned (every later
+//     exchange returns at once) and the engine fails its next synchronising call
+//     (qie_decode / qie_decode_step / prefill with ids / logits); qie_comm_peer_error()
+//     reads the word directly.  Every rank's
 //     collective must be able to run while another waits: one process per GPU, or (ranks of
 //     one process on one device) at most 2 ranks — a process gets 4 hardware queues, and two
 //     ranks' streams sharing one queue would serialise a waiting kernel before its peer.
@@ -220,10 +224,17 @@ template <int OP>
 __global__ __launch_bounds__(256) void peer_kernel(PeerArgs A, const void* src, void* dst, int64_t n) {
     using T = typename std::conditional<OP == kPeerMaxU64, uint64_t,
                                         typename std::conditional<OP == kPeerGatherB, uint8_t, uint32_t>::type>::type;
-    __shared__ unsigned e_s;
+    __shared__ unsigned e_s, err_s;
     const int blk = blockIdx.x, tid = threadIdx.x;
-    if (tid == 0) e_s = __hip_atomic_load(A.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) {
+        e_s = __hip_atomic_load(A.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        err_s = __hip_atomic_load(A.ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     __syncthreads();
+    // a communicator whose exchange once timed out is poisoned: the ranks are out of step
+    // (this rank's generation moved on without the late one), so later exchanges neither
+    // push, wait nor store; the engine reports the error word at its next sync point
+    if (err_s) return;
     const unsigned e = e_s;
     const int par = e & 1;
     // this block's slice (resid: whole groups of 8 so the bf16 row is read in 16-B pieces)
@@ -247,11 +258,15 @@ __global__ __launch_bounds__(256) void peer_kernel(PeerArgs A, const void* src, 
             __builtin_amdgcn_s_sleep(2);
             if (__builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull) {   // ~10 s at 100 MHz
                 __hip_atomic_store(A.ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                err_s = 1;
                 break;
             }
         }
     }
     __syncthreads();
+    // timed out: the slots may hold a stale generation — store nothing, and never take the
+    // ticket, so the generation does not advance past the late rank
+    if (err_s) return;
     __threadfence_system();
     char* mine = A.buf[A.rank];
     if constexpr (OP == kPeerGather || OP == kPeerGatherB) {
@@ -365,6 +380,11 @@ struct PeerComm : qie_comm {
         return 0;
     }
     bool graph_capturable() const override { return true; }
+    int error_state() const override {
+        unsigned v = 0;
+        if (hipMemcpy(&v, ctl + 2, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+        return (int)v;
+    }
 };
 
 static int peer_alloc(PeerComm* c) {
@@ -526,6 +546,11 @@ int qie_comm_rank(const qie_comm* c, int32_t* world, int32_t* rank) {
 int qie_comm_allreduce_sum_f32(qie_comm* c, float* buf, int64_t n, void* stream) {
     QIE_REQUIRE(c && buf && n >= 0, "qie_comm_allreduce_sum_f32: bad arguments");
     return c->allreduce_sum_f32(buf, n, (hipStream_t)stream);
+}
+
+int qie_comm_allreduce_max_u64(qie_comm* c, uint64_t* buf, int64_t n, void* stream) {
+    QIE_REQUIRE(c && buf && n >= 0, "qie_comm_allreduce_max_u64: bad arguments");
+    return c->allreduce_max_u64(buf, n, (hipStream_t)stream);
 }
 
 void qie_comm_destroy(qie_comm* c) { delete c; }

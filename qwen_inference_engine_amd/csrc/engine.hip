@@ -471,6 +471,16 @@ static qie_linear_args lin_proj(const qie_engine* e) {
 // when the engine was asked to (opts.comm_always: the captured-collective path on one GPU).
 static bool use_comm(const qie_engine* e) { return e->comm && (e->sh.tp > 1 || e->opts.comm_always); }
 
+// After a stream synchronisation: a device-side exchange failure (the peer backend's bounded
+// wait) makes the call fail instead of returning ids computed from a partial exchange.
+static int comm_check(const qie_engine* e, const char* who) {
+    if (!use_comm(e)) return 0;
+    const int err = e->comm->error_state();
+    if (err) return fail(-7, "%s: tensor-parallel exchange failed on the device (error word %d: a peer rank did "
+                             "not arrive within the bounded wait); the communicator is unusable", who, err);
+    return 0;
+}
+
 // Row-parallel projection epilogue under tensor parallelism: fp32 partials -> all-reduce
 // -> x = bf16(x + bf16(sum)); the single-GPU path fuses the residual into the GEMV/GEMM.
 static int row_parallel(qie_batch* b, qie_linear_args& a, uint16_t* x, float* part, int64_t rows) {
@@ -689,7 +699,7 @@ static int sync_ids(qie_batch* b, int32_t* next_ids) {
     if (!next_ids) return 0;
     QIE_HIP(hipMemcpyAsync(next_ids, b->d_ids, b->B * 4, hipMemcpyDeviceToHost, b->e->stream));
     QIE_HIP(hipStreamSynchronize(b->e->stream));
-    return 0;
+    return comm_check(b->e, "decode");
 }
 
 }  // namespace qie
@@ -1015,7 +1025,7 @@ void* qie_engine_stream(qie_engine* e) { return e ? (void*)e->stream : nullptr; 
 int qie_engine_sync(qie_engine* e) {
     QIE_REQUIRE(e, "qie_engine_sync: null");
     QIE_HIP(hipStreamSynchronize(e->stream));
-    return 0;
+    return comm_check(e, "qie_engine_sync");
 }
 
 void qie_engine_destroy(qie_engine* e) {
@@ -1273,6 +1283,7 @@ static int prefill_rows(qie_batch* b, int seq0, int n_seqs, const int32_t* ids, 
     if (next_ids) {
         QIE_HIP(hipMemcpyAsync(next_ids, b->d_ids + seq0, (size_t)n_seqs * 4, hipMemcpyDeviceToHost, st));
         QIE_HIP(hipStreamSynchronize(st));
+        QIE_TRY(comm_check(e, who));
     }
     return 0;
 }
@@ -1367,6 +1378,7 @@ int qie_decode(qie_batch* b, int32_t n_steps, const qie_sampling* smp, int32_t* 
         for (int m = 0; m < b->B; m++) b->h_pos[m] += 1;
     }
     QIE_HIP(hipStreamSynchronize(b->e->stream));
+    QIE_TRY(comm_check(b->e, "qie_decode"));
     if (out_ids && n_steps > 0) {
         std::vector<int32_t> row(b->max_ctx);
         for (int m = 0; m < b->B; m++) {
@@ -1386,6 +1398,7 @@ int qie_batch_logits(qie_batch* b, void* host_out) {
         src = b->logits_full;
     }
     QIE_HIP(hipStreamSynchronize(b->e->stream));
+    QIE_TRY(comm_check(b->e, "qie_batch_logits"));
     QIE_HIP(hipMemcpy(host_out, src, (size_t)b->B * b->e->spec.vocab * 2, hipMemcpyDeviceToHost));
     return 0;
 }

@@ -26,4 +26,7 @@ struct qie_comm {
     // x (bf16 [n]) = bf16(x + bf16(all-reduced sum of part)): the row-parallel exchange; the
     // peer backend does it in one kernel, the others all-reduce `part` in place and add
     virtual int allreduce_residual_bf16(const float* part, uint16_t* x, int64_t n, hipStream_t st);
+    // non-zero once an exchange failed on the device (the peer backend's bounded wait timed
+    // out); read after the stream synchronised — a blocking copy of one word
+    virtual int error_state() const { return 0; }
 };

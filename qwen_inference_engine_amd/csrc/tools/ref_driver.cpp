@@ -128,7 +128,6 @@ int main(int argc, char** argv) {
     delete new_seq_1->buffer;
     free(new_seq_1);
     std::free(h_host);
-    release_engine();
-    qie_free(g_gpu_weights_buffer);
+    free_weight_arena(g_gpu_weights_buffer);
     return 0;
 }

@@ -161,12 +161,20 @@ class Engine:
 
     def boost_head(self, every: int, log2f: int) -> None:
         """lm_head rows r % every == 0 times 2^log2f, in place on device (SynthParams'
-        peaked head; same values as HostWeights.boost_head).  bf16 single-GPU engines."""
-        if self.comm is not None or getattr(self, "_fp8", False):
-            raise ValueError("boost_head: bf16 single-GPU engines only")
+        peaked head; same values as HostWeights.boost_head).  bf16 engines; under tensor
+        parallelism each rank scales its vocab slice (rows rank*V/tp ..), untied heads only
+        (a tied head's slice is a view of the replicated embedding)."""
+        if getattr(self, "_fp8", False):
+            raise ValueError("boost_head: bf16 engines only")
+        rows, row0 = self.spec.vocab, 0
+        if self.comm is not None and self.comm.world > 1:
+            if self.spec.tie_embeddings:
+                raise ValueError("boost_head: tensor-parallel engines with an untied head only")
+            rows = self.spec.vocab // self.comm.world
+            row0 = self.comm.rank * rows
         w = _lib.ModelWeightsC()
         _lib.check(self.lib.qie_engine_weights(self.h, C.byref(w), None), "qie_engine_weights")
-        _lib.check(self.lib.qie_scale_rows_pow2(w.lm_head, self.spec.vocab, self.spec.hidden, 0, every, log2f,
+        _lib.check(self.lib.qie_scale_rows_pow2(w.lm_head, rows, self.spec.hidden, row0, every, log2f,
                                                 self.stream), "qie_scale_rows_pow2")
         self.sync()
 

@@ -219,6 +219,73 @@ def test_peer_two_processes_one_gpu(tmp_path):
         assert np.array_equal(out["s"], want_sum), f"rank {r} sum"
 
 
+class _Replay:
+    """The Batch surface tests/parity.py forced_decisions drives (prefill / logits /
+    set_position / decode_step), replaying what a tensor-parallel worker process recorded
+    while it ran the same protocol (tests/tp_engine_worker.py)."""
+
+    def __init__(self, ids, logits):
+        self.ids, self.lg, self.i = [int(t) for t in ids], logits, 0
+
+    def prefill(self, seq, prompt):
+        return self.ids[0]
+
+    def logits(self):
+        return self.lg[self.i][None, :]
+
+    def set_position(self, seq, pos, tok):
+        pass
+
+    def decode_step(self):
+        self.i += 1
+        return [self.ids[self.i]]
+
+
+def test_engine_tp_two_processes_peer_forced_decisions(oracle, tmp_path):
+    """The ENGINE's tensor-parallel forward across processes (verdict r04 item 1): two ranks
+    as two processes on this box's one GPU, peer backend over HIP IPC, each holding half of a
+    Qwen2-7B-width model (2 layers: q/kv heads 14/2 per rank, gate/up 9,472 rows, vocab slice
+    76,032 rows, peaked head), decode steps replayed from captured hipGraphs (the exchanges are
+    graph nodes) — driven through tests/parity.py forced_decisions' protocol: a 16-token
+    prompt then 31 teacher-forced decisions.  Bar: both ranks' ids and gathered logits are
+    identical, no exchange timed out, and rank 0's trace passes forced_decisions' rule against
+    oracle orders 0 / 1 / 2 (the unsharded CPU restatement)."""
+    import os
+    import subprocess
+    import sys
+    world, L, P, n = 2, 2, 16, 32
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    worker = os.path.join(os.path.dirname(__file__), "tp_engine_worker.py")
+    ps = [subprocess.Popen([sys.executable, worker, str(r), str(world), str(tmp_path), str(L), str(P), str(n)],
+                           env=env, stderr=subprocess.PIPE, text=True) for r in range(world)]
+    rcs, errs = [], []
+    for p in ps:
+        try:
+            _, e = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            for q in ps:
+                q.kill()
+            raise AssertionError("tensor-parallel engine worker hung")
+        rcs.append(p.returncode)
+        errs.append(e)
+    if any(rc == 5 for rc in rcs):
+        pytest.skip("IPC mapping refused: " + " | ".join(e.strip()[-300:] for e in errs if e))
+    assert rcs == [0] * world, [e[-2000:] for e in errs]
+    outs = [np.load(tmp_path / f"out{r}.npz") for r in range(world)]
+    for r in range(world):
+        assert int(outs[r]["err"]) == 0, f"rank {r}: a peer exchange timed out"
+    assert np.array_equal(outs[0]["ids"], outs[1]["ids"]), "ranks disagree on ids"
+    assert np.array_equal(outs[0]["logits"], outs[1]["logits"]), "ranks disagree on gathered logits"
+    from parity import PEAKED, forced_decisions
+    spec = S.QWEN2_7B.replace(n_layers=L)
+    hw = W.HostWeights.synthetic(spec, W.SynthParams(seed=0, **PEAKED))
+    prompt = [int(t) for t in outs[0]["prompt"]]
+    rep = forced_decisions(oracle, hw, _Replay(outs[0]["ids"], outs[0]["logits"]), prompt, n)
+    print("tp2 two-process forced decisions:", rep)
+    assert rep["ok"], rep
+
+
 def test_tp_sampling_ranks_agree():
     spec, world = CONFIGS["qwen2-bias-hd64"]
     prompt = list(rng(5).integers(0, spec.vocab, 9))

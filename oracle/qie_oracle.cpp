@@ -140,11 +140,24 @@ static int g_sum_order = 0;
  *   3 = order 0 except the attention softmax in 2's online form;
  *   4 = order 0 except SiLU's exponent in 2's fast-math form;
  *   5 = order 0 except the RMSNorm sum of squares in 2's order;
- *   6 = order 0 except the attention q.k dot products in 2's order (3..6: tools/flip_attrib.py).
- * The logit spread between variant 0 and 1 / 2 at a given depth is the reference
+ *   6 = order 0 except the attention q.k dot products in 2's order (3..6: tools/flip_attrib.py);
+ *   7 = order 0 as nvcc -use_fast_math compiles it (the reference's recorded build,
+ *       build/CMakeFiles/qwen.dir/flags.make:10: --fmad=true, --prec-div=false, fast
+ *       exponent): a*b+c contracted to fmaf where the source has it (RoPE's x0*c - x1*s and
+ *       x1*c + x0*s, RoPE.cu:16-17, as fmaf(x0, c, -(x1*s)) / fmaf(x1, c, x0*s); P.V's
+ *       out_val += p*v, self_attension.cu:138, as fmaf(p, v, out)); every '/' as a times the
+ *       reciprocal of b (div.approx; fm_div); expf as exp2(x log2 e) (__expf).  The RMSNorm
+ *       and q.k sums of squares / products contract too, but a bf16 x bf16 product is exact in
+ *       fp32, so fmaf(t, t, s) == s + t*t there.  The approximate instructions' last-ulp
+ *       behaviour is NVIDIA's and unpublished: rcp / sqrt are modelled correctly rounded.
+ * The logit spread between variant 0 and 1 / 2 / 7 at a given depth is the reference
  * algorithm's own order sensitivity, which sizes the end-to-end parity tolerance
  * (bench.py cpu_baseline, tests/test_gpu_headline.py, DESIGN.md "Parity"). */
 void or_set_sum_order(int v) { g_sum_order = v; }
+
+// order 7 (nvcc -use_fast_math) models: a / b as a * rcp(b), expf(x) as exp2(x log2 e)
+static inline float fm_div(float a, float b) { return a * (1.0f / b); }
+static inline float fm_exp(float x) { return exp2f(x * 1.44269504088896341f); }
 
 /* ---------------------------------------------------------------- RMSNorm
  * Reference: rmsNorm, layers/src/normalization.cu:5-25 (one thread per row):
@@ -178,6 +191,10 @@ void or_rmsnorm(const bf16_t* x, const bf16_t* w, bf16_t* y, int64_t rows, int64
             float inv = 1.0f / sqrtf(sum / (float)H + eps);
             for (int64_t i = 0; i < H; i++)
                 yr[i] = f2bf(bf2f(w[i]) * rbf(bf2f(xr[i]) * inv));
+        } else if (g_sum_order == 7) {
+            float rms = sqrtf(fm_div(sum, (float)H) + eps);
+            for (int64_t i = 0; i < H; i++)
+                yr[i] = f2bf(fm_div(bf2f(xr[i]), rms) * bf2f(w[i]));
         } else {
             float rms = sqrtf((sum / (float)H) + eps);
             for (int64_t i = 0; i < H; i++)
@@ -294,6 +311,11 @@ void or_qknorm(bf16_t* x, const bf16_t* w, int64_t rows, int64_t row_stride, int
             else
                 for (int stride = hd / 2; stride > 0; stride >>= 1)
                     for (int d = 0; d < stride; d++) buf[d] += buf[d + stride];
+            if (g_sum_order == 7) {
+                float rms = sqrtf(fm_div(buf[0], (float)hd) + eps);
+                for (int d = 0; d < hd; d++) v[d] = f2bf(fm_div(bf2f(v[d]), rms) * bf2f(w[d]));
+                continue;
+            }
             float rms = sqrtf((buf[0] / hd) + eps);
             for (int d = 0; d < hd; d++) v[d] = f2bf((bf2f(v[d]) / rms) * bf2f(w[d]));
         }
@@ -327,8 +349,14 @@ void or_rope(bf16_t* x, const float* cos_t, const float* sin_t, const int32_t* p
                 for (int i = 0; i < hd; i += 2) {
                     int t = i / 2;
                     float x0 = bf2f(v[i]), x1 = bf2f(v[i + 1]);
-                    float y0 = x0 * c[t] - x1 * s[t];
-                    float y1 = x1 * c[t] + x0 * s[t];
+                    float y0, y1;
+                    if (g_sum_order == 7) {   // contracted as nvcc --fmad=true does
+                        y0 = fmaf(x0, c[t], -(x1 * s[t]));
+                        y1 = fmaf(x1, c[t], x0 * s[t]);
+                    } else {
+                        y0 = x0 * c[t] - x1 * s[t];
+                        y1 = x1 * c[t] + x0 * s[t];
+                    }
                     v[i] = f2bf(y0);
                     v[i + 1] = f2bf(y1);
                 }
@@ -346,7 +374,7 @@ void or_silu_mul(const bf16_t* gate, const bf16_t* up, bf16_t* h, int64_t n) {
         float g = bf2f(gate[i]);
         // order 2: the reference build's -use_fast_math exponent (flags.make:10), which a
         // GPU libm need not match to the last ulp either
-        const float ex = g_sum_order == 2 || g_sum_order == 4 ? exp2f(-g * 1.44269504088896341f) : expf(-g);
+        const float ex = g_sum_order == 2 || g_sum_order == 4 || g_sum_order == 7 ? fm_exp(-g) : expf(-g);
         float a = rbf(g * (1.0f / (1.0f + ex)));
         h[i] = f2bf(bf2f(up[i]) * a);
     }
@@ -372,9 +400,70 @@ void or_embedding(const bf16_t* E, const int32_t* ids, bf16_t* out, int64_t n, i
  * Cache layout here: [nkv][ctx][hd] for ONE layer (kv_head_stride elements
  * between kv heads, hd between positions).  q/out rows: [mq][nq*hd].
  */
+/* HF numerics (transformers' eager_attention_forward, Qwen2/Qwen3): the scores are a bf16
+ * matmul output, scaled in bf16 (bf16(bf16(q.k) * hd^-0.5)); softmax in fp32 (exp(s - m),
+ * times the reciprocal of the sum), the probabilities rounded to bf16 before the bf16 P.V
+ * matmul (fp32 accumulate, one rounding).  The masked scores are excluded (-inf). */
+static void attention_hf(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, bf16_t* out, int mq, int mkv,
+                         int nq, int nkv, int hd, int causal, int q_abs_base, int64_t kv_head_stride,
+                         int nthreads) {
+    const int group = nq / nkv;
+    const float scaling = (float)(1.0 / std::sqrt((double)hd));
+    int nt = set_threads(nthreads);
+#pragma omp parallel num_threads(nt)
+    {
+        std::vector<float> score(mkv > 0 ? mkv : 1);
+#pragma omp for schedule(static) collapse(2)
+        for (int h = 0; h < nq; h++) {
+            for (int qt = 0; qt < mq; qt++) {
+                const int g = h / group;
+                const bf16_t* qr = q + (int64_t)qt * nq * hd + (int64_t)h * hd;
+                const bf16_t* kh = kc + (int64_t)g * kv_head_stride;
+                const bf16_t* vh = vc + (int64_t)g * kv_head_stride;
+                const int q_abs = q_abs_base + qt;
+                const int n = causal ? std::min(mkv, q_abs + 1) : mkv;
+                float mx = -INFINITY;
+                for (int t = 0; t < n; t++) {
+                    const bf16_t* kr = kh + (int64_t)t * hd;
+                    double acc = 0.0;
+                    for (int d = 0; d < hd; d++) acc += (double)(bf2f(qr[d]) * bf2f(kr[d]));
+                    score[t] = rbf(rbf((float)acc) * scaling);
+                    mx = fmaxf(mx, score[t]);
+                }
+                float sum = 0.f;
+                for (int t = 0; t < n; t++) {
+                    score[t] = expf(score[t] - mx);
+                    sum += score[t];
+                }
+                const float inv = 1.0f / sum;
+                for (int t = 0; t < n; t++) score[t] = rbf(score[t] * inv);
+                bf16_t* orow = out + (int64_t)qt * nq * hd + (int64_t)h * hd;
+                for (int d = 0; d < hd; d++) {
+                    double acc = 0.0;
+                    for (int t = 0; t < n; t++) acc += (double)(score[t] * bf2f(vh[(int64_t)t * hd + d]));
+                    orow[d] = f2bf((float)acc);
+                }
+            }
+        }
+    }
+}
+
+void or_attention_nm(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, bf16_t* out, int mq, int mkv, int nq,
+                     int nkv, int hd, int causal, int q_abs_base, int64_t kv_head_stride, int nthreads, int numerics);
+
 void or_attention(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, bf16_t* out,
                   int mq, int mkv, int nq, int nkv, int hd, int causal, int q_abs_base,
                   int64_t kv_head_stride, int nthreads) {
+    or_attention_nm(q, kc, vc, out, mq, mkv, nq, nkv, hd, causal, q_abs_base, kv_head_stride, nthreads,
+                    QIE_NUMERICS_REF);
+}
+
+void or_attention_nm(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, bf16_t* out, int mq, int mkv, int nq,
+                     int nkv, int hd, int causal, int q_abs_base, int64_t kv_head_stride, int nthreads, int numerics) {
+    if (numerics == QIE_NUMERICS_HF) {
+        attention_hf(q, kc, vc, out, mq, mkv, nq, nkv, hd, causal, q_abs_base, kv_head_stride, nthreads);
+        return;
+    }
     int group = nq / nkv;
     float scale = sqrtf((float)hd);
     int nt = set_threads(nthreads);
@@ -401,7 +490,7 @@ void or_attention(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, bf16_t* o
                         for (int stride = hd / 2; stride > 0; stride >>= 1)
                             for (int d = 0; d < stride; d++) buf[d] += buf[d + stride];
                     }
-                    score[t] = buf[0] / scale;
+                    score[t] = g_sum_order == 7 ? fm_div(buf[0], scale) : buf[0] / scale;
                 }
                 int q_abs = q_abs_base + qt;
                 if (causal)
@@ -433,6 +522,19 @@ void or_attention(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, bf16_t* o
                             acc += ba;
                         }
                         orow[d] = f2bf(acc / sum);
+                    }
+                    continue;
+                } else if (g_sum_order == 7) {
+                    for (int t = 0; t < mkv; t++) {
+                        score[t] = fm_exp(score[t] - mx);
+                        sum += score[t];
+                    }
+                    for (int t = 0; t < mkv; t++) score[t] = fm_div(score[t], sum);
+                    bf16_t* orow = out + (int64_t)qt * nq * hd + (int64_t)h * hd;
+                    for (int d = 0; d < hd; d++) {
+                        float acc = 0.f;
+                        for (int t = 0; t < mkv; t++) acc = fmaf(score[t], bf2f(vh[(int64_t)t * hd + d]), acc);
+                        orow[d] = f2bf(acc);
                     }
                     continue;
                 } else {
@@ -646,8 +748,8 @@ int or_forward(const qie_model_spec* s, const qie_model_weights* w, bf16_t* kcac
                 std::memcpy(vl + g * head_stride + (int64_t)(start_pos + t) * hd,
                             v.data() + (int64_t)t * KD + g * hd, hd * 2);
             }
-        or_attention(q.data(), kl, vl, att.data(), n, ctx, (int)nq, (int)nkv, (int)hd,
-                     /*causal=*/1, start_pos, head_stride, nthreads);
+        or_attention_nm(q.data(), kl, vl, att.data(), n, ctx, (int)nq, (int)nkv, (int)hd,
+                        /*causal=*/1, start_pos, head_stride, nthreads, num);
         or_matmul(att.data(), (const bf16_t*)lw.wo, nullptr, tmp.data(), n, QD, H, nthreads);
         or_resadd(x.data(), tmp.data(), (int64_t)n * H);
         dump(2 * l + 1);

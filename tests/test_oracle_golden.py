@@ -244,3 +244,93 @@ def test_forward_prefill_equals_incremental_decode(oracle):
     m2 = oracle.Model(hw, 64)
     l2 = m2.forward(prompt + ids[:4], 0)
     assert np.array_equal(l2, lg[4])
+
+
+# ---------------------------------------------------- order 7: the nvcc -use_fast_math model
+def _f32(x):
+    return np.float32(x)
+
+
+def test_order7_rmsnorm_is_fast_division_over_the_exact_sequential_sum(oracle):
+    """Order 7 (or_set_sum_order): RMSNorm as nvcc -use_fast_math compiles
+    normalization.cu:13-22.  The contracted sum fmaf(t, t, s) equals s + t*t here (a bf16
+    square is exact in fp32), so only the divisions change: sum * rcp(H) and x * rcp(rms).
+    Checked bit for bit against a sequential float32 numpy emulation."""
+    r = rng(21)
+    H = 384
+    x = oracle.f32_to_bf16(r.standard_normal((4, H)).astype(np.float32))
+    w = oracle.f32_to_bf16(1 + 0.1 * r.standard_normal(H).astype(np.float32))
+    oracle.set_sum_order(7)
+    try:
+        y = oracle.rmsnorm(x, w, 1e-4, "ref")
+    finally:
+        oracle.set_sum_order(0)
+    xf, wf = oracle.bf16_to_f32(x), oracle.bf16_to_f32(w)
+    want = np.zeros_like(x)
+    for i in range(x.shape[0]):
+        s = np.cumsum(xf[i] * xf[i], dtype=np.float32)[-1]       # sequential fp32 (squares exact)
+        rms = np.sqrt(_f32(s * (_f32(1) / _f32(H))) + _f32(1e-4), dtype=np.float32)
+        q = (xf[i] * (_f32(1) / rms)).astype(np.float32)
+        want[i] = oracle.f32_to_bf16((q * wf).astype(np.float32))
+    assert np.array_equal(y, want)
+    y0 = oracle.rmsnorm(x, w, 1e-4, "ref")
+    d = np.abs(oracle.bf16_to_f32(y) - oracle.bf16_to_f32(y0))
+    assert d.max() <= np.abs(oracle.bf16_to_f32(y0)).max() * 2 ** -7   # within a bf16 ulp of order 0
+
+
+def test_order7_rope_is_contracted(oracle):
+    """Order 7: RoPE.cu:16-17 contracted as nvcc --fmad=true does, fmaf(x0, c, -(x1*s)) and
+    fmaf(x1, c, x0*s), checked against a float64 emulation of the fma (the x*c product of
+    a bf16 and an fp32 is exact in float64) on the reference's own table formula."""
+    r = rng(22)
+    hd, nh, rows = 128, 4, 40
+    x = oracle.f32_to_bf16(r.standard_normal((rows, nh * hd)).astype(np.float32))
+    cs, sn = oracle.rope_table(rows + 7, hd, 1e6, "ref")
+    pos = np.arange(7, 7 + rows, dtype=np.int32)
+    oracle.set_sum_order(7)
+    try:
+        y = oracle.rope(x, cs, sn, pos, nh, hd, "ref")
+    finally:
+        oracle.set_sum_order(0)
+    xf = oracle.bf16_to_f32(x).reshape(rows, nh, hd // 2, 2).astype(np.float64)
+    c = cs.reshape(-1, hd // 2)[pos][:, None, :].astype(np.float64)
+    s = sn.reshape(-1, hd // 2)[pos][:, None, :].astype(np.float64)
+    x0, x1 = xf[..., 0], xf[..., 1]
+    t0 = (x1 * s).astype(np.float32).astype(np.float64)   # the un-fused product, rounded
+    t1 = (x0 * s).astype(np.float32).astype(np.float64)
+    y0 = (x0 * c - t0).astype(np.float32)
+    y1 = (x1 * c + t1).astype(np.float32)
+    want = oracle.f32_to_bf16(np.stack([y0, y1], -1).reshape(rows, nh * hd))
+    assert np.array_equal(y, want)
+    # the fused and unfused fp32 results differ by at most an fp32 ulp or two, which the
+    # bf16 rounding after RoPE almost always absorbs (measured: no element of this sample)
+    y_ref = oracle.rope(x, cs, sn, pos, nh, hd, "ref")
+    assert (y != y_ref).mean() < 1e-3
+
+
+def test_order7_attention_fast_math(oracle):
+    """Order 7 attention (self_attension.cu:84-138 under -use_fast_math): scores divided by
+    a reciprocal, __expf, p * rcp(sum), P.V as an fmaf chain — within 2e-2 of float64 and
+    a valid evaluation distinct from order 0."""
+    r = rng(23)
+    nq, nkv, hd, ctx = 4, 2, 64, 300
+    q = oracle.f32_to_bf16(r.standard_normal((3, nq * hd)).astype(np.float32))
+    k = oracle.f32_to_bf16(r.standard_normal((nkv, ctx, hd)).astype(np.float32))
+    v = oracle.f32_to_bf16(r.standard_normal((nkv, ctx, hd)).astype(np.float32))
+    base = ctx - 3
+    oracle.set_sum_order(7)
+    try:
+        o7 = oracle.attention(q, k, v, nq, nkv, hd, True, base)
+    finally:
+        oracle.set_sum_order(0)
+    o0 = oracle.attention(q, k, v, nq, nkv, hd, True, base)
+    f7, f0 = oracle.bf16_to_f32(o7), oracle.bf16_to_f32(o0)
+    assert np.abs(f7 - f0).max() <= 2 ** -6 * np.abs(f0).max()
+    qf, kf, vf = (oracle.bf16_to_f32(t).astype(np.float64) for t in (q, k, v))
+    for t in range(3):
+        for h in range(nq):
+            g = h // (nq // nkv)
+            sc = kf[g, :base + t + 1] @ qf[t, h * hd:(h + 1) * hd] / np.sqrt(hd)
+            p = np.exp(sc - sc.max())
+            p /= p.sum()
+            assert np.abs(f7[t, h * hd:(h + 1) * hd] - p @ vf[g, :base + t + 1]).max() < 2e-2

@@ -98,7 +98,11 @@ typedef struct qie_engine_opts {
     int32_t comm_always;     /* 1: run the exchange steps (row-parallel all-reduces, the
                                 greedy key max, the logit gather) through tp_comm even at
                                 world 1 — the captured-collective path on one GPU (tests) */
-    int32_t reserved[6];
+    int32_t prefill_fp8;     /* 1 (with weight_fp8): the prefill projections run on the
+                                block-scaled fp8 MFMA (QIE_LINEAR_ACT_FP8) — activations
+                                quantised per row to e4m3 before each projection, a
+                                different model from the bf16-activation one (numerics flag) */
+    int32_t reserved[5];
 } qie_engine_opts;
 
 int qie_engine_create(const qie_model_spec* spec, const qie_engine_opts* opts, qie_engine** out);

@@ -101,6 +101,7 @@ typedef struct qie_linear_args {
                                zeroes them before the launch                            */
     int64_t key_col0;       /* global index of output column 0 in the keys (vocab-
                                parallel lm_head shard offset; 0 otherwise)              */
+    const uint8_t* x_exps;  /* QIE_LINEAR_ACT_FP8: [M] e8m0 row exponents of x (below)  */
 } qie_linear_args;
 
 int qie_linear(const qie_linear_args* args, void* stream);
@@ -266,6 +267,23 @@ int qie_dequantize_fp8(const void* w_fp8, int64_t rows, int64_t cols, void* out_
  * only: M <= 16 rows; the engine tiles its own decode projections, tiled weights are not
  * read by the prefill GEMMs, which take the dequantised bf16 copy). */
 #define QIE_LINEAR_FP8_T16 16
+/* Block-scaled fp8 ACTIVATIONS — the CDNA4 fp8 MFMA path (v_mfma_scale_f32_16x16x128_
+ * f8f6f4), an explicit numerics choice (the engine's qie_engine_opts.prefill_fp8): x holds
+ * e4m3 codes [M, K] with row stride ldx BYTES and x_exps their per-row e8m0 exponents, row m
+ * standing for 2^(x_exps[m] - 127) * e4m3(code) (qie_quantize_rows_fp8).  The weights must be
+ * fp8 (QIE_LINEAR_FP8, plain or QIE_LINEAR_FP8_T16 tiled); their power-of-two row scales are
+ * the MFMA's other e8m0 operand.  K % 128 == 0, ldx % 16 == 0, no fused norm / arg-max, any
+ * M (the batched-decode row limit of the tiled layout does not apply).  Replaces the
+ * reference's matrix_mul (matrix_mul.cu:165-288) for a model whose prefill activations are
+ * quantised; the oracle runs the same model (or_set_act_fp8). */
+#define QIE_LINEAR_ACT_FP8 32
+/* Per-row activation quantisation for QIE_LINEAR_ACT_FP8: s[m] = the smallest power of two
+ * with max_k |x[m, k]| / s[m] <= 448 (1 for an all-zero row; e4m3_row_scale), codes
+ * q[m, k] = e4m3(x[m, k] / s[m]) rounded to nearest even (|x / s| <= 448: nothing saturates),
+ * exps[m] = log2(s[m]) + 127.  x bf16 [rows, cols], row stride ldx elements; q row stride ldq
+ * bytes.  cols % 8 == 0, ldx % 8 == 0, ldq % 16 == 0. */
+int qie_quantize_rows_fp8(const void* x, int64_t ldx, int64_t rows, int64_t cols, void* q, int64_t ldq,
+                          void* exps, void* stream);
 int qie_fp8_tile16(const void* w_fp8, int64_t rows, int64_t cols, void* out, void* stream);
 /* Test probe: out_dev[i] = the device decode of e4m3 code i (i < 256). */
 int qie_debug_fp8_decode(float* out_dev);

@@ -51,6 +51,9 @@ def lib():
             "or_sample_ref": (C.c_int, [P, I64, C.c_int, F, F, C.c_uint64]),
             "or_curand_uniform_first": (F, [C.c_uint64]),
             "or_set_sum_order": (None, [C.c_int]),
+            "or_set_act_fp8": (None, [C.c_int]),
+            "or_quant_rows_fp8": (None, [P, C.c_int64, C.c_int64, P]),
+            "or_e4m3_round": (C.c_float, [C.c_float]),
             "or_set_layer_dump": (None, [P]),
             "or_forward": (C.c_int, [C.POINTER(qlib.ModelSpecC), C.POINTER(qlib.ModelWeightsC), P, P,
                                      C.c_int, P, C.c_int, C.c_int, P, P, C.c_int]),
@@ -161,6 +164,16 @@ def set_sum_order(v: int) -> None:
     lib().or_set_sum_order(int(v))
 
 
+def quant_rows_fp8(x):
+    """Per-row e4m3 activation quantisation (or_quant_rows_fp8): (dequantised bf16 rows,
+    exponents e with scale 2^e)."""
+    x = np.array(x, np.uint16, copy=True, order="C")
+    rows, cols = x.shape
+    e = np.zeros(rows, np.int32)
+    lib().or_quant_rows_fp8(_p(x), rows, cols, _p(e))
+    return x, e
+
+
 def argmax(logits) -> int:
     logits = np.ascontiguousarray(logits, np.uint16)
     return lib().or_argmax_ref(_p(logits), logits.size)
@@ -174,8 +187,9 @@ def sample(logits, k, temperature, top_p=1.0, seed=1234) -> int:
 class Model:
     """Full reference-semantics forward (or_forward) over a HostWeights checkpoint."""
 
-    def __init__(self, hw, max_ctx: int, nthreads: int = 0):
+    def __init__(self, hw, max_ctx: int, nthreads: int = 0, prefill_act_fp8: bool = False):
         from qwen_inference_engine_amd.engine import weights_struct
+        self.prefill_act_fp8 = prefill_act_fp8   # the engine's prefill_fp8 numerics (or_set_act_fp8)
         self.hw = hw
         self.spec = hw.spec
         self.max_ctx = max_ctx
@@ -194,8 +208,15 @@ class Model:
         sp = self.pos if start_pos is None else start_pos
         logits = np.zeros(self.spec.vocab, np.uint16)
         hidden = np.zeros(self.spec.hidden, np.uint16)
-        rc = lib().or_forward(C.byref(self._spec_c), C.byref(self._w), _p(self.k), _p(self.v), self.max_ctx,
-                              _p(ids), ids.size, sp, _p(logits), _p(hidden), self.nthreads)
+        q8 = self.prefill_act_fp8 and sp == 0   # the prefill call (decode steps keep bf16 activations)
+        if q8:
+            lib().or_set_act_fp8(1)
+        try:
+            rc = lib().or_forward(C.byref(self._spec_c), C.byref(self._w), _p(self.k), _p(self.v), self.max_ctx,
+                                  _p(ids), ids.size, sp, _p(logits), _p(hidden), self.nthreads)
+        finally:
+            if q8:
+                lib().or_set_act_fp8(0)
         if rc != 0:
             raise RuntimeError("or_forward failed")
         self.pos = sp + ids.size

@@ -698,6 +698,60 @@ int or_sample_ref(const bf16_t* logits, int64_t V, int k, float temperature, flo
 /* Parity diagnostics (tools/flip_attrib.py): when set, or_forward copies the LAST token's
  * residual row into dump[slot][H] — slot 0 after the embedding, 2l + 1 after layer l's
  * attention residual, 2l + 2 after its MLP residual (the engine's qie_batch_debug_step). */
+/* fp8 activations (the engine's opts.prefill_fp8, QIE_LINEAR_ACT_FP8 in qie_ops.h): when set,
+ * or_forward replaces the input rows of each layer projection (QKV, O, gate/up, down) by their
+ * per-row e4m3 quantisation — s = the smallest power of two with max|x| / s <= 448 (1 for a
+ * zero row), x -> e4m3_rne(x / s) * s — before the (unchanged) matmul.  The rounding is
+ * restated from the OCP e4m3fn value set itself (nearest representable value, ties to the
+ * even code), independently of the engine's encoder.  Every dequantised value is a bf16. */
+static int g_act_fp8 = 0;
+void or_set_act_fp8(int v) { g_act_fp8 = v; }
+
+static float e4m3_value(int code) {   // non-negative codes 0..0x7E
+    const int ex = (code >> 3) & 15, man = code & 7;
+    return ex == 0 ? (float)man * 0.001953125f : std::ldexp(1.0f + (float)man / 8.0f, ex - 7);
+}
+
+float or_e4m3_round(float x) {   // nearest e4m3fn value (|x| <= 448), ties to even code
+    const float a = std::fabs(x);
+    int lo = 0, hi = 0x7E;
+    while (hi - lo > 1) {   // e4m3_value is increasing in the code over 0..0x7E
+        const int mid = (lo + hi) / 2;
+        if (e4m3_value(mid) <= a) lo = mid;
+        else hi = mid;
+    }
+    const float vl = e4m3_value(lo), vh = e4m3_value(hi);
+    float r;
+    if (a <= vl) r = vl;
+    else if (a >= vh) r = vh;
+    else {
+        const double dl = (double)a - vl, dh = (double)vh - a;
+        r = dl < dh ? vl : (dh < dl ? vh : ((lo & 1) == 0 ? vl : vh));
+    }
+    return x < 0 ? -r : r;
+}
+
+void or_quant_rows_fp8(bf16_t* x, int64_t rows, int64_t cols, int32_t* exps) {
+    for (int64_t r = 0; r < rows; r++) {
+        bf16_t* xr = x + r * cols;
+        float amax = 0.f;
+        for (int64_t c = 0; c < cols; c++) amax = std::max(amax, std::fabs(bf2f(xr[c])));
+        int e = 0;
+        if (amax > 0.f) {
+            int E;
+            std::frexp(amax, &E);
+            e = E - 9;
+            while (std::ldexp(448.0, e) < (double)amax) e++;
+            while (std::ldexp(448.0, e - 1) >= (double)amax) e--;
+        }
+        if (exps) exps[r] = e;
+        for (int64_t c = 0; c < cols; c++) {
+            const float q = or_e4m3_round((float)std::ldexp((double)bf2f(xr[c]), -e));
+            xr[c] = f2bf((float)std::ldexp((double)q, e));
+        }
+    }
+}
+
 static bf16_t* g_layer_dump = nullptr;
 void or_set_layer_dump(bf16_t* dump) { g_layer_dump = dump; }
 
@@ -730,6 +784,7 @@ int or_forward(const qie_model_spec* s, const qie_model_weights* w, bf16_t* kcac
     for (int64_t l = 0; l < L; l++) {
         const qie_layer_weights& lw = w->layers[l];
         or_rmsnorm(x.data(), (const bf16_t*)lw.attn_norm, hn.data(), n, H, s->rms_eps, num);
+        if (g_act_fp8) or_quant_rows_fp8(hn.data(), n, H, nullptr);
         or_matmul(hn.data(), (const bf16_t*)lw.wq, (const bf16_t*)lw.bq, q.data(), n, H, QD, nthreads);
         or_matmul(hn.data(), (const bf16_t*)lw.wk, (const bf16_t*)lw.bk, k.data(), n, H, KD, nthreads);
         or_matmul(hn.data(), (const bf16_t*)lw.wv, (const bf16_t*)lw.bv, v.data(), n, H, KD, nthreads);
@@ -750,13 +805,16 @@ int or_forward(const qie_model_spec* s, const qie_model_weights* w, bf16_t* kcac
             }
         or_attention_nm(q.data(), kl, vl, att.data(), n, ctx, (int)nq, (int)nkv, (int)hd,
                         /*causal=*/1, start_pos, head_stride, nthreads, num);
+        if (g_act_fp8) or_quant_rows_fp8(att.data(), n, QD, nullptr);
         or_matmul(att.data(), (const bf16_t*)lw.wo, nullptr, tmp.data(), n, QD, H, nthreads);
         or_resadd(x.data(), tmp.data(), (int64_t)n * H);
         dump(2 * l + 1);
         or_rmsnorm(x.data(), (const bf16_t*)lw.ffn_norm, hn.data(), n, H, s->rms_eps, num);
+        if (g_act_fp8) or_quant_rows_fp8(hn.data(), n, H, nullptr);
         or_matmul(hn.data(), (const bf16_t*)lw.w_up, nullptr, up.data(), n, H, I, nthreads);
         or_matmul(hn.data(), (const bf16_t*)lw.w_gate, nullptr, gate.data(), n, H, I, nthreads);
         or_silu_mul(gate.data(), up.data(), hm.data(), (int64_t)n * I);
+        if (g_act_fp8) or_quant_rows_fp8(hm.data(), n, I, nullptr);
         or_matmul(hm.data(), (const bf16_t*)lw.w_down, nullptr, tmp.data(), n, I, H, nthreads);
         or_resadd(x.data(), tmp.data(), (int64_t)n * H);
         dump(2 * l + 2);

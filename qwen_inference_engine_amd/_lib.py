@@ -25,6 +25,7 @@ QIE_LINEAR_TILE256 = 2
 QIE_LINEAR_TILE128 = 4
 QIE_LINEAR_STREAMK = 8
 QIE_LINEAR_FP8_T16 = 16
+QIE_LINEAR_ACT_FP8 = 32
 QIE_ATTN_PREROPED = 0x100   # qie_attention_decode numerics flag: q / new k arrive rotated
 QIE_COMM_ID_BYTES = 128
 QIE_COMM_PEER_HANDLE_BYTES = 128
@@ -62,7 +63,7 @@ class LinearArgsC(C.Structure):
         ("seg_rows", C.c_int64 * 3), ("M", C.c_int64), ("K", C.c_int64), ("N", C.c_int64),
         ("y", C.c_void_p), ("ldy", C.c_int64), ("epilogue", C.c_int32), ("numerics", C.c_int32),
         ("norm_w", C.c_void_p), ("norm_eps", C.c_float), ("flags", C.c_int32),
-        ("argmax_keys", C.c_void_p), ("key_col0", C.c_int64),
+        ("argmax_keys", C.c_void_p), ("key_col0", C.c_int64), ("x_exps", C.c_void_p),
     ]
 
 
@@ -76,7 +77,8 @@ class KvCacheC(C.Structure):
 class EngineOptsC(C.Structure):
     _fields_ = [("device", C.c_int32), ("max_ctx", C.c_int32), ("use_graph", C.c_int32),
                 ("tp_rank", C.c_int32), ("tp_size", C.c_int32), ("tp_comm", C.c_void_p),
-                ("weight_fp8", C.c_int32), ("comm_always", C.c_int32), ("reserved", C.c_int32 * 6)]
+                ("weight_fp8", C.c_int32), ("comm_always", C.c_int32), ("prefill_fp8", C.c_int32),
+                ("reserved", C.c_int32 * 5)]
 
 
 # (name, restype, argtypes) — every symbol the public headers declare.
@@ -133,6 +135,7 @@ SIGNATURES = [
     ("qie_scale_rows_pow2", C.c_int, [_P, _I64, _I64, _I64, _I64, _I32, _P]),
     ("qie_fp8_weight_bytes", C.c_int64, [_I64, _I64]),
     ("qie_quantize_fp8", C.c_int, [_P, _I64, _I64, _P, _P]),
+    ("qie_quantize_rows_fp8", C.c_int, [_P, _I64, _I64, _I64, _P, _I64, _P, _P]),
     ("qie_quantize_fp8_host", C.c_int, [_P, _I64, _I64, _P]),
     ("qie_dequantize_fp8", C.c_int, [_P, _I64, _I64, _P, _P]),
     ("qie_fp8_tile16", C.c_int, [_P, _I64, _I64, _P, _P]),

@@ -130,6 +130,7 @@ struct qie_batch {
     uint16_t *pf_x = nullptr, *pf_hn = nullptr, *pf_qkv = nullptr, *pf_q = nullptr, *pf_att = nullptr,
              *pf_h = nullptr;
     int32_t *pf_pos = nullptr, *pf_ids = nullptr;
+    uint8_t *pf_q8 = nullptr, *pf_e8 = nullptr;   // fp8 prefill (opts.prefill_fp8): codes [rows][max K], exps [rows]
     void* pf_attn_ws = nullptr;
     int64_t pf_attn_ws_bytes = 0;   // the split workspace depends on n (short prompts split), not on n <= pf_rows
     // paged KV (qie_batch_create_paged): pool pages of page_tokens tokens, block table
@@ -652,6 +653,14 @@ static int enqueue_decode(qie_batch* b, const qie_sampling* smp) {
     return enqueue_head(b, b->x_res, b->e->spec.hidden, 0, b->B, smp);
 }
 
+// opts.prefill_fp8 (numerics flag): the prefill projections on the block-scaled fp8 MFMA
+// GEMM (QIE_LINEAR_ACT_FP8) — fp8 weights in the engine's arena, every projection input
+// quantised per row (qie_quantize_rows_fp8), K of each a multiple of 128
+static bool prefill_mx(const qie_engine* e) {
+    const int64_t H = e->spec.hidden, QD = (int64_t)e->sh.nq * e->spec.head_dim, I = e->sh.ffn;
+    return e->fp8 && e->opts.prefill_fp8 && H % 128 == 0 && QD % 128 == 0 && I % 128 == 0;
+}
+
 static int ensure_prefill_scratch(qie_batch* b, int64_t n) {
     if (n <= b->pf_rows) {
         // rows fit; the attention workspace is not monotone in n (<= 8 rows run the split
@@ -671,7 +680,8 @@ static int ensure_prefill_scratch(qie_batch* b, int64_t n) {
     const TpShard& sh = b->e->sh;
     const int64_t H = s.hidden, QD = (int64_t)sh.nq * s.head_dim, KD = (int64_t)sh.nkv * s.head_dim;
     void** olds[] = {(void**)&b->pf_x, (void**)&b->pf_hn, (void**)&b->pf_qkv, (void**)&b->pf_q, (void**)&b->pf_att,
-                     (void**)&b->pf_h, (void**)&b->pf_pos, (void**)&b->pf_ids, &b->pf_attn_ws, (void**)&b->pf_part};
+                     (void**)&b->pf_h, (void**)&b->pf_pos, (void**)&b->pf_ids, &b->pf_attn_ws, (void**)&b->pf_part,
+                     (void**)&b->pf_q8, (void**)&b->pf_e8};
     for (void** p : olds) {   // nulled as freed: a failed re-allocation below leaves nothing dangling
         if (*p) hipFree(*p);
         *p = nullptr;
@@ -684,6 +694,11 @@ static int ensure_prefill_scratch(qie_batch* b, int64_t n) {
     QIE_TRY(dmalloc((void**)&b->pf_q, n * QD * 2));
     QIE_TRY(dmalloc((void**)&b->pf_att, n * QD * 2));
     QIE_TRY(dmalloc((void**)&b->pf_h, n * (int64_t)sh.ffn * 2));
+    if (prefill_mx(b->e)) {
+        const int64_t kmax = std::max<int64_t>(std::max<int64_t>(H, QD), sh.ffn);
+        QIE_TRY(dmalloc((void**)&b->pf_q8, n * kmax));
+        QIE_TRY(dmalloc((void**)&b->pf_e8, std::max<int64_t>(n, 16)));
+    }
     QIE_TRY(dmalloc((void**)&b->pf_pos, n * 4));
     QIE_TRY(dmalloc((void**)&b->pf_ids, n * 4));
     b->pf_attn_ws = nullptr;
@@ -1181,7 +1196,7 @@ void qie_batch_destroy(qie_batch* b) {
     void* ps[] = {b->kc, b->vc, b->d_table, b->d_pos, b->d_rope_cur, b->d_step, b->d_hist, b->d_ids, b->d_keys, b->x_res, b->qkv, b->q,
                   b->att, b->h, b->logits, b->attn_ws, b->dec_ws, b->samp_ws, b->pf_x, b->pf_hn, b->pf_qkv, b->pf_q,
                   b->pf_att, b->pf_h, b->pf_pos, b->pf_ids, b->pf_attn_ws, b->part, b->logits_full,
-                  b->gather_tmp, b->pf_part, b->xn};
+                  b->gather_tmp, b->pf_part, b->xn, b->pf_q8, b->pf_e8};
     for (void* p : ps)
         if (p) hipFree(p);
     delete b;
@@ -1238,7 +1253,47 @@ static int prefill_rows(qie_batch* b, int seq0, int n_seqs, const int32_t* ids, 
         if (pf16) a.flags &= ~(QIE_LINEAR_FP8 | QIE_LINEAR_FP8_T16);
         return a;
     };
+    const bool mx = prefill_mx(e);
+    // fp8 activations: quantise the projection input x [n][K] (bf16) into pf_q8 / pf_e8 and
+    // point the linear at the codes
+    auto mx_in = [&](qie_linear_args& a, const uint16_t* x, int64_t K) -> int {
+        QIE_TRY(qie_quantize_rows_fp8(x, K, n, K, b->pf_q8, K, b->pf_e8, st));
+        a.x = b->pf_q8; a.ldx = K; a.x_exps = b->pf_e8;
+        a.flags |= QIE_LINEAR_ACT_FP8;
+        return 0;
+    };
     for (int l = 0; l < s.n_layers; l++) {
+        if (mx) {   // every projection on fp8 codes x fp8 weights (e->layers: the fp8 arena)
+            const qie_layer_weights& L = e->layers[l];
+            QIE_TRY(qie_rmsnorm(b->pf_x, L.attn_norm, b->pf_hn, n, H, s.rms_eps, s.numerics, st));
+            qie_linear_args a = lin_proj(e);
+            QIE_TRY(mx_in(a, b->pf_hn, H));
+            a.w[0] = L.wq; a.w[1] = L.wk; a.w[2] = L.wv;
+            a.bias[0] = L.bq; a.bias[1] = L.bk; a.bias[2] = L.bv;
+            a.seg_rows[0] = QD; a.seg_rows[1] = KD; a.seg_rows[2] = KD;
+            a.M = n; a.K = H; a.N = QKVD; a.y = b->pf_qkv; a.ldy = QKVD; a.epilogue = QIE_EPI_STORE;
+            QIE_TRY(qie_linear(&a, st));
+            QIE_TRY(qie_qkv_post(b->pf_qkv, n, b->pf_pos, len, L.q_norm, L.k_norm, e->rope_cos, e->rope_sin, sh.nq,
+                                 &cache, l, s.rms_eps, s.numerics, b->pf_q, st));
+            QIE_TRY(qie_attention(b->pf_q, n, b->pf_pos, len, &cache, l, sh.nq, b->pf_att, b->pf_attn_ws, st));
+            a = lin_proj(e);
+            QIE_TRY(mx_in(a, b->pf_att, QD));
+            a.w[0] = L.wo; a.seg_rows[0] = H;
+            a.M = n; a.K = QD; a.N = H; a.ldy = H;
+            QIE_TRY(row_parallel(b, a, b->pf_x, b->pf_part, n));
+            QIE_TRY(qie_rmsnorm(b->pf_x, L.ffn_norm, b->pf_hn, n, H, s.rms_eps, s.numerics, st));
+            a = lin_proj(e);
+            QIE_TRY(mx_in(a, b->pf_hn, H));
+            a.w[0] = L.w_gate; a.w[1] = L.w_up; a.seg_rows[0] = I; a.seg_rows[1] = I;
+            a.M = n; a.K = H; a.N = I; a.y = b->pf_h; a.ldy = I; a.epilogue = QIE_EPI_SWIGLU;
+            QIE_TRY(qie_linear(&a, st));
+            a = lin_proj(e);
+            QIE_TRY(mx_in(a, b->pf_h, I));
+            a.w[0] = L.w_down; a.seg_rows[0] = H;
+            a.M = n; a.K = I; a.N = H; a.ldy = H;
+            QIE_TRY(row_parallel(b, a, b->pf_x, b->pf_part, n));
+            continue;
+        }
         const qie_layer_weights& L = pf16 ? e->layers_pf[l] : e->layers[l];
         QIE_TRY(qie_rmsnorm(b->pf_x, L.attn_norm, b->pf_hn, n, H, s.rms_eps, s.numerics, st));
         qie_linear_args a = pf_base();
@@ -1614,14 +1669,16 @@ int qie_linear(const qie_linear_args* a, void* stream) {
     QIE_REQUIRE(a->epilogue != QIE_EPI_F32 || (a->bias[0] == nullptr && a->bias[1] == nullptr && a->bias[2] == nullptr),
                 "qie_linear: F32 (partial-sum) epilogue takes no bias");
     QIE_REQUIRE(a->argmax_keys == nullptr || a->epilogue == QIE_EPI_STORE, "qie_linear: arg-max needs STORE");
+    const bool act_fp8 = (a->flags & QIE_LINEAR_ACT_FP8) != 0;
+    hipStream_t st = (hipStream_t)stream;
+    if (act_fp8) return gemm(a, st);   // fp8 activations: the block-scaled MFMA GEMM at every M
     QIE_REQUIRE(!(a->flags & QIE_LINEAR_FP8_T16) ||
                     ((a->flags & QIE_LINEAR_FP8) && a->M >= 1 && a->M <= 16 && a->K % 64 == 0 &&
                      (a->epilogue == QIE_EPI_SWIGLU ? a->N % 16 == 0
                                                     : a->seg_rows[0] % 16 == 0 && a->seg_rows[1] % 16 == 0 &&
                                                           a->seg_rows[2] % 16 == 0)),
                 "qie_linear: 16-row tiled fp8 weights are read by the batched-decode kernels only (M <= 16, K %% 64 == 0, "
-                "segments of whole 16-row tiles)");
-    hipStream_t st = (hipStream_t)stream;
+                "segments of whole 16-row tiles) and, with fp8 activations, the block-scaled GEMM");
     if (a->M <= 16) return gemv(a, st);   // GEMV (M = 1..8) or the skinny MFMA kernel (2..16)
     return gemm(a, st);
 }

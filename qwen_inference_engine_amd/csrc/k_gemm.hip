@@ -1127,7 +1127,403 @@ static int launch_gemm(int epi, unsigned gm, const GemmParams& p, size_t shm, hi
     return 0;
 }
 
+// ---------------------------------------------------------------------------
+// Block-scaled fp8 prefill GEMM (round 5; BASELINE config 4's "CDNA4 fp8 MFMA", numerics flag
+// QIE_LINEAR_ACT_FP8):  C[m, n] = sum_k (2^ea[m] qa[m, k]) (sw[n] qw[n, k])  with e4m3
+// activation codes qa and per-row power-of-two exponents ea (qie_quantize_rows_fp8), e4m3
+// weight codes qw with power-of-two row scales sw (the engine's fp8 arena, plain or 16-row
+// tiled).  Both scales are row constants, so they enter v_mfma_scale_f32_16x16x128_f8f6f4 as
+// its per-lane e8m0 operands (every lane of an A row / B column passes the same byte) and the
+// accumulators come out scaled: the epilogues are gemm8's.  The product of two e4m3 values is
+// exact; the instruction's K = 128 per step doubles the bf16 rate per clock (MI355X_MICROARCH
+// "Matrix cores": twice the cycles of the bf16 16x16 form at 4x the K).
+//   Structure = gemm8_kernel's (256x256 tile, 8 waves 2 x 4, four phases per k-tile, LDS-DMA
+// units in read order, waves 4-7 one barrier behind): a k-tile is BK = 128 codes, i.e. the
+// same 128-B LDS rows as gemm8's 64 bf16, so the buffers, unit schedule, swizzle and waits are
+// unchanged; a fragment is 32 codes (chunks 2g, 2g + 1 of the row: k = 32 g + [0, 32), the
+// 16x16x128 lane map) and a phase issues 8 MFMAs of twice the cycles instead of 16.
+// Tiled weights (QIE_LINEAR_FP8_T16) are gathered straight from their 1-KiB blocks by the
+// per-lane DMA addresses (chunk c of row r: block (r / 16, c / 4), bytes 16 ((r % 16) +
+// 16 (c % 4))), so the decode layout is the prefill's too — no bf16 copy is read.
+namespace mx {
+constexpr int BK = 128;   // codes per k-tile row (128 B)
+}
+
+struct MxParams {
+    const uint8_t* A;     // [M][lda] e4m3 codes
+    int64_t lda;          // bytes
+    const uint8_t* ea;    // [M] e8m0 row exponents
+    const uint8_t* w[3];  // fp8 segments: codes, then fp32 row scales
+    const uint16_t* b[3];
+    int64_t rows[3];      // segment rows
+    int64_t n0, n01;
+    int64_t M, K, N;
+    uint16_t* C;
+    int64_t ldc;
+};
+
+// segment, row-in-segment of tile column c (0..255) of column tile nt (big_wrow's mapping)
+template <int EPI>
+__device__ __forceinline__ int mx_wrow(const MxParams& p, int64_t nt, int c, int64_t& r) {
+    if constexpr (EPI == QIE_EPI_SWIGLU) {
+        const int ws = c / 64, q = c % 64;
+        const int64_t j = nt * 128 + ws * 32 + (q % 32);
+        r = j < p.N ? j : p.N - 1;
+        return q >= 32 ? 1 : 0;
+    } else {
+        int64_t rr = nt * 256 + c;
+        rr = rr < p.N ? rr : p.N - 1;
+        if (rr < p.n0) { r = rr; return 0; }
+        if (rr < p.n01) { r = rr - p.n0; return 1; }
+        r = rr - p.n01;
+        return 2;
+    }
+}
+
+typedef int i32x8_mx __attribute__((ext_vector_type(8)));
+
+template <int EPI, bool T16>
+__global__ __launch_bounds__(512) void gemm8mx_kernel(MxParams p, int n_mt, G8Split sk) {
+#pragma clang fp contract(off)
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    const int fr = lane & 15, g = lane >> 4;
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int q8 = nwg >> 3, r8 = nwg & 7, xcd = orig & 7;
+    const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+    const int tile = wid / sk.splitk, part = wid % sk.splitk;
+    const int64_t mt = tile % n_mt, nt = tile / n_mt;
+    const int64_t m0 = mt * g8::BM;
+    const int64_t K = p.K;
+
+    // e8m0 operands, packed 4 per register (byte i of sa_pk[qa]: A row 128 wm + 64 qa + 16 i +
+    // fr; byte 2 qb + j of sb_pk: B tile column 64 wn + 32 qb + 16 j + fr -> the exponent of the
+    // weight row's power-of-two scale): 3 VGPRs, the budget gemm8's 254 leaves
+    uint32_t sa_pk[2] = {0u, 0u}, sb_pk = 0u;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        int64_t ar = m0 + 128 * wm + 16 * q + fr;
+        ar = ar < p.M ? ar : p.M - 1;
+        sa_pk[q >> 2] |= (uint32_t)p.ea[ar] << (8 * (q & 3));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        int64_t r;
+        const int sg = mx_wrow<EPI>(p, nt, 64 * wn + 16 * j + fr, r);
+        const uint8_t* base = sg == 0 ? p.w[0] : (sg == 1 ? p.w[1] : p.w[2]);
+        const int64_t rows = sg == 0 ? p.rows[0] : (sg == 1 ? p.rows[1] : p.rows[2]);
+        const uint32_t bits = __float_as_uint(reinterpret_cast<const float*>(base + rows * K)[r]);
+        sb_pk |= ((bits >> 23) & 0xffu) << (8 * j);
+    }
+    // the exponents are waited for here, once: an opaque register pin makes them values of
+    // this point, so no wait for them is left inside the DMA-pipelined loop
+    asm volatile("" : "+v"(sa_pk[0]), "+v"(sa_pk[1]), "+v"(sb_pk));
+
+    // DMA sources (gemm8's units and rows): A as 32-bit row offsets from p.A (4 VGPRs), W as
+    // pointers (segments may lie anywhere)
+    uint32_t aoff[2][2];
+    const uint8_t* wsrc[2][2];
+    int dst_row[4][2];
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const int b = 2 * wave + i;
+            int row0;
+            if (u == 0 || u == 3) row0 = (b < 8 ? 8 * b : 128 + 8 * (b - 8)) + (u == 3 ? 64 : 0);
+            else row0 = 64 * (b >> 2) + 8 * (b & 3) + (u == 2 ? 32 : 0);
+            dst_row[u][i] = row0;
+            const int rw = row0 + (lane >> 3);
+            const int cs = (lane & 7) ^ g8_swz(rw);
+            if (u == 0 || u == 3) {
+                int64_t ar = m0 + rw;
+                ar = ar < p.M ? ar : p.M - 1;   // rows past M: re-read row M-1, never stored
+                aoff[u == 3][i] = (uint32_t)(ar * p.lda + cs * 16);
+            } else {
+                int64_t r;
+                const int sg = mx_wrow<EPI>(p, nt, rw, r);
+                const uint8_t* base = sg == 0 ? p.w[0] : (sg == 1 ? p.w[1] : p.w[2]);
+                if constexpr (T16)
+                    wsrc[u - 1][i] = base + (r >> 4) * 16 * K + (cs >> 2) * 1024 + 16 * ((r & 15) + 16 * (cs & 3));
+                else
+                    wsrc[u - 1][i] = base + r * K + cs * 16;
+            }
+        }
+    constexpr int64_t WSTEP = T16 ? 2048 : mx::BK;   // weight bytes per k-tile
+    const int nk_all = (int)(K / mx::BK);
+    const int kb = (int)((int64_t)part * nk_all / sk.splitk);
+    const int nk = (int)((int64_t)(part + 1) * nk_all / sk.splitk) - kb;
+    auto stage = [&](int u, int kt) {
+        unsigned char* buf = smem + (kt & 1) * g8::BUF + ((u == 0 || u == 3) ? 0 : g8::BM * 128);
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            if (u == 0 || u == 3)
+                glds16(p.A + (int64_t)(kb + kt) * mx::BK + aoff[u == 3][i], buf + dst_row[u][i] * 128);
+            else
+                glds16(wsrc[u - 1][i] + (int64_t)(kb + kt) * WSTEP, buf + dst_row[u][i] * 128);
+        }
+    };
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    i32x8_mx fa[4], fb0[2], fb1[2];
+
+    auto frag = [&](const unsigned char* rowp, int row) -> i32x8_mx {
+        const u32x4_g8 lo = *reinterpret_cast<const u32x4_g8*>(rowp + (((2 * g) ^ g8_swz(row)) * 16));
+        const u32x4_g8 hi = *reinterpret_cast<const u32x4_g8*>(rowp + (((2 * g + 1) ^ g8_swz(row)) * 16));
+        return i32x8_mx{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    };
+    auto read_a = [&](const unsigned char* buf, int qa) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int row = 128 * wm + 64 * qa + 16 * i + fr;
+            fa[i] = frag(buf + row * 128, row);
+        }
+    };
+    auto read_b = [&](const unsigned char* buf, int qb, i32x8_mx (&fb)[2]) {
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int row = 64 * wn + 32 * qb + 16 * j + fr;
+            fb[j] = frag(buf + g8::BM * 128 + row * 128, row);
+        }
+    };
+    auto mfma_q = [&](int qa, int qb, const i32x8_mx (&fb)[2]) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int j = 0; j < 2; j++)
+                acc[4 * qa + i][2 * qb + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                    fa[i], fb[j], acc[4 * qa + i][2 * qb + j], 0, 0, 0, (int)((sa_pk[qa] >> (8 * i)) & 0xffu), 0,
+                    (int)((sb_pk >> (8 * (2 * qb + j))) & 0xffu));
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto bar = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto wait8 = [&](bool tail) {
+        if (tail) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    };
+
+    // prologue (gemm8's): UA0(0) UB0(0) UB1(0) UA1(0) UA0(1) UB0(1)
+    stage(0, 0); stage(1, 0); stage(2, 0); stage(3, 0);
+    if (nk > 1) { stage(0, 1); stage(1, 1); }
+    if (nk > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    if (wm == 1) bar();
+    for (int t = 0; t < nk; t++) {
+        const unsigned char* buf = smem + (t & 1) * g8::BUF;
+        const bool tail = t >= nk - 2;
+        // keep the packed exponents loop-variant: the byte extractions stay next to their
+        // MFMAs instead of being hoisted into 12 registers live across the loop
+        asm volatile("" : "+v"(sa_pk[0]), "+v"(sa_pk[1]), "+v"(sb_pk));
+        read_b(buf, 0, fb0);
+        __builtin_amdgcn_sched_barrier(0);
+        read_a(buf, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + 1 < nk) stage(2, t + 1);
+        wait8(tail);
+        bar();
+        mfma_q(0, 0, fb0);
+        bar();
+        read_b(buf, 1, fb1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + 1 < nk) stage(3, t + 1);
+        wait8(tail);
+        bar();
+        mfma_q(0, 1, fb1);
+        bar();
+        read_a(buf, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + 2 < nk) stage(0, t + 2);
+        bar();
+        mfma_q(1, 1, fb1);
+        bar();
+        if (t + 2 < nk) stage(1, t + 2);
+        wait8(tail);
+        bar();
+        mfma_q(1, 0, fb0);
+        bar();
+    }
+    if (wm == 0) bar();
+
+    if (sk.splitk > 1) {   // uniform (gemm8's split-K hand-off, part order)
+        const int64_t tb = (int64_t)tile * sk.splitk;
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(sk.slab + (tb + part) * 65536, (short)0, 65536 * 4, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_g8, acc[i][j]), rs,
+                                                       ((wave * 32 + i * 4 + j) * 64 + lane) * 16, 0, 16);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        int* flag = reinterpret_cast<int*>(smem);
+        if (tid == 0) {
+            const unsigned old = __hip_atomic_fetch_add(sk.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            *flag = old == (unsigned)sk.splitk - 1 ? 1 : 0;
+        }
+        __syncthreads();
+        if (*flag == 0) return;
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int q = 0; q < sk.splitk; q++) {
+            const auto rq = __builtin_amdgcn_make_buffer_rsrc(sk.slab + (tb + q) * 65536, (short)0, 65536 * 4, 0x00020000);
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                  rq, ((wave * 32 + i * 4 + j) * 64 + lane) * 16, 0, 16));
+                    acc[i][j] = q == 0 ? v : acc[i][j] + v;
+                }
+        }
+        if (tid == 0) __hip_atomic_store(sk.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+
+    // ---------------- epilogue (gemm8_kernel's)
+    constexpr int NJ = 4;
+    if constexpr (EPI == QIE_EPI_SWIGLU) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+#pragma unroll
+            for (int jj = 0; jj < NJ / 2; jj++) {
+                const int64_t col = nt * 128 + 32 * wn + 16 * jj + fr;
+                if (col >= p.N) continue;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int64_t row = m0 + wm * 128 + i * 16 + g * 4 + r;
+                    if (row >= p.M) continue;
+                    const float gg = rbf(acc[i][jj][r]);
+                    const float uu = rbf(acc[i][jj + NJ / 2][r]);
+                    const float av = rbf(gg * (1.0f / (1.0f + expf(-gg))));
+                    p.C[row * p.ldc + col] = f2bf(uu * av);
+                }
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < NJ; j++) {
+            const int64_t col = nt * 256 + wn * 64 + j * 16 + fr;
+            if (col >= p.N) continue;
+            float bias = 0.f;
+            if constexpr (EPI == QIE_EPI_STORE) {
+                const uint16_t* b = col < p.n0 ? p.b[0] : (col < p.n01 ? p.b[1] : p.b[2]);
+                if (b) bias = bf2f(b[col < p.n0 ? col : (col < p.n01 ? col - p.n0 : col - p.n01)]);
+            }
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int64_t row = m0 + wm * 128 + i * 16 + g * 4 + r;
+                    if (row >= p.M) continue;
+                    if constexpr (EPI == QIE_EPI_F32) {
+                        reinterpret_cast<float*>(p.C)[row * p.ldc + col] = acc[i][j][r];
+                        continue;
+                    }
+                    uint16_t* dst = p.C + row * p.ldc + col;
+                    if constexpr (EPI == QIE_EPI_RESIDUAL)
+                        *dst = f2bf(bf2f(*dst) + rbf(acc[i][j][r]));
+                    else
+                        *dst = f2bf(acc[i][j][r] + bias);
+                }
+            }
+        }
+    }
+}
+
+template <int EPI, bool T16>
+static int launch_gemm8mx_t(const MxParams& p, int n_mt, int n_tiles, const G8Split& sk, hipStream_t st) {
+    const void* fn = (const void*)gemm8mx_kernel<EPI, T16>;
+    constexpr size_t shm = 2 * (size_t)g8::BUF;
+    static bool raised = false;
+    if (!raised) {
+        QIE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+        raised = true;
+    }
+    hipLaunchKernelGGL((gemm8mx_kernel<EPI, T16>), dim3((unsigned)(n_tiles * sk.splitk)), dim3(512), shm, st, p, n_mt,
+                       sk);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+template <bool T16>
+static int launch_gemm8mx(int epi, const MxParams& p, int n_mt, int n_tiles, const G8Split& sk, hipStream_t st) {
+    if (epi == QIE_EPI_SWIGLU) return launch_gemm8mx_t<QIE_EPI_SWIGLU, T16>(p, n_mt, n_tiles, sk, st);
+    if (epi == QIE_EPI_RESIDUAL) return launch_gemm8mx_t<QIE_EPI_RESIDUAL, T16>(p, n_mt, n_tiles, sk, st);
+    if (epi == QIE_EPI_F32) return launch_gemm8mx_t<QIE_EPI_F32, T16>(p, n_mt, n_tiles, sk, st);
+    return launch_gemm8mx_t<QIE_EPI_STORE, T16>(p, n_mt, n_tiles, sk, st);
+}
+
+// QIE_LINEAR_ACT_FP8 (qie_ops.h): every M, one 256x256 kernel; split-K where the tiles do not
+// fill the chip once (the fewest rounds of (tile, part) items; parts of >= 8 k-tiles)
+static int gemm_mx(const qie_linear_args* a, hipStream_t st) {
+    const bool t16 = (a->flags & QIE_LINEAR_FP8_T16) != 0;
+    QIE_REQUIRE((a->flags & QIE_LINEAR_FP8) && a->x_exps, "qie_linear: ACT_FP8 needs fp8 weights and x_exps");
+    QIE_REQUIRE(a->K % mx::BK == 0 && a->ldx >= a->K && a->ldx % 16 == 0,
+                "qie_linear: ACT_FP8 needs K %% 128 == 0 and ldx (bytes) %% 16 == 0");
+    QIE_REQUIRE(a->norm_w == nullptr && a->argmax_keys == nullptr, "qie_linear: ACT_FP8 takes no fused norm / arg-max");
+    if (t16)
+        QIE_REQUIRE(a->epilogue == QIE_EPI_SWIGLU ? a->N % 16 == 0
+                                                  : a->seg_rows[0] % 16 == 0 && a->seg_rows[1] % 16 == 0 &&
+                                                        a->seg_rows[2] % 16 == 0,
+                    "qie_linear: tiled fp8 segments must be whole 16-row tiles");
+    MxParams p;
+    p.A = (const uint8_t*)a->x;
+    p.lda = a->ldx;
+    p.ea = a->x_exps;
+    for (int i = 0; i < 3; i++) {
+        p.w[i] = (const uint8_t*)a->w[i];
+        p.b[i] = (const uint16_t*)a->bias[i];
+    }
+    const bool sw = a->epilogue == QIE_EPI_SWIGLU;
+    p.rows[0] = sw ? a->N : a->seg_rows[0];
+    p.rows[1] = sw ? a->N : a->seg_rows[1];
+    p.rows[2] = sw ? 0 : a->seg_rows[2];
+    p.n0 = a->seg_rows[0];
+    p.n01 = a->seg_rows[0] + a->seg_rows[1];
+    p.M = a->M;
+    p.K = a->K;
+    p.N = a->N;
+    p.C = (uint16_t*)a->y;
+    p.ldc = a->ldy;
+    const int64_t cols = sw ? 2 * a->N : a->N;
+    const int64_t n_mt = cdiv(a->M, g8::BM), tiles = n_mt * cdiv(cols, 256);
+    const int64_t cus = device_cu_count();
+    const int nk = (int)(a->K / mx::BK);
+    G8Split sk{1, nullptr, nullptr};
+    if (tiles < cus) {
+        int best = 1;
+        double best_t = 1e30;
+        const int smax = dev_env("QIE_MX_SPLITK_MAX", 4);
+        for (int s = 1; s <= smax && nk / s >= 8; s++) {
+            const double t = (double)((tiles * s + cus - 1) / cus) / s;
+            if (t < best_t - 1e-9) {
+                best_t = t;
+                best = s;
+            }
+        }
+        if (best > 1 && g8_workspace(st, (int)tiles * best, (int)tiles, &sk) == 0) sk.splitk = best;
+    }
+    return t16 ? launch_gemm8mx<true>(a->epilogue, p, (int)n_mt, (int)tiles, sk, st)
+               : launch_gemm8mx<false>(a->epilogue, p, (int)n_mt, (int)tiles, sk, st);
+}
+
 int gemm(const qie_linear_args* a, hipStream_t st) {
+    if (a->flags & QIE_LINEAR_ACT_FP8) return gemm_mx(a, st);
     QIE_REQUIRE(a->norm_w == nullptr, "qie_linear: fused RMSNorm is GEMV-only (M <= 8)");
     QIE_REQUIRE(a->argmax_keys == nullptr, "qie_linear: fused arg-max is GEMV-only (M <= 8)");
     GemmParams p;

@@ -821,6 +821,54 @@ int qie_residual_add_f32(void* x, const float* sum, int64_t n, void* stream) {
 
 int64_t qie_fp8_weight_bytes(int64_t rows, int64_t cols) { return rows * cols + rows * 4; }
 
+// Per-row activation quantisation (QIE_LINEAR_ACT_FP8): one block per row, amax pass then
+// the code pass (the row's second read hits L2); codes by v_cvt_pk_fp8_f32 (round to nearest
+// even; |x / s| <= 448 by the scale, so its saturation never acts) — checked bit for bit
+// against the oracle's table restatement of e4m3 rounding (tests/test_gpu_fp8.py).
+__global__ __launch_bounds__(256) void quantize_rows_fp8_kernel(const uint16_t* __restrict__ x, int64_t ldx,
+                                                                int64_t cols, uint8_t* __restrict__ q, int64_t ldq,
+                                                                uint8_t* __restrict__ exps) {
+    __shared__ float red[4];
+    const int64_t r = blockIdx.x, c8 = cols / 8;
+    const uint4* xr = reinterpret_cast<const uint4*>(x + r * ldx);
+    float amax = 0.f;
+    for (int64_t i = threadIdx.x; i < c8; i += 256) {
+        const uint4 v = xr[i];
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) amax = fmaxf(amax, fmaxf(fabsf(bf_lo(w[j])), fabsf(bf_hi(w[j]))));
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off, 64));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
+    __syncthreads();
+    amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    const float s = e4m3_row_scale(amax);
+    const float inv = 1.0f / s;   // exact: a power of two
+    if (threadIdx.x == 0) exps[r] = (uint8_t)((__float_as_uint(s) >> 23) & 0xffu);
+    uint2* qr = reinterpret_cast<uint2*>(q + r * ldq);
+    for (int64_t i = threadIdx.x; i < c8; i += 256) {
+        const uint4 v = xr[i];
+        int lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf_lo(v.x) * inv, bf_hi(v.x) * inv, 0, false);
+        lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf_lo(v.y) * inv, bf_hi(v.y) * inv, lo, true);
+        int hi = __builtin_amdgcn_cvt_pk_fp8_f32(bf_lo(v.z) * inv, bf_hi(v.z) * inv, 0, false);
+        hi = __builtin_amdgcn_cvt_pk_fp8_f32(bf_lo(v.w) * inv, bf_hi(v.w) * inv, hi, true);
+        qr[i] = make_uint2((uint32_t)lo, (uint32_t)hi);
+    }
+}
+
+int qie_quantize_rows_fp8(const void* x, int64_t ldx, int64_t rows, int64_t cols, void* q, int64_t ldq, void* exps,
+                          void* stream) {
+    QIE_REQUIRE(x && q && exps && rows >= 0 && cols > 0 && cols % 8 == 0 && ldx >= cols && ldx % 8 == 0 &&
+                    ldq >= cols && ldq % 16 == 0 && ((uintptr_t)x % 16) == 0 && ((uintptr_t)q % 16) == 0,
+                "qie_quantize_rows_fp8: bad arguments (cols %% 8, ldx %% 8, ldq %% 16, 16-B aligned buffers)");
+    if (rows == 0) return 0;
+    hipLaunchKernelGGL(quantize_rows_fp8_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream,
+                       (const uint16_t*)x, ldx, cols, (uint8_t*)q, ldq, (uint8_t*)exps);
+    QIE_LAUNCH_CHECK();
+    return 0;
+}
+
 int qie_quantize_fp8(const void* w_bf16, int64_t rows, int64_t cols, void* out, void* stream) {
     QIE_REQUIRE(w_bf16 && out && rows > 0 && cols > 0 && cols % 16 == 0 && ((uintptr_t)out % 16) == 0,
                 "qie_quantize_fp8: bad arguments (cols must be a multiple of 16, out 16-B aligned)");

@@ -133,7 +133,8 @@ class Comm:
 
 class Engine:
     def __init__(self, spec: ModelSpec, device: int = 0, max_ctx: int = 4096, use_graph: bool = True,
-                 comm: Optional[Comm] = None, weight_fp8: bool = False, comm_always: bool = False):
+                 comm: Optional[Comm] = None, weight_fp8: bool = False, comm_always: bool = False,
+                 prefill_fp8: bool = False):
         self.lib = _lib.load()
         self.spec = spec
         self._spec_c = spec.to_c()
@@ -143,6 +144,9 @@ class Engine:
         opts.tp_comm = comm.h if comm else None
         opts.weight_fp8 = int(weight_fp8)
         opts.comm_always = int(comm_always)   # exchange steps through comm even at world 1 (tests)
+        # numerics flag: prefill projections on the block-scaled fp8 MFMA (activations quantised
+        # per row to e4m3; needs weight_fp8) — the oracle's Model(prefill_act_fp8=True)
+        opts.prefill_fp8 = int(prefill_fp8)
         self.comm = comm
         self._fp8 = weight_fp8
         h = C.c_void_p()

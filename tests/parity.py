@@ -47,10 +47,11 @@ class OrderPair:
     order 2 (every fp32 reduction reordered), stepped in lock-step; tracks the running
     maxima of their norm-relative and absolute logit spreads."""
 
-    def __init__(self, oracle, hw, max_ctx, nthreads=0, with_spread=True):
+    def __init__(self, oracle, hw, max_ctx, nthreads=0, with_spread=True, act_fp8=False):
         self.O = oracle
-        self.m0 = oracle.Model(hw, max_ctx, nthreads=nthreads)
-        self.m2 = oracle.Model(hw, max_ctx, nthreads=nthreads) if with_spread else None
+        self.act_fp8 = act_fp8   # the engine's prefill_fp8 numerics (oracle Model prefill_act_fp8)
+        self.m0 = oracle.Model(hw, max_ctx, nthreads=nthreads, prefill_act_fp8=act_fp8)
+        self.m2 = oracle.Model(hw, max_ctx, nthreads=nthreads, prefill_act_fp8=act_fp8) if with_spread else None
         self.rel_spread = 0.0
         self.abs_spread = 0.0
 
@@ -71,7 +72,7 @@ class OrderPair:
     def calibrate(self, vocab, n_prompt=24, n_steps=6, seed=12345):
         """Spread of a fixed teacher-forced calibration run on fresh oracle models (same
         weights); folds into the running maxima."""
-        cal = OrderPair(self.O, self.m0.hw, n_prompt + n_steps + 2, self.m0.nthreads)
+        cal = OrderPair(self.O, self.m0.hw, n_prompt + n_steps + 2, self.m0.nthreads, act_fp8=self.act_fp8)
         prompt = [int(t) for t in np.random.default_rng(seed).integers(0, vocab, n_prompt)]
         oracle_trace(self.O, cal, prompt, n_steps)
         self.rel_spread = max(self.rel_spread, cal.rel_spread)
@@ -130,9 +131,9 @@ class OrderSet:
 
     ORDERS = (0, 1, 2, 7)
 
-    def __init__(self, oracle, hw, max_ctx, nthreads=0):
+    def __init__(self, oracle, hw, max_ctx, nthreads=0, act_fp8=False):
         self.O = oracle
-        self.models = [oracle.Model(hw, max_ctx, nthreads=nthreads) for _ in self.ORDERS]
+        self.models = [oracle.Model(hw, max_ctx, nthreads=nthreads, prefill_act_fp8=act_fp8) for _ in self.ORDERS]
 
     def forward(self, ids, start=None):
         out = []
@@ -145,7 +146,7 @@ class OrderSet:
         return out
 
 
-def forced_decisions(oracle, hw, batch, prompt, n, seed=77, nthreads=0, progress=False):
+def forced_decisions(oracle, hw, batch, prompt, n, seed=77, nthreads=0, progress=False, act_fp8=False):
     """Runs the protocol above on slot 0 of `batch` (an engine over the same weights as
     `hw`).  Returns the report dict; report["ok"] applies the rule:
       * every step's engine logits within max(1e-3, 2 x the run's max order-0 vs order-2 /
@@ -159,7 +160,7 @@ def forced_decisions(oracle, hw, batch, prompt, n, seed=77, nthreads=0, progress
     V = hw.spec.vocab
     P = len(prompt)
     forced = [int(t) for t in np.random.default_rng(seed).integers(0, V, max(n - 1, 0))]
-    ors = OrderSet(oracle, hw, P + n + 2, nthreads)
+    ors = OrderSet(oracle, hw, P + n + 2, nthreads, act_fp8=act_fp8)   # act_fp8: the engine's prefill_fp8
     steps = []
     t_e = batch.prefill(0, prompt)
     for i in range(n):

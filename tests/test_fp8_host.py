@@ -47,3 +47,21 @@ def test_quantize_ties_to_even():
     assert scales[0] == 1.0
     t = W.e4m3_table()
     assert list(t[codes[0, :4]]) == [448.0, 1.0, 1.25, -1.0]
+
+
+def test_oracle_activation_quantiser_equals_libqie_row_quantiser(oracle):
+    """The oracle's fp8-activation restatement (or_quant_rows_fp8: e4m3 rounding from the
+    value set, ties to the even code) and libqie's host row quantiser (e4m3_encode,
+    e4m3_row_scale) agree on every row — scales and dequantised values, including rows
+    with ties, subnormal codes and zeros."""
+    rng = np.random.default_rng(7)
+    rows = [rng.standard_normal(512) * s for s in (1.0, 3e-3, 77.0, 2.5e4, 1e-30)]
+    ties = np.array([t * 2.0 ** k for k in range(-9, 9) for t in (1.0625, 1.1875, 0.0068359375, 447.0, 448.0)])
+    rows.append(np.resize(np.concatenate([ties, -ties]), 512))
+    rows.append(np.zeros(512))
+    w = _bf16(np.stack(rows))
+    codes, scales = W.quantize_fp8(w)
+    dq_lib = W.dequantize_fp8(codes, scales)
+    dq_or, e = oracle.quant_rows_fp8(w)
+    assert np.array_equal(2.0 ** e.astype(np.float64), scales.astype(np.float64))
+    assert np.array_equal(dq_or, dq_lib)

@@ -303,7 +303,7 @@ def run(a):
 OTHER_CONFIGS = [
     {"key": "config2", "model": "Qwen2-0.5B", "batch": 1, "prompt": 128, "gen": 128, "fp8": False,
      "workload": "Qwen2-0.5B bf16, batch=1, prompt=128, gen=128 (BASELINE configs[1])"},
-    {"key": "config4", "model": "Qwen2-7B", "batch": 8, "prompt": 1024, "gen": 256, "fp8": True,
+    {"key": "config4", "model": "Qwen2-7B", "batch": 8, "prompt": 1024, "gen": 256, "fp8": True, "fp8_mfma": True,
      "workload": "Qwen2-7B fp8 weights, batch=8, prompt=1024, gen=256 (BASELINE configs[3])"},
 ]
 
@@ -352,6 +352,12 @@ def run_config(Q, S, W, c):
         dt = time.perf_counter() - t0
         ms = dt * 1e3 / steps
         us_dom, by_dom = b.time_kernel(0, 54)
+        mx = None
+        if c.get("fp8_mfma"):   # the same prefill with fp8 activations on the block-scaled fp8 MFMA
+            lg_ref = None
+            b.prefill_batch(0, prompts) if B > 1 else b.prefill(0, prompts[0])
+            lg_ref = b.logits()
+            mx = fp8_mfma_prefill(Q, spec, W, B, P, max_ctx, prompts, lg_ref, t_pf)
         step_bytes = spec.decode_weight_bytes(fp8=c["fp8"]) + B * spec.kv_bytes_per_position() * (P + (steps + 1) / 2.0)
         gbs = step_bytes / (ms * 1e-3) / 1e9
         return {"workload": c["workload"], "value": round(B * steps / dt, 2), "unit": "tokens/s",
@@ -364,7 +370,8 @@ def run_config(Q, S, W, c):
                                     "algorithmic_bytes": by_dom,
                                     "live_frac": round(by_dom / us_dom / 1e3 / HBM_PEAK_GBS, 4),
                                     "timing": "hipEvents on the engine stream around 54 launches cycling over "
-                                              "layers 1..L-1 (in-graph durations: profiles/r04_*rocprof*)"}}
+                                              "layers 1..L-1 (in-graph durations: profiles/r04_*rocprof*)"},
+                **({"prefill_fp8_mfma": mx} if mx else {})}
     finally:
         if b is not None:   # the batch before its engine
             b.close()
@@ -457,6 +464,47 @@ def config5(Q, S, W, a, comm, group, rank, local):
             eng.close()
     res["wall_s"] = round(time.perf_counter() - t_cfg, 1)
     return res
+
+
+def fp8_mfma_prefill(Q, spec, W, B, P, max_ctx, prompts, lg_ref, t_ref):
+    """Config 4's prefill with the numerics flag prefill_fp8: every projection on the
+    block-scaled fp8 MFMA (v_mfma_scale_f32_16x16x128_f8f6f4; activations quantised per row
+    to e4m3).  A different model from the bf16-activation one: its change to the first
+    decision's logits (norm-relative, all B rows) is reported beside the speed; parity against
+    the oracle's identical quantisation is tests/test_gpu_fp8_mx.py."""
+    eng = b = None
+    try:
+        eng = Q.Engine(spec, max_ctx=max_ctx, weight_fp8=True, prefill_fp8=True).init_synthetic(W.SynthParams(seed=0))
+        b = eng.batch(B, max_ctx)
+
+        def prefill():
+            return b.prefill_batch(0, prompts) if B > 1 else [b.prefill(0, prompts[0])]
+        prefill()
+        lg = b.logits()
+        pts = []
+        for _ in range(2):
+            eng.sync()
+            t0 = time.perf_counter()
+            prefill()
+            eng.sync()
+            pts.append(time.perf_counter() - t0)
+        t = float(np.median(pts))
+        g = (lg.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+        r = (lg_ref.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+        rel = float(np.linalg.norm(g - r) / max(np.linalg.norm(r), 1e-30))
+        return {"prefill_tok_s": round(B * P / t, 1), "prefill_ms": round(t * 1e3, 3),
+                "speedup_vs_bf16_activations": round(t_ref / t, 3),
+                "prefill_tflops_job": round(spec.prefill_flops(P, B) / t / 1e12, 1),
+                "first_logits_change_norm_rel": round(rel, 5),
+                "numerics": "prefill_fp8: per-row e4m3 activations x fp8 weights on v_mfma_scale_f32_16x16x128_f8f6f4 "
+                            "(a different model; parity vs the oracle's identical quantisation in tests)"}
+    except Exception as ex:
+        return {"error": str(ex)[:300]}
+    finally:
+        if b is not None:
+            b.close()
+        if eng is not None:
+            eng.close()
 
 
 def pmc_traffic(kernel="gate_up", tag=""):

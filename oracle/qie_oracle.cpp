@@ -141,6 +141,8 @@ static int g_sum_order = 0;
  *   4 = order 0 except SiLU's exponent in 2's fast-math form;
  *   5 = order 0 except the RMSNorm sum of squares in 2's order;
  *   6 = order 0 except the attention q.k dot products in 2's order (3..6: tools/flip_attrib.py);
+ *   8 = order 2, and in the fp8-activation projections (or_set_act_fp8) the fp8 MFMA's
+ *       accumulation model (mx_block_dot);
  *   7 = order 0 as nvcc -use_fast_math compiles it (the reference's recorded build,
  *       build/CMakeFiles/qwen.dir/flags.make:10: --fmad=true, --prec-div=false, fast
  *       exponent): a*b+c contracted to fmaf where the source has it (RoPE's x0*c - x1*s and
@@ -154,6 +156,38 @@ static int g_sum_order = 0;
  * algorithm's own order sensitivity, which sizes the end-to-end parity tolerance
  * (bench.py cpu_baseline, tests/test_gpu_headline.py, DESIGN.md "Parity"). */
 void or_set_sum_order(int v) { g_sum_order = v; }
+// order 8 is order 2 everywhere, plus (in the fp8-activation projections) the fp8 MFMA's
+// accumulation model below
+static inline bool ord2() { return g_sum_order == 2 || g_sum_order == 8; }
+static int g_act_fp8 = 0;   // the engine's prefill_fp8 numerics (or_set_act_fp8, below)
+
+/* Order 8, fp8-activation projections: the block-scaled fp8 MFMA's accumulation modelled.
+ * tools/mx_mfma_probe.hip measures v_mfma_scale_f32_16x16x128_f8f6f4 on gfx950 at up to
+ * 1.5e-4 of sum|p| from the exact sum of its 128 products (e4m3 x e4m3 products are exact; the
+ * instruction's internal sum is not fp32-exact).  Modelled here as: each 128-k block's
+ * products summed exactly, the block sum rounded to a multiple of 2^(floor(log2 max|p|) - 12),
+ * then added in fp32 — an evaluation with the hardware's error size, so that the parity bar of
+ * the fp8 prefill (2 x the order-0 vs order-8 spread) contains what its re-quantisation of
+ * every projection input does to a difference of that size. */
+static float mx_block_dot(const float* a, const float* w, int64_t K) {
+    float acc = 0.f;
+    for (int64_t k0 = 0; k0 < K; k0 += 128) {
+        double s = 0.0, mp = 0.0;
+        for (int64_t k = k0; k < std::min<int64_t>(K, k0 + 128); k++) {
+            const double p = (double)a[k] * (double)w[k];
+            s += p;
+            mp = std::max(mp, std::fabs(p));
+        }
+        if (mp > 0.0) {
+            int e;
+            std::frexp(mp, &e);
+            const double q = std::ldexp(1.0, e - 1 - 12);
+            s = std::nearbyint(s / q) * q;
+        }
+        acc = acc + (float)s;
+    }
+    return acc;
+}
 
 // order 7 (nvcc -use_fast_math) models: a / b as a * rcp(b), expf(x) as exp2(x log2 e)
 static inline float fm_div(float a, float b) { return a * (1.0f / b); }
@@ -171,7 +205,7 @@ void or_rmsnorm(const bf16_t* x, const bf16_t* w, bf16_t* y, int64_t rows, int64
         const bf16_t* xr = x + r * H;
         bf16_t* yr = y + r * H;
         float sum = 0.f;
-        if (g_sum_order == 2 || g_sum_order == 5) {
+        if (ord2() || g_sum_order == 5) {
             float part[256];
             for (int j = 0; j < 256; j++) part[j] = 0.f;
             for (int64_t i = 0; i < H; i++) {
@@ -218,7 +252,24 @@ void or_matmul(const bf16_t* A, const bf16_t* W, const bf16_t* bias, bf16_t* C,
     std::vector<float> Af((size_t)M * K);
     for (int64_t i = 0; i < M * K; i++) Af[i] = bf2f(A[i]);
     int nt = set_threads(nthreads);
-    if (g_sum_order == 1 || g_sum_order == 2) {
+    if (g_sum_order == 8 && g_act_fp8) {
+#pragma omp parallel num_threads(nt)
+        {
+            std::vector<float> wf((size_t)K);
+#pragma omp for schedule(static)
+            for (int64_t n = 0; n < N; n++) {
+                const bf16_t* wr = W + n * K;
+                for (int64_t k = 0; k < K; k++) wf[k] = bf2f(wr[k]);
+                for (int64_t m = 0; m < M; m++) {
+                    float f = mx_block_dot(Af.data() + m * K, wf.data(), K);
+                    if (bias) f = f + bf2f(bias[n]);
+                    C[m * N + n] = f2bf(f);
+                }
+            }
+        }
+        return;
+    }
+    if (g_sum_order == 1 || ord2()) {
 #pragma omp parallel num_threads(nt)
         {
             std::vector<float> wf((size_t)K);
@@ -306,7 +357,7 @@ void or_qknorm(bf16_t* x, const bf16_t* w, int64_t rows, int64_t row_stride, int
                 continue;
             }
             for (int d = 0; d < hd; d++) { float t = bf2f(v[d]); buf[d] = t * t; }
-            if (g_sum_order == 2)
+            if (ord2())
                 for (int d = 1; d < hd; d++) buf[0] += buf[d];
             else
                 for (int stride = hd / 2; stride > 0; stride >>= 1)
@@ -374,7 +425,7 @@ void or_silu_mul(const bf16_t* gate, const bf16_t* up, bf16_t* h, int64_t n) {
         float g = bf2f(gate[i]);
         // order 2: the reference build's -use_fast_math exponent (flags.make:10), which a
         // GPU libm need not match to the last ulp either
-        const float ex = g_sum_order == 2 || g_sum_order == 4 || g_sum_order == 7 ? fm_exp(-g) : expf(-g);
+        const float ex = ord2() || g_sum_order == 4 || g_sum_order == 7 ? fm_exp(-g) : expf(-g);
         float a = rbf(g * (1.0f / (1.0f + ex)));
         h[i] = f2bf(bf2f(up[i]) * a);
     }
@@ -480,7 +531,7 @@ void or_attention_nm(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, bf16_t
                 for (int t = 0; t < mkv; t++) {
                     const bf16_t* kr = kh + (int64_t)t * hd;
                     for (int d = 0; d < hd; d++) buf[d] = bf2f(qr[d]) * bf2f(kr[d]);
-                    if (g_sum_order == 2 || g_sum_order == 6) {
+                    if (ord2() || g_sum_order == 6) {
                         float part[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
                         for (int d = 0; d < hd; d++) part[d & 7] += buf[d];
                         for (int w = 4; w > 0; w >>= 1)
@@ -499,7 +550,7 @@ void or_attention_nm(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, bf16_t
                 float mx = -1e9f;
                 for (int t = 0; t < mkv; t++) mx = fmaxf(mx, score[t]);
                 float sum = 0.f;
-                if (g_sum_order == 2 || g_sum_order == 3) {
+                if (ord2() || g_sum_order == 3) {
                     // the online-softmax (flash) formulation every split / tiled kernel uses:
                     // exponent as exp2((s - m) * log2 e) (the reference build's -use_fast_math
                     // __expf), per-128-key block sums, and P.V normalised AFTER the
@@ -704,7 +755,6 @@ int or_sample_ref(const bf16_t* logits, int64_t V, int k, float temperature, flo
  * zero row), x -> e4m3_rne(x / s) * s — before the (unchanged) matmul.  The rounding is
  * restated from the OCP e4m3fn value set itself (nearest representable value, ties to the
  * even code), independently of the engine's encoder.  Every dequantised value is a bf16. */
-static int g_act_fp8 = 0;
 void or_set_act_fp8(int v) { g_act_fp8 = v; }
 
 static float e4m3_value(int code) {   // non-negative codes 0..0x7E

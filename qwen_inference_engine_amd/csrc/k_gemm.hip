@@ -1183,7 +1183,7 @@ __device__ __forceinline__ int mx_wrow(const MxParams& p, int64_t nt, int c, int
 typedef int i32x8_mx __attribute__((ext_vector_type(8)));
 
 template <int EPI, bool T16>
-__global__ __launch_bounds__(512) void gemm8mx_kernel(MxParams p, int n_mt, G8Split sk) {
+__global__ __launch_bounds__(512) void gemm8mx_kernel(MxParams p, int n_mt, G8Split sk, int dbg) {
 #pragma clang fp contract(off)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -1300,9 +1300,12 @@ __global__ __launch_bounds__(512) void gemm8mx_kernel(MxParams p, int n_mt, G8Sp
         for (int i = 0; i < 4; i++)
 #pragma unroll
             for (int j = 0; j < 2; j++)
+            {
                 acc[4 * qa + i][2 * qb + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
                     fa[i], fb[j], acc[4 * qa + i][2 * qb + j], 0, 0, 0, (int)((sa_pk[qa] >> (8 * i)) & 0xffu), 0,
                     (int)((sb_pk >> (8 * (2 * qb + j))) & 0xffu));
+                if (QIE_DBG(dbg == 1)) asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+            }
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
     };
@@ -1455,8 +1458,9 @@ static int launch_gemm8mx_t(const MxParams& p, int n_mt, int n_tiles, const G8Sp
         QIE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
         raised = true;
     }
+    static const int dbg = dev_env("QIE_MX_DBG", 0);
     hipLaunchKernelGGL((gemm8mx_kernel<EPI, T16>), dim3((unsigned)(n_tiles * sk.splitk)), dim3(512), shm, st, p, n_mt,
-                       sk);
+                       sk, dbg);
     QIE_LAUNCH_CHECK();
     return 0;
 }

@@ -59,7 +59,10 @@ class OrderPair:
         lg0 = self.m0.forward(ids, start)
         lg2 = None
         if self.m2 is not None:
-            self.O.set_sum_order(2)
+            # fp8 activations: order 8 (order 2 + the fp8 MFMA's accumulation model; the
+            # quantisation of every projection input turns the hardware's accumulation error
+            # into rounding flips an exact-sum order never shows)
+            self.O.set_sum_order(8 if self.act_fp8 else 2)
             try:
                 lg2 = self.m2.forward(ids, start)
             finally:
@@ -133,11 +136,13 @@ class OrderSet:
 
     def __init__(self, oracle, hw, max_ctx, nthreads=0, act_fp8=False):
         self.O = oracle
+        # fp8 activations: order 8 in the place of order 2 (OrderPair)
+        self.orders = tuple(8 if (o == 2 and act_fp8) else o for o in self.ORDERS)
         self.models = [oracle.Model(hw, max_ctx, nthreads=nthreads, prefill_act_fp8=act_fp8) for _ in self.ORDERS]
 
     def forward(self, ids, start=None):
         out = []
-        for o, m in zip(self.ORDERS, self.models):
+        for o, m in zip(self.orders, self.models):
             self.O.set_sum_order(o)
             try:
                 out.append(m.forward(ids, start))

@@ -5,10 +5,11 @@ matrix_mul.cu:165-288) — against the oracle's fp8-activation mode (or_set_act_
 * qie_quantize_rows_fp8 == or_quant_rows_fp8 bit for bit (exponents and dequantised values);
 * qie_linear with fp8 activations (plain and 16-row tiled fp8 weights; STORE + bias over three
   segments, SWIGLU, RESIDUAL, F32; split-K and full-chip grids) == the oracle's matmul of the
-  dequantised operands within the fp32-sum bar of tests/test_gpu_ops.py: every e4m3 x e4m3
-  product is exact, only the summation order differs;
+  dequantised operands within MX_ACC_REL of sum|a w| (every e4m3 x e4m3 product is exact; the
+  instruction's internal sum is not fp32-exact, tools/mx_mfma_probe.hip);
 * the engine (Qwen2-7B widths, 2 layers, fp8 weights, prefill_fp8) teacher-forced against the
-  oracle with the same activation quantisation in its prefill (tests/parity.py's bar).
+  oracle with the same activation quantisation in its prefill (tests/parity.py's bar, whose
+  second evaluation is then oracle order 8: order 2 + the MFMA accumulation model).
 """
 import ctypes as C
 
@@ -25,6 +26,12 @@ from qwen_inference_engine_amd import _lib, spec as S, weights as W
 from qwen_inference_engine_amd._lib import LinearArgsC
 
 pytestmark = pytest.mark.gpu
+
+# The fp8 MFMA's own accumulation is not fp32-exact: tools/mx_mfma_probe.hip measures one
+# v_mfma_scale_f32_16x16x128_f8f6f4 at up to 1.5e-4 of sum|p| from the exact sum of its 128
+# (exact) products on random e4m3 data.  The op bar is therefore this fraction of sum|a w|
+# (besides one bf16 ulp), not the 1e-5 of the bf16 GEMMs.
+MX_ACC_REL = 5e-4
 
 
 def _quant_dev(qlib, x):
@@ -94,7 +101,7 @@ def test_linear_act_fp8_store_bias(oracle, qlib, tiled, M, K, n):
     _mx_linear(qlib, q, e, [(d, r) for (d, _), r in zip(qw, n)], [G.dev(b) for b in bs], M, K, N, y,
                _lib.QIE_EPI_STORE, tiled)
     scale = np.concatenate([_abs_scale(oracle, dqx, dq) for _, dq in qw], axis=1)
-    G.assert_sum_close(G.host_bf16(y), want, scale, what=f"act_fp8 M={M} K={K} tiled={tiled}")
+    G.assert_sum_close(G.host_bf16(y), want, scale, rel=MX_ACC_REL, what=f"act_fp8 M={M} K={K} tiled={tiled}")
 
 
 @pytest.mark.parametrize("tiled", [False, True])
@@ -110,27 +117,36 @@ def test_linear_act_fp8_full_chip_grid(oracle, qlib, tiled):
     rows = np.array([0, 1, 255, 256, 1000, 1023, 1777, 2047])
     dqx, _ = oracle.quant_rows_fp8(x[rows])
     want = oracle.matmul(dqx, dq)
-    G.assert_sum_close(G.host_bf16(y)[rows], want, _abs_scale(oracle, dqx, dq), what="act_fp8 full grid")
+    G.assert_sum_close(G.host_bf16(y)[rows], want, _abs_scale(oracle, dqx, dq), rel=MX_ACC_REL,
+                       what="act_fp8 full grid")
 
 
 @pytest.mark.parametrize("M", [40, 600])
 @pytest.mark.parametrize("tiled", [False, True])
 def test_linear_act_fp8_swiglu_residual_f32(oracle, qlib, M, tiled):
+    """SWIGLU: the epilogue on the kernel's own accumulators — the gate and up halves run as
+    STORE launches of the same kernel (K = 896: 7 k-tiles, no split in either launch, so every
+    accumulator sees the same MFMA sequence) and the SWIGLU output must equal the oracle's
+    silu_mul of those bf16 halves (within one ulp: device vs host expf); the halves against
+    the oracle's matmul under MX_ACC_REL.  RESIDUAL and F32 (the down projection's two
+    epilogues) against the oracle under the same accumulation bar."""
     K, I = 896, 640
     x = rand_bf16(oracle, (M, K), seed=6)
     (dg, qg), (du, qu) = _fp8w(qlib, rand_bf16(oracle, (I, K), 0.08, seed=7), tiled), \
         _fp8w(qlib, rand_bf16(oracle, (I, K), 0.08, seed=8), tiled)
     dqx, _ = oracle.quant_rows_fp8(x)
-    want = oracle.silu_mul(oracle.matmul(dqx, qg), oracle.matmul(dqx, qu))
     q, e = _quant_dev(qlib, x)
+    halves = []
+    for d_, q_ in ((dg, qg), (du, qu)):
+        yh = G.zeros_bf16(M, I)
+        _mx_linear(qlib, q, e, [(d_, I)], [None], M, K, I, yh, _lib.QIE_EPI_STORE, tiled)
+        halves.append(G.host_bf16(yh))
+        G.assert_sum_close(halves[-1], oracle.matmul(dqx, q_), _abs_scale(oracle, dqx, q_), rel=MX_ACC_REL,
+                           what="act_fp8 gate/up half")
     y = G.zeros_bf16(M, I)
     _mx_linear(qlib, q, e, [(dg, I), (du, I)], [], M, K, I, y, _lib.QIE_EPI_SWIGLU, tiled)
-    d = G.ulp_diff(G.host_bf16(y), want)
-    assert (d == 0).mean() > 0.97
-    gs = G.bf(oracle.matmul(dqx, qg)).astype(np.float64)
-    u = np.abs(G.bf(oracle.matmul(dqx, qu)).astype(np.float64))
-    ill = (np.abs(gs) < 1e-2 * _abs_scale(oracle, dqx, qg)) | (u < 1e-2 * _abs_scale(oracle, dqx, qu)) | (gs < -4)
-    assert not ((d > 2) & ~ill).any()
+    d = G.ulp_diff(G.host_bf16(y), oracle.silu_mul(halves[0], halves[1]))
+    assert d.max() <= 1 and (d == 0).mean() > 0.99, f"SWIGLU epilogue: max {d.max()} ulps"
     # residual and fp32 partial epilogues (the down projection; K = I)
     dw, qw = _fp8w(qlib, rand_bf16(oracle, (K, I), 0.02, seed=4), tiled)
     h = rand_bf16(oracle, (M, I), seed=3)
@@ -141,12 +157,13 @@ def test_linear_act_fp8_swiglu_residual_f32(oracle, qlib, M, tiled):
     yr = G.dev(res)
     _mx_linear(qlib, hq, he, [(dw, K)], [], M, I, K, yr, _lib.QIE_EPI_RESIDUAL, tiled)
     acc = G.bf(oracle.matmul(dqh, qw)).astype(np.float64)
-    tol = 2.0 ** -7 * (np.abs(acc) + np.abs(G.bf(want))) + 1e-5 * _abs_scale(oracle, dqh, qw)
+    sc = _abs_scale(oracle, dqh, qw)
+    tol = 2.0 ** -7 * (np.abs(acc) + np.abs(G.bf(want))) + MX_ACC_REL * sc
     assert (np.abs(G.bf(G.host_bf16(yr)).astype(np.float64) - G.bf(want)) <= tol).all()
     yf = G.zeros((M, K), np.float32)
     _mx_linear(qlib, hq, he, [(dw, K)], [], M, I, K, yf, _lib.QIE_EPI_F32, tiled)
     exact = oracle.bf16_to_f32(dqh).astype(np.float64) @ oracle.bf16_to_f32(qw).astype(np.float64).T
-    assert np.abs(G.host(yf) - exact).max() <= 1e-5 * _abs_scale(oracle, dqh, qw).max() + 1e-6
+    assert (np.abs(G.host(yf) - exact) <= MX_ACC_REL * sc + 1e-6).all()
 
 
 def test_linear_act_fp8_rejects_bad_shapes(qlib):

@@ -20,6 +20,7 @@
 
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace qie {
 
@@ -324,7 +325,7 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
     // (a whole number of 256-B bank rows apart) hit the same banks: 8-way conflicts.
     auto vswz = [](int r) { return 2 * (r & (CPR / 2 - 1)); };
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int fr = lane & 15, g = lane >> 4;
     const int h = blockIdx.y, seq = blockIdx.z;
     const int R = a.rows_per_seq;
@@ -351,10 +352,10 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
         const int gq = gact[q] ? grp[q] : 0;
         const int qrow = min(16 * gq + fr, R - 1);
         qpos[q] = a.pos[row0 + qrow];
-        gpos[q] = gact[q] ? a.pos[row0 + min(16 * gq + 15, R - 1)] : -1;   // -1: no tile
+        gpos[q] = __builtin_amdgcn_readfirstlane(gact[q] ? a.pos[row0 + min(16 * gq + 15, R - 1)] : -1);   // -1: no tile
         // the group's first position (positions are non-decreasing): a key tile ending at or
         // before it is unmasked for every row of the group
-        gmin[q] = a.full_tiles ? a.pos[row0 + min(16 * gq, R - 1)] : -1;
+        gmin[q] = __builtin_amdgcn_readfirstlane(a.full_tiles ? a.pos[row0 + min(16 * gq, R - 1)] : -1);
         const uint16_t* qp = a.q + (row0 + qrow) * (int64_t)a.nq * HD + (int64_t)h * HD;
 #pragma unroll
         for (int ks = 0; ks < KSTEPS; ks++) qf[q][ks] = *reinterpret_cast<const bf16x8_t*>(qp + ks * 32 + g * 8);
@@ -402,10 +403,12 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
         if (kt + 1 < nkt) issue(kt + 1, cur ^ 1);
         const uint16_t* K = Ks + cur * KT * HD;
         const uint16_t* Vt = Vs + cur * KT * HD;
-        bool on[QG];
-#pragma unroll
-        for (int q = 0; q < QG; q++) on[q] = kt * KT <= gpos[q];   // wave-uniform
-        if (on[0] || on[1]) {
+        // which of the wave's two groups take this key tile (wave-uniform: gpos is
+        // readfirstlane'd); the tile body is instantiated per case, so no MFMA sits behind a
+        // per-instruction exec-mask branch (the compiler could not prove on[] uniform and
+        // wrapped every MFMA in s_and_saveexec / s_cbranch_execz / s_or_b64)
+        auto tile = [&](auto q0c, auto q1c) {
+            constexpr bool ON[QG] = {decltype(q0c)::value, decltype(q1c)::value};
             f32x4_t sacc[QG][4];
 #pragma unroll
             for (int t = 0; t < 4; t++) {
@@ -418,13 +421,13 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
                     const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(K + r * HD + ((ch ^ (r & (CPR - 1))) * 8));
 #pragma unroll
                     for (int q = 0; q < QG; q++)
-                        if (on[q]) sacc[q][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[q][ks], sacc[q][t], 0, 0, 0);
+                        if (ON[q]) sacc[q][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[q][ks], sacc[q][t], 0, 0, 0);
                 }
             }
             float pv[QG][4][4];   // this tile's probabilities (fp32), split into bf16 parts at P.V
 #pragma unroll
             for (int q = 0; q < QG; q++) {
-                if (!on[q]) continue;
+                if (!ON[q]) continue;
                 float (&sv)[4][4] = pv[q];
                 float mt = -INFINITY;
                 // (an fma form, exp2(fma(s, sl2, -m)), saves 16 VALU per tile but rounds
@@ -485,7 +488,7 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
                 for (int q = 0; q < QG; q++)
 #pragma unroll
                     for (int jj = 0; jj < 8; jj++) {
-                        const float e = on[q] ? pv[q][2 * c + (jj >> 2)][jj & 3] : 0.f;
+                        const float e = ON[q] ? pv[q][2 * c + (jj >> 2)][jj & 3] : 0.f;
                         ph[q][jj] = (__bf16)e;
                         pl[q][jj] = (__bf16)(e - (float)ph[q][jj]);
                     }
@@ -502,13 +505,17 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
                         __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
                     for (int q = 0; q < QG; q++) {
-                        if (!on[q]) continue;
+                        if (!ON[q]) continue;
                         oacc[q][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph[q], vb8, oacc[q][d], 0, 0, 0);
                         oacc[q][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pl[q], vb8, oacc[q][d], 0, 0, 0);
                     }
                 }
             }
-        }
+        };
+        const bool on0 = kt * KT <= gpos[0], on1 = kt * KT <= gpos[1];
+        if (on0 && on1) tile(std::true_type{}, std::true_type{});
+        else if (on1) tile(std::false_type{}, std::true_type{});
+        else if (on0) tile(std::true_type{}, std::false_type{});
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs of tile kt+1
         __syncthreads();                                     // ... and every other wave's
         cur ^= 1;

@@ -1509,7 +1509,9 @@ static int gemm_mx(const qie_linear_args* a, hipStream_t st) {
     const int64_t cus = device_cu_count();
     const int nk = (int)(a->K / mx::BK);
     G8Split sk{1, nullptr, nullptr};
-    if (tiles < cus) {
+    // split only below half the chip (r05, same box, 2,048 rows): O (112 tiles) 91.0 unsplit
+    // vs 78.0 split 3, down (112) 307 vs 188; QKV (144 tiles) 69.4 unsplit vs 93.9 split 3
+    if (2 * tiles <= cus) {
         int best = 1;
         double best_t = 1e30;
         const int smax = dev_env("QIE_MX_SPLITK_MAX", 4);

@@ -784,7 +784,10 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
                                    has_new);
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (!(SPEC && spec) || chunk != KS) load_step(0);   // (uniform) the speculative step was not this split's
+    // (uniform) the speculative step is this split's first step iff the split starts at key
+    // KS s: one-step splits, and split 0 of every context (the one-split contexts of <= 2
+    // steps, Qwen2-0.5B's ctx 129-256, re-issued the same loads behind the position: +1.2 us)
+    if (!(SPEC && spec) || t0 != KS * s) load_step(0);
     if (SPEC && spec) {
         // rows past the context hold whatever the cache has there: their scores are masked
         // to -inf (P = 0), and their V rows are zeroed so that 0 * V stays 0 for any bits

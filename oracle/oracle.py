@@ -52,6 +52,7 @@ def lib():
             "or_curand_uniform_first": (F, [C.c_uint64]),
             "or_set_sum_order": (None, [C.c_int]),
             "or_set_act_fp8": (None, [C.c_int]),
+            "or_set_hf_eager": (None, [C.c_int]),
             "or_quant_rows_fp8": (None, [P, C.c_int64, C.c_int64, P]),
             "or_e4m3_round": (C.c_float, [C.c_float]),
             "or_set_layer_dump": (None, [P]),
@@ -162,6 +163,13 @@ def topk(logits, k):
 def set_sum_order(v: int) -> None:
     """Matmul summation-order variant (0 default, 1 alternative; see or_set_sum_order)."""
     lib().or_set_sum_order(int(v))
+
+
+def set_hf_eager(v: int) -> None:
+    """HF numerics attention form: 0 = fp32 scores / softmax (transformers' sdpa and fused
+    kernels; the engine's), 1 = transformers' eager_attention_forward (bf16 scores and
+    probabilities; the tests/golden/hf_* fixtures)."""
+    lib().or_set_hf_eager(int(v))
 
 
 def quant_rows_fp8(x):

@@ -451,7 +451,11 @@ void or_embedding(const bf16_t* E, const int32_t* ids, bf16_t* out, int64_t n, i
  * Cache layout here: [nkv][ctx][hd] for ONE layer (kv_head_stride elements
  * between kv heads, hd between positions).  q/out rows: [mq][nq*hd].
  */
-/* HF numerics (transformers' eager_attention_forward, Qwen2/Qwen3): the scores are a bf16
+/* HF numerics: transformers has two attention arithmetics.  Its default (sdpa, and every
+ * fused / flash kernel) keeps the scores and the softmax in fp32 — the reference form below,
+ * which the engine's flash kernels compute; or_set_hf_eager(1) selects eager_attention_forward
+ * instead (the tests' eager fixtures):
+ * transformers' eager_attention_forward (Qwen2/Qwen3): the scores are a bf16
  * matmul output, scaled in bf16 (bf16(bf16(q.k) * hd^-0.5)); softmax in fp32 (exp(s - m),
  * times the reciprocal of the sum), the probabilities rounded to bf16 before the bf16 P.V
  * matmul (fp32 accumulate, one rounding).  The masked scores are excluded (-inf). */
@@ -499,6 +503,9 @@ static void attention_hf(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, bf
     }
 }
 
+static int g_hf_eager = 0;
+void or_set_hf_eager(int v) { g_hf_eager = v; }
+
 void or_attention_nm(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, bf16_t* out, int mq, int mkv, int nq,
                      int nkv, int hd, int causal, int q_abs_base, int64_t kv_head_stride, int nthreads, int numerics);
 
@@ -511,7 +518,7 @@ void or_attention(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, bf16_t* o
 
 void or_attention_nm(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, bf16_t* out, int mq, int mkv, int nq,
                      int nkv, int hd, int causal, int q_abs_base, int64_t kv_head_stride, int nthreads, int numerics) {
-    if (numerics == QIE_NUMERICS_HF) {
+    if (numerics == QIE_NUMERICS_HF && g_hf_eager) {
         attention_hf(q, kc, vc, out, mq, mkv, nq, nkv, hd, causal, q_abs_base, kv_head_stride, nthreads);
         return;
     }

@@ -30,12 +30,14 @@ def load(name):
 
 
 def oracle_spread(oracle, hw, prompt, ids):
-    """Orders 0 and 2 of the oracle (hf numerics) teacher-forced on `ids`: (order-0 logits
-    per step, max norm-relative spread, max absolute spread)."""
+    """Orders 0 and 2 of the oracle (hf numerics, transformers' eager attention form — the
+    fixtures') teacher-forced on `ids`: (order-0 logits per step, max norm-relative spread,
+    max absolute spread)."""
     n = len(ids)
     outs = {}
     for o in (0, 2):
         oracle.set_sum_order(o)
+        oracle.set_hf_eager(1)   # the fixtures' attention form (transformers eager)
         try:
             m = oracle.Model(hw, len(prompt) + n + 2)
             lg = [m.forward(prompt, 0)]
@@ -43,6 +45,7 @@ def oracle_spread(oracle, hw, prompt, ids):
                 lg.append(m.forward([t]))
         finally:
             oracle.set_sum_order(0)
+            oracle.set_hf_eager(0)
         outs[o] = lg
     rel = max(norm_rel(a, b) for a, b in zip(outs[2], outs[0]))
     ab = max(float(np.abs(G.bf(a).astype(np.float64) - G.bf(b)).max()) for a, b in zip(outs[2], outs[0]))

@@ -42,6 +42,7 @@ CASES = {
                           tie_word_embeddings=True),
 }
 PROMPT_LEN, N_NEW = 12, 16
+ATTN = "eager"   # eager_attention_forward: bf16 scores and probabilities (the oracle's or_set_hf_eager form)
 
 
 def to_bf16_bits(t):
@@ -56,7 +57,7 @@ def make(name, cfg):
     Cfg = transformers.Qwen2Config if cfg["model_type"] == "qwen2" else transformers.Qwen3Config
     Mdl = transformers.Qwen2ForCausalLM if cfg["model_type"] == "qwen2" else transformers.Qwen3ForCausalLM
     kw = {k: v for k, v in cfg.items() if k != "model_type"}
-    c = Cfg(attn_implementation="eager", **kw)
+    c = Cfg(attn_implementation=ATTN, **kw)
     spec = S.ModelSpec.from_hf_config(dict(cfg), name=name, numerics="hf")
     hw = W.HostWeights.synthetic(spec, W.SynthParams(**SYN))
     torch.manual_seed(0)

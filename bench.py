@@ -36,6 +36,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# Measured stream bandwidth of the dominant kernel's own bytes at its own grid on this part
+# (frac also against a measured stream-copy peak): tools/step_floor.hip, 28
+# back-to-back gate/up-sized pure streams (271.6 MB each, grid-stride 4 blocks x 4 waves per
+# CU, 16-B nt loads) in one hipGraph: 42.29 us per launch (profiles/r05_step_floor.txt)
+STREAM_GATE_UP_GBS = 271.633408e6 / 42.29e-6 / 1e9
+STREAM_SRC = "profiles/r05_step_floor.txt (tools/step_floor.hip)"
 METRIC = "decode tokens/s + prefill tok/s, Qwen2-7B bf16 batch=1, 1/2/4/8 MI355X"
 
 
@@ -264,6 +270,8 @@ def run(a):
         "roofline": {"bound": "hbm", "kernel": "gate_up_gemv (rms + gate/up GEMV + SwiGLU, layers 1..L-1)",
                      "achieved": dom["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(dom["GBps"] / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "stream_peak": round(STREAM_GATE_UP_GBS, 1),
+                     "frac_vs_stream": round(dom["GBps"] / STREAM_GATE_UP_GBS, 4), "stream_source": STREAM_SRC,
                      "algorithmic_bytes": dom["bytes"], "traffic_source": traffic_src},
         "step_roofline": {"bytes_per_step": step_bytes, "achieved_GBps_per_gpu": round(step_gbs, 1),
                           "frac": round(step_gbs / HBM_PEAK_GBS, 4),

@@ -41,9 +41,9 @@ def roles(names):
         r = None
         if n.startswith("attn_prefill"):
             r = "attention"
-        elif n.startswith("gemm_big_kernel<2"):
+        elif n.startswith("gemm_big_kernel<2") or n.startswith("gemm8_kernel<2"):
             r = "gate_up"
-        elif n.startswith("gemm_kernel") or n.startswith("gemm_big_kernel"):
+        elif n.startswith("gemm_kernel") or n.startswith("gemm_big_kernel") or n.startswith("gemm8_kernel"):
             r = {"attention": "o", "gate_up": "down"}.get(prev, "qkv")
         out.append(r)
         if r:

@@ -380,9 +380,11 @@ struct PeerComm : qie_comm {
         return 0;
     }
     bool graph_capturable() const override { return true; }
-    int error_state() const override {
+    int error_state(void* stream) const override {   // stream-ordered (never the null stream)
         unsigned v = 0;
-        if (hipMemcpy(&v, ctl + 2, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+        if (hipMemcpyAsync(&v, ctl + 2, sizeof(v), hipMemcpyDeviceToHost, (hipStream_t)stream) != hipSuccess ||
+            hipStreamSynchronize((hipStream_t)stream) != hipSuccess)
+            return -1;
         return (int)v;
     }
 };

@@ -472,11 +472,20 @@ static qie_linear_args lin_proj(const qie_engine* e) {
 // when the engine was asked to (opts.comm_always: the captured-collective path on one GPU).
 static bool use_comm(const qie_engine* e) { return e->comm && (e->sh.tp > 1 || e->opts.comm_always); }
 
+// Device -> host on the engine stream (then wait): never the legacy null stream, whose
+// implicit ordering against every blocking stream HIP refuses while ANY thread of the process
+// captures a graph (the TP ranks of one process capture their decode graphs concurrently).
+static hipError_t d2h(const qie_engine* e, void* dst, const void* src, size_t bytes) {
+    hipError_t he = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, e->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+    return he;
+}
+
 // After a stream synchronisation: a device-side exchange failure (the peer backend's bounded
 // wait) makes the call fail instead of returning ids computed from a partial exchange.
 static int comm_check(const qie_engine* e, const char* who) {
     if (!use_comm(e)) return 0;
-    const int err = e->comm->error_state();
+    const int err = e->comm->error_state(e->stream);
     if (err) return fail(-7, "%s: tensor-parallel exchange failed on the device (error word %d: a peer rank did "
                              "not arrive within the bounded wait); the communicator is unusable", who, err);
     return 0;
@@ -1185,7 +1194,7 @@ int qie_batch_block_table(qie_batch* b, int32_t seq, int32_t* host_pages, int32_
     QIE_REQUIRE(b && b->d_table && host_pages && seq >= 0 && seq < b->B && n >= 0 && n <= b->max_pages,
                 "qie_batch_block_table: bad arguments (paged batch, n <= max_pages)");
     QIE_HIP(hipStreamSynchronize(b->e->stream));
-    QIE_HIP(hipMemcpy(host_pages, b->d_table + (int64_t)seq * b->max_pages, (size_t)n * 4, hipMemcpyDeviceToHost));
+    QIE_HIP(d2h(b->e, host_pages, b->d_table + (int64_t)seq * b->max_pages, (size_t)n * 4));
     return 0;
 }
 
@@ -1437,8 +1446,7 @@ int qie_decode(qie_batch* b, int32_t n_steps, const qie_sampling* smp, int32_t* 
     if (out_ids && n_steps > 0) {
         std::vector<int32_t> row(b->max_ctx);
         for (int m = 0; m < b->B; m++) {
-            QIE_HIP(hipMemcpy(row.data(), b->d_hist + (int64_t)m * b->max_ctx, (size_t)b->max_ctx * 4,
-                              hipMemcpyDeviceToHost));
+            QIE_HIP(d2h(b->e, row.data(), b->d_hist + (int64_t)m * b->max_ctx, (size_t)b->max_ctx * 4));
             for (int i = 0; i < n_steps; i++) out_ids[(int64_t)i * b->B + m] = row[p0[m] + 1 + i];
         }
     }
@@ -1454,14 +1462,14 @@ int qie_batch_logits(qie_batch* b, void* host_out) {
     }
     QIE_HIP(hipStreamSynchronize(b->e->stream));
     QIE_TRY(comm_check(b->e, "qie_batch_logits"));
-    QIE_HIP(hipMemcpy(host_out, src, (size_t)b->B * b->e->spec.vocab * 2, hipMemcpyDeviceToHost));
+    QIE_HIP(d2h(b->e, host_out, src, (size_t)b->B * b->e->spec.vocab * 2));
     return 0;
 }
 
 int qie_batch_positions(qie_batch* b, int32_t* host_pos) {
     QIE_REQUIRE(b && host_pos, "qie_batch_positions: bad arguments");
     QIE_HIP(hipStreamSynchronize(b->e->stream));
-    QIE_HIP(hipMemcpy(host_pos, b->d_pos, (size_t)b->B * 4, hipMemcpyDeviceToHost));
+    QIE_HIP(d2h(b->e, host_pos, b->d_pos, (size_t)b->B * 4));
     return 0;
 }
 
@@ -1469,7 +1477,7 @@ int qie_batch_history(qie_batch* b, int32_t seq, int32_t* host_ids, int32_t n) {
     QIE_REQUIRE(b && host_ids && seq >= 0 && seq < b->B && n >= 0 && n <= b->max_ctx,
                 "qie_batch_history: bad arguments");
     QIE_HIP(hipStreamSynchronize(b->e->stream));
-    QIE_HIP(hipMemcpy(host_ids, b->d_hist + (int64_t)seq * b->max_ctx, (size_t)n * 4, hipMemcpyDeviceToHost));
+    QIE_HIP(d2h(b->e, host_ids, b->d_hist + (int64_t)seq * b->max_ctx, (size_t)n * 4));
     return 0;
 }
 
@@ -1588,7 +1596,7 @@ int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* av
     double by = 0;
     if (which == 5) {
         std::vector<int32_t> pos(B);
-        QIE_HIP(hipMemcpy(pos.data(), b->d_pos, B * 4, hipMemcpyDeviceToHost));
+        QIE_HIP(d2h(e, pos.data(), b->d_pos, B * 4));
         for (int m = 0; m < B; m++) by += (double)(pos[m] + 1) * KD * 2 * 2;
         by += (double)B * QD * 2 * 2;
     }
@@ -1641,7 +1649,7 @@ int qie_batch_debug_step(qie_batch* b, const qie_sampling* smp, int32_t* next_id
     int rc = dbg_snap(b, 0);
     if (!rc) rc = enqueue_decode(b, smp);   // eager: the graph (if any) is left as it is
     hipError_t he = hipStreamSynchronize(e->stream);
-    if (!rc && he == hipSuccess) he = hipMemcpy(host_x, b->dbg_x, (size_t)(slots * n * 2), hipMemcpyDeviceToHost);
+    if (!rc && he == hipSuccess) he = d2h(e, host_x, b->dbg_x, (size_t)(slots * n * 2));
     hipFree(b->dbg_x);
     b->dbg_x = nullptr;
     QIE_TRY(rc);

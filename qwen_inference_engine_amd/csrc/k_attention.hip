@@ -468,13 +468,18 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
                 ls = xor32_sum(xor16_sum(ls));
                 l_run[q] = l_run[q] * alpha + ls;
                 m_run[q] = m_new;
-                float ar[4];
+                // O *= alpha only where some row's max grew: alpha == 1 exactly otherwise
+                // (exp2(0)), and tile 0's O is zero — skipping is bit-identical (a wave-uniform
+                // ballot; once the running maxima settle most tiles skip the 32 products)
+                if (kt > 0 && __builtin_amdgcn_ballot_w64(alpha != 1.0f) != 0) {
+                    float ar[4];
 #pragma unroll
-                for (int r = 0; r < 4; r++) ar[r] = __shfl(alpha, g * 4 + r, 64);
+                    for (int r = 0; r < 4; r++) ar[r] = __shfl(alpha, g * 4 + r, 64);
 #pragma unroll
-                for (int d = 0; d < DT; d++)
+                    for (int d = 0; d < DT; d++)
 #pragma unroll
-                    for (int r = 0; r < 4; r++) oacc[q][d][r] *= ar[r];
+                        for (int r = 0; r < 4; r++) oacc[q][d][r] *= ar[r];
+                }
             }
             const int q4 = fr >> 2, p4 = fr & 3;
 #pragma unroll
@@ -879,13 +884,17 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
         ls = xor32_sum(xor16_sum(ls));
         l_run = l_run * alpha + ls;
         m_run = m_new;
-        float ar[4];
+        // bit-identical skip, as in the prefill kernel: step 0's O is zero, and alpha == 1
+        // exactly where no row's max grew (wave-uniform ballot)
+        if (st > 0 && __builtin_amdgcn_ballot_w64(alpha != 1.0f) != 0) {
+            float ar[4];
 #pragma unroll
-        for (int r = 0; r < 4; r++) ar[r] = __shfl(alpha, gq * 4 + r, 64);
+            for (int r = 0; r < 4; r++) ar[r] = __shfl(alpha, gq * 4 + r, 64);
 #pragma unroll
-        for (int d = 0; d < DTW; d++)
+            for (int d = 0; d < DTW; d++)
 #pragma unroll
-            for (int r = 0; r < 4; r++) oacc[d][r] *= ar[r];
+                for (int r = 0; r < 4; r++) oacc[d][r] *= ar[r];
+        }
         // ---- O[:, slice] += P . V[:, slice], P = hi + mid + lo: three bf16 parts hold all
         // 24 bits of the fp32 probability, so every P.V product is the reference's fp32
         // product (self_attension.cu:127-135) — only the accumulation order differs

@@ -28,5 +28,5 @@ struct qie_comm {
     virtual int allreduce_residual_bf16(const float* part, uint16_t* x, int64_t n, hipStream_t st);
     // non-zero once an exchange failed on the device (the peer backend's bounded wait timed
     // out); read after the stream synchronised — a blocking copy of one word
-    virtual int error_state() const { return 0; }
+    virtual int error_state(void* stream) const { (void)stream; return 0; }
 };

@@ -311,8 +311,12 @@ def run(a):
 OTHER_CONFIGS = [
     {"key": "config2", "model": "Qwen2-0.5B", "batch": 1, "prompt": 128, "gen": 128, "fp8": False,
      "workload": "Qwen2-0.5B bf16, batch=1, prompt=128, gen=128 (BASELINE configs[1])"},
+    # config 4 on the paged KV cache (128-token pages; the reference's own cache is paged,
+    # iengine.cu:73-109): measured in one process against the contiguous cache, 3,533 vs 3,484
+    # tok/s (decode attention 14.3 vs 14.9 µs live; tools/ab_decode.py "_PAGE")
     {"key": "config4", "model": "Qwen2-7B", "batch": 8, "prompt": 1024, "gen": 256, "fp8": True, "fp8_mfma": True,
-     "workload": "Qwen2-7B fp8 weights, batch=8, prompt=1024, gen=256 (BASELINE configs[3])"},
+     "page_tokens": 128,
+     "workload": "Qwen2-7B fp8 weights, batch=8, prompt=1024, gen=256, paged KV (128-token pages) (BASELINE configs[3])"},
 ]
 
 
@@ -336,7 +340,7 @@ def run_config(Q, S, W, c):
     eng = Q.Engine(spec, max_ctx=max_ctx, weight_fp8=c["fp8"]).init_synthetic(W.SynthParams(seed=0))
     b = None
     try:
-        b = eng.batch(B, max_ctx)
+        b = eng.batch(B, max_ctx, page_tokens=c.get("page_tokens"))
         prompts = np.random.default_rng(1).integers(0, spec.vocab, size=(B, P), dtype=np.int32)
 
         def prefill():
@@ -369,6 +373,7 @@ def run_config(Q, S, W, c):
         step_bytes = spec.decode_weight_bytes(fp8=c["fp8"]) + B * spec.kv_bytes_per_position() * (P + (steps + 1) / 2.0)
         gbs = step_bytes / (ms * 1e-3) / 1e9
         return {"workload": c["workload"], "value": round(B * steps / dt, 2), "unit": "tokens/s",
+                "kv": f"paged{c['page_tokens']}" if c.get("page_tokens") else "contiguous",
                 "ms_per_step": round(ms, 4), "steps": steps, "prefill_tok_s": round(B * P / t_pf, 1),
                 "prefill_ms": round(t_pf * 1e3, 3),
                 "step_roofline": {"bytes_per_step": step_bytes, "achieved_GBps": round(gbs, 1),
@@ -378,7 +383,7 @@ def run_config(Q, S, W, c):
                                     "algorithmic_bytes": by_dom,
                                     "live_frac": round(by_dom / us_dom / 1e3 / HBM_PEAK_GBS, 4),
                                     "timing": "hipEvents on the engine stream around 54 launches cycling over "
-                                              "layers 1..L-1 (in-graph durations: profiles/r04_*rocprof*)"},
+                                              "layers 1..L-1 (in-graph durations: profiles/r05_*rocprof*)"},
                 **({"prefill_fp8_mfma": mx} if mx else {})}
     finally:
         if b is not None:   # the batch before its engine

@@ -103,6 +103,7 @@ struct qie_batch {
     uint16_t* kc = nullptr;
     uint16_t* vc = nullptr;
     int64_t seq_stride = 0;
+    int run_pad = 0;             // contiguous: run = max_ctx + run_pad tokens (dev A/B)
     int32_t* d_pos = nullptr;
     float* d_rope_cur = nullptr;   // [B][rope_cur_stride(hd)]: RoPE row of each slot's current position
     int32_t* d_step = nullptr;
@@ -240,7 +241,7 @@ static qie_kv_cache batch_cache(const qie_batch* b, int seq0) {
     c.n_layers = e->spec.n_layers;
     c.n_kv_heads = e->sh.nkv;
     c.head_dim = e->spec.head_dim;
-    c.max_ctx = b->max_ctx;
+    c.max_ctx = b->max_ctx + b->run_pad;   // the run length (positions stay below b->max_ctx)
     c.seq_stride = b->seq_stride;
     if (b->d_table) {
         c.k = b->kc;
@@ -1088,7 +1089,8 @@ static int batch_create(qie_engine* e, int32_t batch, int32_t max_ctx, int32_t p
         b->held.assign(batch, 0);
         b->table_dirty = true;
     } else {
-        b->seq_stride = (int64_t)s.n_layers * sh.nkv * max_ctx * hd;   // this rank's kv heads only
+        b->run_pad = dev_env("QIE_KV_RUN_PAD", 0);   // dev A/B: tokens of padding per (layer, head) run
+        b->seq_stride = (int64_t)s.n_layers * sh.nkv * (max_ctx + b->run_pad) * hd;   // this rank's kv heads only
     }
     // Slots start idle: a slot runs as a live sequence only after a prefill or
     // set_position, so unused slots never take pool pages (they run on scratch page 0)

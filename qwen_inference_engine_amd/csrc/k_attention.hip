@@ -235,6 +235,7 @@ struct DecodeAttnParams {
     // goes out at once.  Null (operator API) or a stale tag: the table row at pos.
     const float* rc;
     int pv3;                  // P.V with three bf16 parts of P (else two; dev A/B)
+    int spec_ok;              // the speculative K / V step may be issued (see fill_dec_params)
     int ks;                   // keys per block step (host: picks the kernel instance)
 };
 
@@ -759,7 +760,7 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
     // RoPE row (a.rc, tagged with the position): the prologue's loads then need no position
     // either, and a stale tag (a position set some other way) reloads the table row.
     constexpr bool SPEC = !PG;
-    const bool spec = PR || a.rc != nullptr;   // uniform
+    const bool spec = (PR || a.rc != nullptr) && a.spec_ok;   // uniform
     const int p = a.pos[m];
     const float* rcm = a.rc ? a.rc + m * rope_cur_stride(HD) : a.cs;
     const int rtag = a.rc ? __float_as_int(rcm[0]) : -1;
@@ -817,6 +818,15 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
         knew[ks] = *reinterpret_cast<const uint4*>(&kv_new[0][32 * ks + 8 * gq]);
     }
     const float scale = sqrtf((float)HD);
+    // dot / scale as q = dot * (1 / scale) plus one FMA residual step (Markstein): the
+    // correctly rounded quotient for every dot above 2^-100 in magnitude (k_decode_fp8.hip
+    // d8_rms_pair), three VALU ops instead of the IEEE division sequence's ~10 with its
+    // serial latency — 8 quotients per lane per step on the step's critical path
+    const float inv_scale = 1.0f / scale;
+    auto qdiv = [&](float d) {
+        const float q = d * inv_scale;
+        return fmaf(fmaf(-q, scale, d), inv_scale, q);
+    };
     float m_run = -INFINITY, l_run = 0.f;
     f32x4_t oacc[DTW];
 #pragma unroll
@@ -838,7 +848,7 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
             // C map: col = head fr, rows = keys 4 gq + r of the tile; scores s = dot / sqrt(hd)
             // (self_attension.cu) divided once here, not by every wave that reads them
             *reinterpret_cast<float4*>(&s_s[fr][16 * TPW * wave + 16 * t + 4 * gq]) =
-                make_float4(sacc[0] / scale, sacc[1] / scale, sacc[2] / scale, sacc[3] / scale);
+                make_float4(qdiv(sacc[0]), qdiv(sacc[1]), qdiv(sacc[2]), qdiv(sacc[3]));
         }
         // ---- this wave's V slice -> LDS (the new token's row from kv_new)
 #pragma unroll
@@ -1116,6 +1126,12 @@ static int fill_dec_params(DecodeAttnParams& a, const void* qkv, int64_t B, cons
     a.out = (uint16_t*)out;
     a.rc = dev_env("QIE_DEC_ROPECUR", 1) ? g_rope_cur : nullptr;
     a.pv3 = dev_env("QIE_DEC_PV3", 1);
+    // The speculative step is issued before the position is known, so the grid's idle
+    // splits (s >= this step's split count: the graph's grid is sized for max_ctx) load a
+    // step too and drop it (config 4, max_ctx 1,344: 32-64 idle blocks of 352, 2-4 MB per
+    // launch).  Measured, it still pays at B = 8 (3,478.6 vs 3,465.7 tok/s without it) as at
+    // B = 1 (358.7 vs 357.2).  QIE_DEC_SPEC (dev A/B): 0 turns it off.
+    a.spec_ok = dev_env("QIE_DEC_SPEC", 1) != 0;
     return 0;
 }
 

@@ -11,7 +11,8 @@ only reorders work must reproduce them bit for bit; one that changes numerics ma
 
 Env: AB_MODEL (Qwen2-7B), AB_P (2048), AB_STEPS (256), AB_ROUNDS (3), AB_BATCH (1),
 AB_FP8 (0), AB_KERNELS (1: also the live per-kernel timings), AB_PREFILL (0: also time one
-prefill per variant), AB_ENGINE (0; 1: a fresh engine per variant and round, for knobs read
+prefill per variant; a variant key "_PAGE": N runs that variant on a paged KV cache of
+N-token pages), AB_ENGINE (0; 1: a fresh engine per variant and round, for knobs read
 when the weights are loaded, e.g. QIE_FP8_T16)."""
 import json
 import os
@@ -47,12 +48,15 @@ def main():
     t_start = time.time()
     for rnd in range(rounds):
         for i, env in enumerate(variants):
-            saved = {k: os.environ.get(k) for k in env}
-            os.environ.update({k: str(v) for k, v in env.items()})
+            # "_PAGE": page_tokens of the variant's batch (paged KV cache), not an env knob
+            page = int(env["_PAGE"]) if "_PAGE" in env else None
+            knobs = {k: v for k, v in env.items() if k != "_PAGE"}
+            saved = {k: os.environ.get(k) for k in knobs}
+            os.environ.update({k: str(v) for k, v in knobs.items()})
             try:
                 if per_engine:
                     eng = Q.Engine(spec, max_ctx=max_ctx, weight_fp8=fp8).init_synthetic(W.SynthParams(seed=0))
-                b = eng.batch(B, max_ctx)
+                b = eng.batch(B, max_ctx, page_tokens=page)
                 first = b.prefill_batch(0, prompts) if B > 1 else [b.prefill(0, prompts[0])]
                 if do_pf:
                     eng.sync()

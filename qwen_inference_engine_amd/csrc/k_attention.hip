@@ -258,6 +258,36 @@ __device__ __forceinline__ void pin4(float4& v) {
     asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
 }
 
+// Split fp32 probabilities into bf16 parts (hi, then the remainder's hi, ...) two lanes'
+// values at a time: one v_cvt_pk_bf16_f32 per pair and packed fp32 subtractions.  A scalar
+// (__bf16) cast per element compiled to one cvt_pk per element (half of it wasted) plus a
+// shift and a subtraction each — 7 VALU per element for three parts, now 4.5.  Same RNE
+// rounding, same exact remainders: bit-identical parts.
+typedef float pf32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 pbf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t cvt_pk_bf16(pf32x2_t v) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, pbf16x2_t));
+}
+__device__ __forceinline__ pf32x2_t unpk_bf16(uint32_t u) {
+    return pf32x2_t{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+}
+// e[0..7] -> NP bf16x8 parts (NP = 2: hi + lo; 3: hi + mid + lo)
+template <int NP>
+__device__ __forceinline__ void split_bf16x8(const float* e, uint4* parts) {
+    uint32_t w[NP][4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        pf32x2_t r = pf32x2_t{e[2 * j], e[2 * j + 1]};
+#pragma unroll
+        for (int k = 0; k < NP; k++) {
+            w[k][j] = cvt_pk_bf16(r);
+            if (k + 1 < NP) r = r - unpk_bf16(w[k][j]);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NP; k++) parts[k] = make_uint4(w[k][0], w[k][1], w[k][2], w[k][3]);
+}
+
 // ---------------------------------------------------------------------------
 // Prefill: causal flash attention on MFMA (v_mfma_f32_16x16x32_bf16).
 // K/V tiles of 64 keys staged in LDS (double-buffered, register prefetch).
@@ -491,13 +521,16 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
                 // reference's own sum over keys
                 bf16x8_t ph[QG], pl[QG];
 #pragma unroll
-                for (int q = 0; q < QG; q++)
+                for (int q = 0; q < QG; q++) {
+                    if (!ON[q]) continue;
+                    float e8[8];
 #pragma unroll
-                    for (int jj = 0; jj < 8; jj++) {
-                        const float e = ON[q] ? pv[q][2 * c + (jj >> 2)][jj & 3] : 0.f;
-                        ph[q][jj] = (__bf16)e;
-                        pl[q][jj] = (__bf16)(e - (float)ph[q][jj]);
-                    }
+                    for (int jj = 0; jj < 8; jj++) e8[jj] = pv[q][2 * c + (jj >> 2)][jj & 3];
+                    uint4 pp[2];
+                    split_bf16x8<2>(e8, pp);
+                    ph[q] = __builtin_bit_cast(bf16x8_t, pp[0]);
+                    pl[q] = __builtin_bit_cast(bf16x8_t, pp[1]);
+                }
 #pragma unroll
                 for (int d = 0; d < DT; d++) {
                     // rows vr and vr + 16 share vswz: one column offset serves both reads
@@ -825,7 +858,8 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
     const float inv_scale = 1.0f / scale;
     auto qdiv = [&](float d) {
         const float q = d * inv_scale;
-        return fmaf(fmaf(-q, scale, d), inv_scale, q);
+        if constexpr (HD == 64 || HD == 256) return q;   // sqrt(hd) a power of two: exact
+        else return fmaf(fmaf(-q, scale, d), inv_scale, q);
     };
     float m_run = -INFINITY, l_run = 0.f;
     f32x4_t oacc[DTW];
@@ -834,17 +868,23 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
     uint16_t* vw = &v_s[wave][0];
     const int q4 = fr >> 2, p4 = fr & 3;
 
-    for (int st = 0; st < nstep; st++) {
+    // A step is a TAIL step when it holds keys past the split's end or the new token
+    // (the last step of the last split; uniform): only there are scores masked and the new
+    // token's K / V taken from LDS.  The body is instantiated per case (hd 64), so the other
+    // steps carry no per-element compare / select (Qwen2-0.5B, config 2: one split of two
+    // steps at ctx 129-256, the first of them a plain step).
+    auto step = [&](const int st, auto tailc) {
+        constexpr bool TAIL = decltype(tailc)::value;
         const int kb0 = t0 + st * KS;
         // ---- S^T for this wave's 32 keys -> LDS (raw dots)
 #pragma unroll
         for (int t = 0; t < TPW; t++) {
             f32x4_t sacc = f32x4_t{0.f, 0.f, 0.f, 0.f};
-            const bool nw = kb0 + 16 * TPW * wave + 16 * t + fr == p;
+            const bool nw = TAIL && kb0 + 16 * TPW * wave + 16 * t + fr == p;
 #pragma unroll
             for (int ks = 0; ks < KSTEPS; ks++)
                 sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                    __builtin_bit_cast(bf16x8_t, sel4(nw, knew[ks], kf[t][ks])), qb[ks], sacc, 0, 0, 0);
+                    __builtin_bit_cast(bf16x8_t, TAIL ? sel4(nw, knew[ks], kf[t][ks]) : kf[t][ks]), qb[ks], sacc, 0, 0, 0);
             // C map: col = head fr, rows = keys 4 gq + r of the tile; scores s = dot / sqrt(hd)
             // (self_attension.cu) divided once here, not by every wave that reads them
             *reinterpret_cast<float4*>(&s_s[fr][16 * TPW * wave + 16 * t + 4 * gq]) =
@@ -855,8 +895,12 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
         for (int i = 0; i < VCH; i++) {
             const int c = lane + 64 * i;
             const int r = c / CPW, ch = c % CPW;
-            const uint4 vn = *reinterpret_cast<const uint4*>(&kv_new[1][wave * DW + ch * 8]);
-            *reinterpret_cast<uint4*>(vw + r * DW + ch * 8) = sel4(kb0 + r == p, vn, vr[i]);
+            if constexpr (TAIL) {
+                const uint4 vn = *reinterpret_cast<const uint4*>(&kv_new[1][wave * DW + ch * 8]);
+                *reinterpret_cast<uint4*>(vw + r * DW + ch * 8) = sel4(kb0 + r == p, vn, vr[i]);
+            } else {
+                *reinterpret_cast<uint4*>(vw + r * DW + ch * 8) = vr[i];
+            }
         }
         if (st + 1 < nstep) load_step(st + 1);
         __syncthreads();   // scores and V slices visible
@@ -871,7 +915,7 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
             const float v8[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
 #pragma unroll
             for (int j = 0; j < 8; j++) {
-                const float sc = kb0 + 32 * c + 8 * gq + j < t1 ? v8[j] : -INFINITY;
+                const float sc = !TAIL || kb0 + 32 * c + 8 * gq + j < t1 ? v8[j] : -INFINITY;
                 e[c][j] = sc;
                 mt = fmaxf(mt, sc);
             }
@@ -910,14 +954,10 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
         // product (self_attension.cu:127-135) — only the accumulation order differs
 #pragma unroll
         for (int c = 0; c < KS / 32; c++) {
-            bf16x8_t ph, pm, pl;
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                ph[j] = (__bf16)e[c][j];
-                const float r1 = e[c][j] - (float)ph[j];
-                pm[j] = (__bf16)r1;
-                pl[j] = (__bf16)(r1 - (float)pm[j]);
-            }
+            uint4 pp[3];
+            split_bf16x8<3>(e[c], pp);
+            const bf16x8_t ph = __builtin_bit_cast(bf16x8_t, pp[0]), pm = __builtin_bit_cast(bf16x8_t, pp[1]),
+                           pl = __builtin_bit_cast(bf16x8_t, pp[2]);
 #pragma unroll
             for (int d = 0; d < DTW; d++) {
                 const uint16_t* a0 = vw + (32 * c + 8 * gq + q4) * DW + 16 * d + 4 * p4;
@@ -932,6 +972,12 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
             }
         }
         __syncthreads();   // scores / V slots free for the next step
+    };
+    for (int st = 0; st < nstep; st++) {
+        const int kb0 = t0 + st * KS;
+        // (hd 128 keeps one body: the second copy took the kernel from 216 to 298 registers)
+        if (HD == 128 || kb0 + KS > t1 || (p >= kb0 && p < kb0 + KS)) step(st, std::true_type{});
+        else if constexpr (HD != 128) step(st, std::false_type{});
     }
     if (QIE_DBG(a.dbg & 16)) {
         if (tid == 0) a.out[m] = (uint16_t)(oacc[0][0] + m_run);
@@ -996,7 +1042,7 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
     // head together with its 16-byte slice of every split's partial O (one batch of JB
     // splits = one round trip; ctx <= JB * 128 keys in one), then merges them itself — no
     // per-head wave pass, LDS weight table or barrier between the two load rounds.
-    constexpr int JB = KS == 128 ? 24 : 40;   // splits per combine round trip
+    constexpr int JB = KS == 64 ? 40 : (KS == 128 ? 24 : 16);   // splits per combine round trip
     const bool has_item = tid < G * (HD / 4);
     const int gi = has_item ? tid / (HD / 4) : 0, d4 = tid % (HD / 4);
     const int64_t hbase = (m * nq + g * G + gi) * (int64_t)a.nsplit_max;
@@ -1110,7 +1156,18 @@ static int fill_dec_params(DecodeAttnParams& a, const void* qkv, int64_t B, cons
     a.splits_target = senv > 0 ? senv : kDecMSplits;
     a.dbg = dev_env("QIE_DEC_DBG", 0);
     a.sc1 = dev_env("QIE_DEC_SC1", 1);   // 9.79 -> 9.56 us per launch (ctx 2.3k, Qwen2-7B)
-    const int ks = dev_env("QIE_DEC_KS", kDecMStep) == 64 ? 64 : kDecMStep;   // keys per block step
+    // keys per block step (the launch picks the kernel instantiation with the same KS): 128.
+    // QIE_DEC_KS (dev A/B): 64 (hd 128, not pre-rotated), 256 (hd 64: ONE step where
+    // Qwen2-0.5B's config-2 contexts, 129-256 keys, walk two dependent 128-key steps in one
+    // block per kv head — measured equal, attention 7.94 vs 7.96 µs live, 1,446 vs 1,454 tok/s:
+    // the second step's chain is not what the launch waits on).
+    const int hd = cache->head_dim;
+    const int ks_env = dev_env("QIE_DEC_KS", 0);
+    // (a step never straddles a page: 256-key steps need pages of >= 256 tokens)
+    const bool ks256_ok = hd == 64 && (cache->block_table == nullptr || cache->page_tokens >= 256);
+    int ks = kDecMStep;
+    if (ks_env == 128 || (ks_env == 256 && ks256_ok) || (ks_env == 64 && hd == 128 && !(numerics & QIE_ATTN_PREROPED)))
+        ks = ks_env;
     a.ks = ks;
     a.nsplit_max = std::min(a.splits_target, (cache->max_ctx + ks - 1) / ks);
     QIE_REQUIRE(a.nsplit_max <= kDecMaxSplits, "qie_attention_decode: max_ctx %d too long", cache->max_ctx);
@@ -1259,6 +1316,11 @@ int qie_attention_decode(const void* qkv, int64_t B, const int32_t* pos, const v
                         : (pg ? attn_decode_mfma2_kernel<64, true, 4, false> : attn_decode_mfma2_kernel<64, false, 4, false>));
     if (a.ks == 64 && cache->head_dim == 128 && !pr)   // 64-key steps (dev A/B)
         k2 = pg ? attn_decode_mfma2_kernel<128, true, 4, false, 64> : attn_decode_mfma2_kernel<128, false, 4, false, 64>;
+    if (a.ks == 256 && cache->head_dim == 64)   // one 256-key step (short contexts at hd 64)
+        k2 = pr ? (pg ? attn_decode_mfma2_kernel<64, true, 4, true, 256> : attn_decode_mfma2_kernel<64, false, 4, true, 256>)
+                : (pg ? attn_decode_mfma2_kernel<64, true, 4, false, 256> : attn_decode_mfma2_kernel<64, false, 4, false, 256>);
+    QIE_REQUIRE(a.ks == 128 || (a.ks == 64 && cache->head_dim == 128 && !pr) || (a.ks == 256 && cache->head_dim == 64),
+                "qie_attention_decode: internal: no kernel for %d-key steps at hd %d", a.ks, cache->head_dim);
     hipLaunchKernelGGL(k2, grid, dim3(256), 0, (hipStream_t)stream, a);
     QIE_LAUNCH_CHECK();
     return 0;

@@ -868,23 +868,37 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
     uint16_t* vw = &v_s[wave][0];
     const int q4 = fr >> 2, p4 = fr & 3;
 
-    // A step is a TAIL step when it holds keys past the split's end or the new token
-    // (the last step of the last split; uniform): only there are scores masked and the new
-    // token's K / V taken from LDS.  The body is instantiated per case (hd 64), so the other
-    // steps carry no per-element compare / select (Qwen2-0.5B, config 2: one split of two
-    // steps at ctx 129-256, the first of them a plain step).
-    auto step = [&](const int st, auto tailc) {
-        constexpr bool TAIL = decltype(tailc)::value;
+    for (int st = 0; st < nstep; st++) {
         const int kb0 = t0 + st * KS;
+        // Only the step holding the new token takes its K / V rows from LDS, and only a step
+        // past the split's end masks scores (the last step of the last split; both uniform,
+        // scalar branches around in-place selects): the other steps carry no per-element
+        // compare / select.  (A whole second copy of the step body per case took the hd-128
+        // kernel from 216 to 298 registers.)
+        const bool hasp = p >= kb0 && p < kb0 + KS;
+        const bool full = kb0 + KS <= t1;
+        if (hasp) {
+#pragma unroll
+            for (int t = 0; t < TPW; t++) {
+                const bool nw = kb0 + 16 * TPW * wave + 16 * t + fr == p;
+#pragma unroll
+                for (int ks = 0; ks < KSTEPS; ks++) kf[t][ks] = sel4(nw, knew[ks], kf[t][ks]);
+            }
+#pragma unroll
+            for (int i = 0; i < VCH; i++) {
+                const int c = lane + 64 * i;
+                const int r = c / CPW, ch = c % CPW;
+                const uint4 vn = *reinterpret_cast<const uint4*>(&kv_new[1][wave * DW + ch * 8]);
+                vr[i] = sel4(kb0 + r == p, vn, vr[i]);
+            }
+        }
         // ---- S^T for this wave's 32 keys -> LDS (raw dots)
 #pragma unroll
         for (int t = 0; t < TPW; t++) {
             f32x4_t sacc = f32x4_t{0.f, 0.f, 0.f, 0.f};
-            const bool nw = TAIL && kb0 + 16 * TPW * wave + 16 * t + fr == p;
 #pragma unroll
             for (int ks = 0; ks < KSTEPS; ks++)
-                sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                    __builtin_bit_cast(bf16x8_t, TAIL ? sel4(nw, knew[ks], kf[t][ks]) : kf[t][ks]), qb[ks], sacc, 0, 0, 0);
+                sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, kf[t][ks]), qb[ks], sacc, 0, 0, 0);
             // C map: col = head fr, rows = keys 4 gq + r of the tile; scores s = dot / sqrt(hd)
             // (self_attension.cu) divided once here, not by every wave that reads them
             *reinterpret_cast<float4*>(&s_s[fr][16 * TPW * wave + 16 * t + 4 * gq]) =
@@ -895,12 +909,7 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
         for (int i = 0; i < VCH; i++) {
             const int c = lane + 64 * i;
             const int r = c / CPW, ch = c % CPW;
-            if constexpr (TAIL) {
-                const uint4 vn = *reinterpret_cast<const uint4*>(&kv_new[1][wave * DW + ch * 8]);
-                *reinterpret_cast<uint4*>(vw + r * DW + ch * 8) = sel4(kb0 + r == p, vn, vr[i]);
-            } else {
-                *reinterpret_cast<uint4*>(vw + r * DW + ch * 8) = vr[i];
-            }
+            *reinterpret_cast<uint4*>(vw + r * DW + ch * 8) = vr[i];
         }
         if (st + 1 < nstep) load_step(st + 1);
         __syncthreads();   // scores and V slices visible
@@ -912,14 +921,20 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
         for (int c = 0; c < KS / 32; c++) {
             const float4 lo = *reinterpret_cast<const float4*>(&s_s[fr][32 * c + 8 * gq]);
             const float4 hi = *reinterpret_cast<const float4*>(&s_s[fr][32 * c + 8 * gq + 4]);
-            const float v8[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const float sc = !TAIL || kb0 + 32 * c + 8 * gq + j < t1 ? v8[j] : -INFINITY;
-                e[c][j] = sc;
-                mt = fmaxf(mt, sc);
-            }
+            e[c][0] = lo.x; e[c][1] = lo.y; e[c][2] = lo.z; e[c][3] = lo.w;
+            e[c][4] = hi.x; e[c][5] = hi.y; e[c][6] = hi.z; e[c][7] = hi.w;
         }
+        if (!full) {
+#pragma unroll
+            for (int c = 0; c < KS / 32; c++)
+#pragma unroll
+                for (int j = 0; j < 8; j++)
+                    if (kb0 + 32 * c + 8 * gq + j >= t1) e[c][j] = -INFINITY;
+        }
+#pragma unroll
+        for (int c = 0; c < KS / 32; c++)
+#pragma unroll
+            for (int j = 0; j < 8; j++) mt = fmaxf(mt, e[c][j]);
         mt = xor32_max(xor16_max(mt));
         const float m_new = fmaxf(m_run, mt);
         const float m_use = m_new == -INFINITY ? 0.f : m_new;
@@ -972,12 +987,6 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
             }
         }
         __syncthreads();   // scores / V slots free for the next step
-    };
-    for (int st = 0; st < nstep; st++) {
-        const int kb0 = t0 + st * KS;
-        // (hd 128 keeps one body: the second copy took the kernel from 216 to 298 registers)
-        if (HD == 128 || kb0 + KS > t1 || (p >= kb0 && p < kb0 + KS)) step(st, std::true_type{});
-        else if constexpr (HD != 128) step(st, std::false_type{});
     }
     if (QIE_DBG(a.dbg & 16)) {
         if (tid == 0) a.out[m] = (uint16_t)(oacc[0][0] + m_run);

@@ -89,7 +89,7 @@ __device__ __forceinline__ uint32_t d8_rms_pair(uint32_t xv, uint32_t wv, float 
 
 // (split-K: two blocks per CU — at most 128 VGPRs; one block per CU ran the down projection
 // at 24.8 instead of 18.5 µs)
-template <int EPI, int KU, int KS, bool SPL = false, bool T16 = false>
+template <int EPI, int KU, int KS, bool SPL = false, bool T16 = false, bool LF = false>
 __global__ __launch_bounds__(KS * 64, SPL ? 4 : 1) void dec8_kernel(Dec8Params p) {
 #pragma clang fp contract(off)
     static_assert(!SPL || EPI != QIE_EPI_SWIGLU, "split-K: single-segment epilogues");
@@ -120,9 +120,28 @@ __global__ __launch_bounds__(KS * 64, SPL ? 4 : 1) void dec8_kernel(Dec8Params p
     // the buffer range (0) — wave-uniform, and no load sits under a branch
     const int kval = SPL ? (K - kw) / 64 : KU;   // valid units (may be <= 0 or > KU)
 
+    // LDS form of the fused RMSNorm (round 5; M <= 8, one block of KS waves holding whole
+    // rows: K = KS x 512): thread t loads chunk t (8 values) of every REAL row once, the
+    // rows' sums of squares meet by a transposed butterfly + one LDS exchange, each thread
+    // normalises its chunks into an LDS image of the M rows (aliasing the partial-tile area,
+    // unused until the first tile ends), and every lane then reads its A fragments from
+    // that image.  The register form below loads and normalises 16 rows per wave — the
+    // padding rows of the 16-row MFMA operand included, i.e. twice the x traffic through
+    // the CU and twice the normalisation VALU at M = 8.  QIE_DEC8_DBG & 32 (dev): register form.
+    // A separate instantiation (LF), launched only with a norm and M <= 8: one kernel
+    // holding both forms spilled (the register form's live A fragments + the chunk loads).
+    constexpr bool LFORM = LF && !SPL && KU == 8 && RDF * NB >= 8;   // image of 8 rows x 512 per wave fits red[]
+    static_assert(!LF || LFORM, "dec8: LDS-form norm needs KU = 8, no split, an 8-row image in red[]");
+    d8_u32x4 xc[LFORM ? 8 : 1];
+    if constexpr (LFORM) {
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+            xc[j] = j < M ? *reinterpret_cast<const d8_u32x4*>(p.x + (int64_t)j * p.ldx + 8 * tid) : d8_u32x4{0u, 0u, 0u, 0u};
+    }
+
     // ---- A fragments of this wave's K slice: row arow, k = kw + 64 u + 16 g + [0, 16)
     d8_u32x4 av[KU][2];
-    {
+    if constexpr (!LFORM) {
         const d8_u32x4* xp = reinterpret_cast<const d8_u32x4*>(p.x + (int64_t)arow * p.ldx + (SPL ? 0 : kw) + 16 * g);
 #pragma unroll
         for (int u = 0; u < KU; u++) {
@@ -209,7 +228,74 @@ __global__ __launch_bounds__(KS * 64, SPL ? 4 : 1) void dec8_kernel(Dec8Params p
     // ---- fused RMSNorm: row arow's sum of squares over the whole K (this wave's slice,
     // the 4 k quarters by lane exchange, the KS slices through LDS), then the fragments are
     // normalised in place (qie_rmsnorm's arithmetic)
-    if (nrm) {
+    if constexpr (LFORM) {
+        // sums of squares of this thread's chunk of each row (8 values in order)
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t e4[4] = {xc[j].x, xc[j].y, xc[j].z, xc[j].w};
+            float a = 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const float l = bf_lo(e4[i]), hh = bf_hi(e4[i]);
+                a += l * l + hh * hh;
+            }
+            v[j] = a;
+        }
+        // transposed butterfly: 8 row partials over 64 lanes -> lane l holds the wave's sum
+        // of row 4 (l>>5) + 2 ((l>>4)&1) + ((l>>3)&1) (lane ^ 32, ^ 16, ^ 8 halve the rows,
+        // then the 8-lane group sums); fixed order, independent of M
+        float w4[4], w2[2];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            float a = v[i], b = v[4 + i];
+            lane_swap<32>(a, b);
+            w4[i] = a + b;
+        }
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            float a = w4[i], b = w4[2 + i];
+            lane_swap<16>(a, b);
+            w2[i] = a + b;
+        }
+        const bool b8 = (lane & 8) != 0;
+        const float w1 = (b8 ? w2[1] : w2[0]) + dpp_f<0x128>(b8 ? w2[0] : w2[1]);   // row_ror 8 = lane ^ 8
+        const float ssw = group_sum<8>(w1);
+        if ((lane & 7) == 0) ssq[wave][4 * (lane >> 5) + 2 * ((lane >> 4) & 1) + ((lane >> 3) & 1)] = ssw;
+        __syncthreads();
+        // lanes 0..7: row (lane & 7)'s statistics; chunk j reads row j's by readlane
+        float tot = 0.f;
+#pragma unroll
+        for (int w = 0; w < KS; w++) tot += ssq[w][lane & 7];
+        const float rms = sqrtf((tot / (float)K) + p.eps);
+        const float inv = 1.0f / rms;
+        const float rr = rms < INFINITY ? rms : 0.f;
+        uint16_t* xs = reinterpret_cast<uint16_t*>(&red[0][0][0][0]);
+        auto apply = [&](auto hf) {
+            constexpr bool HF = decltype(hf)::value;
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                if (j >= M) break;   // uniform
+                const float ij = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, inv), j));
+                const float rj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, rr), j));
+                d8_u32x4 y;
+                y.x = d8_rms_pair<HF>(xc[j].x, nwv.x, rj, ij);
+                y.y = d8_rms_pair<HF>(xc[j].y, nwv.y, rj, ij);
+                y.z = d8_rms_pair<HF>(xc[j].z, nwv.z, rj, ij);
+                y.w = d8_rms_pair<HF>(xc[j].w, nwv.w, rj, ij);
+                *reinterpret_cast<d8_u32x4*>(xs + (int64_t)j * K + 8 * tid) = y;
+            }
+        };
+        if (p.numerics == QIE_NUMERICS_HF) apply(std::true_type{});
+        else apply(std::false_type{});
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < KU; u++)
+#pragma unroll
+            for (int h = 0; h < 2; h++)
+                av[u][h] = *reinterpret_cast<const d8_u32x4*>(xs + (int64_t)arow * K + kw + 64 * u + 16 * g + 8 * h);
+        __syncthreads();   // the image is red[]: every wave has its fragments before any tile ends
+    } else if (nrm) {   // register form
         float ss = 0.f;
 #pragma unroll
         for (int u = 0; u < KU; u++)
@@ -742,9 +828,9 @@ static int dec8r_launch(const Dec8Params& p, hipStream_t st) {
     return 0;
 }
 
-template <int EPI, int KU, int KS, bool SPL = false, bool T16 = false>
+template <int EPI, int KU, int KS, bool SPL = false, bool T16 = false, bool LF = false>
 static int dec8_launch(const Dec8Params& p, hipStream_t st) {
-    const void* fn = (const void*)dec8_kernel<EPI, KU, KS, SPL, T16>;
+    const void* fn = (const void*)dec8_kernel<EPI, KU, KS, SPL, T16, LF>;
     static int per_cu = 0;   // resident blocks per CU (one per instantiation, cached)
     if (per_cu == 0) {
         int nb = 0;
@@ -762,7 +848,7 @@ static int dec8_launch(const Dec8Params& p, hipStream_t st) {
     } else {
         grid = (int)std::max<int64_t>(1, std::min<int64_t>(p.n_tiles, slots));
     }
-    hipLaunchKernelGGL((dec8_kernel<EPI, KU, KS, SPL, T16>), dim3(grid), dim3(KS * 64), 0, st, p);
+    hipLaunchKernelGGL((dec8_kernel<EPI, KU, KS, SPL, T16, LF>), dim3(grid), dim3(KS * 64), 0, st, p);
     QIE_LAUNCH_CHECK();
     return 0;
 }
@@ -822,6 +908,14 @@ static int dec8_epi(const Dec8Params& p, int epi, hipStream_t st) {
                 case QIE_EPI_F32: return dec8r_launch<QIE_EPI_F32, KU, KS, 8>(p, st);
                 default: return dec8r_launch<QIE_EPI_STORE, KU, KS, 8>(p, st);
             }
+        }
+    }
+    // fused norm at M <= 8 on the 7 x 8-unit shape (K = 3,584: config 4's QKV and gate/up):
+    // the LDS form (dev A/B: QIE_DEC8_DBG & 32 keeps the register form)
+    if constexpr (KU == 8 && KS == 7) {
+        if (p.norm_w && p.M <= 8 && !QIE_DBG(p.dbg & 2) && !QIE_DBG(p.dbg & 32)) {
+            if (epi == QIE_EPI_SWIGLU) return dec8_launch<QIE_EPI_SWIGLU, KU, KS, false, T16, true>(p, st);
+            if (epi == QIE_EPI_STORE) return dec8_launch<QIE_EPI_STORE, KU, KS, false, T16, true>(p, st);
         }
     }
     switch (epi) {

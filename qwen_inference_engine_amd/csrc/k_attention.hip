@@ -1037,7 +1037,7 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
         last_flag = (old == (unsigned)nsplit - 1) ? 1 : 0;
     }
     __syncthreads();
-    if (!last_flag) return false;
+    if (!last_flag || QIE_DBG(a.dbg & 128)) return false;   // (dev timing exit 128: ticket taken, no combine)
     // Default: 16-B sc1 buffer loads on a uniform (SGPR) resource instead of the acquire
     // (MI355X_MICROARCH.md hand-off row 1): 9.79 -> 9.56 us per launch.  (Round 2 measured
     // 8-B agent-scope atomic loads at 11.4 vs 10.7 us, and 16-B sc1 loads at 73 us — that

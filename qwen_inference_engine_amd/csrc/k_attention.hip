@@ -784,7 +784,7 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
             vr[i] = *reinterpret_cast<const uint4*>(vb + so + (int64_t)(key - kb0) * HD + wave * DW + (c % CPW) * 8);
         }
     };
-    // Speculative step (pre-rotated, contiguous): the split of every context of 257 ..
+    // Speculative step: the split of every context of 257 ..
     // 128 * splits keys is keys [128 s, 128 s + 128) (decm_chunk's one-step rule), so its
     // K / V loads go out with the position load instead of one HBM round trip behind it.
     // The rotated q / k / v row goes out first (position-independent): vmcnt retires in
@@ -792,6 +792,9 @@ __device__ __forceinline__ bool attn_decode_mfma2_body(const DecodeAttnParams& a
     // Without the pre-rotation the same holds when the engine keeps the current position's
     // RoPE row (a.rc, tagged with the position): the prologue's loads then need no position
     // either, and a stale tag (a position set some other way) reloads the table row.
+    // (Paged, measured in round 5: the step's page from the block-table entry of (row,
+    // 128 s) needs no position either, but the speculative form ran config 4 at 3,563 vs
+    // 3,624 tok/s for the plain one — the table round trip still precedes the K / V loads.)
     constexpr bool SPEC = !PG;
     const bool spec = (PR || a.rc != nullptr) && a.spec_ok;   // uniform
     const int p = a.pos[m];

@@ -89,6 +89,9 @@ __device__ __forceinline__ uint32_t d8_rms_pair(uint32_t xv, uint32_t wv, float 
 
 // (split-K: two blocks per CU — at most 128 VGPRs; one block per CU ran the down projection
 // at 24.8 instead of 18.5 µs)
+// (The bound's second argument is HIP's minimum waves per SIMD: 4 = 128 VGPRs.  Measured
+// and dropped: the LDS-form QKV at 128 VGPRs, two blocks per CU so that config 4's 288
+// column tiles run in one round — 10.3 vs 8.85 µs, it spills.)
 template <int EPI, int KU, int KS, bool SPL = false, bool T16 = false, bool LF = false>
 __global__ __launch_bounds__(KS * 64, SPL ? 4 : 1) void dec8_kernel(Dec8Params p) {
 #pragma clang fp contract(off)

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Batch-8 decode kernel timings (qie_batch_time_kernel) under environment variants
-(UB8_ENVS: ';'-separated 'K=V,K=V' lists; '-' = none).  One process, interleaved rounds."""
+(UB8_ENVS: ';'-separated 'K=V,K=V' lists; '-' = none).  UB8_DECODE=N: N decode steps first;
+UB8_PAGE=T: paged KV cache of T-token pages.  One process, interleaved rounds."""
 import json
 import os
 import sys
@@ -18,10 +19,14 @@ NAMES = {0: "gate_up", 1: "down", 2: "qkv", 3: "o", 4: "lm_head", 5: "attn"}
 def main():
     spec = S.PRESETS["Qwen2-7B"]
     B, P = int(os.environ.get("UB8_B", "8")), 1024
-    eng = Q.Engine(spec, max_ctx=P + 64, weight_fp8=os.environ.get("UB8_FP8") == "1").init_synthetic(W.SynthParams(seed=0))
-    b = eng.batch(B, P + 64)
+    eng = Q.Engine(spec, max_ctx=P + 64 + int(os.environ.get("UB8_DECODE", "0")), weight_fp8=os.environ.get("UB8_FP8") == "1").init_synthetic(W.SynthParams(seed=0))
+    b = eng.batch(B, P + 64 + int(os.environ.get("UB8_DECODE", "0")), page_tokens=int(os.environ["UB8_PAGE"]) if os.environ.get("UB8_PAGE") else None)
     for sq in range(B):
         b.prefill(sq, np.random.default_rng(sq).integers(0, spec.vocab, P))
+    nd = int(os.environ.get("UB8_DECODE", "0"))   # decode steps before timing (graph + RoPE row state)
+    if nd:
+        b.decode(nd, want_ids=False)
+        eng.sync()
     envs = [e for e in os.environ.get("UB8_ENVS", "-").split(";")]
     res = {}
     for rnd in range(3):

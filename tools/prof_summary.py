@@ -60,6 +60,15 @@ ROLE = {
     "fp8_tile16_kernel": "fp8 16-row tiling of the decode projections (setup)",
     "gemm_big_kernel<1, 128> [g 224 x 512]": "prefill O GEMM (256x128 LDS-DMA, one round of 224 tiles, +residual)",
     "dequantize_fp8_kernel": "fp8 -> bf16 prefill copy (setup)",
+    # round 5: LDS-form fused norm (dec8_kernel<..., LF>), paged KV in the config-4 line
+    "dec8_kernel<2, 8, 7, false, true, true>": "fp8 decode gate/up (+fused RMSNorm, LDS form, SwiGLU), tiled weights  [dominant]",
+    "dec8_kernel<0, 8, 7, false, true, true>": "fp8 decode QKV (+fused RMSNorm, LDS form, bias), tiled weights",
+    "dec8_kernel<0, 8, 7, false, true, false>": "bench live timing of O (store epilogue)",
+    "dec8_kernel<1, 8, 7, false, true, false>": "fp8 decode O-proj (+residual), tiled weights",
+    "dec8_kernel<1, 4, 8, true, true, false>": "fp8 decode down (+residual), split-K 10 x (8 waves x 4 units), tiled",
+    "dec8_kernel<0, 4, 8, true, true, false>": "bench live timing of down (store epilogue)",
+    "attn_decode_mfma2_kernel<128, true, 4, false, 128>": "decode attention, paged KV (fused RoPE/KV append, split-K, in-launch combine)",
+    "attn_prefill_mfma2_kernel<128, true>": "prefill flash attention, paged KV (MFMA, 32 rows/wave)",
 }
 
 

@@ -19,7 +19,7 @@ if on 2; then
   rc=$?; echo "rocprof headline rc=$rc"; [ $rc -eq 0 ] || exit $rc
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_cfg4" -o run \
       -- python3 "$R/bench.py" --steps 64 --warmup 4 --prefill-iters 1 --no-cpu-baseline --no-configs \
-      --batch 8 --fp8 --prompt 1024 --gen 256 > "$R/gpurun_out/prof_cfg4.log" 2>&1
+      --batch 8 --fp8 --prompt 1024 --gen 256 --page-tokens 128 > "$R/gpurun_out/prof_cfg4.log" 2>&1
   rc=$?; echo "rocprof config4 rc=$rc"; [ $rc -eq 0 ] || exit $rc
   cd "$R"
 fi

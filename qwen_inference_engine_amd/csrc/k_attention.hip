@@ -429,16 +429,14 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int cur = 0;
-    for (int kt = 0; kt < nkt; kt++) {
-        // into the other buffer: every wave finished tile kt-1 before the last barrier
-        if (kt + 1 < nkt) issue(kt + 1, cur ^ 1);
-        const uint16_t* K = Ks + cur * KT * HD;
-        const uint16_t* Vt = Vs + cur * KT * HD;
-        // which of the wave's two groups take this key tile (wave-uniform: gpos is
-        // readfirstlane'd); the tile body is instantiated per case, so no MFMA sits behind a
-        // per-instruction exec-mask branch (the compiler could not prove on[] uniform and
-        // wrapped every MFMA in s_and_saveexec / s_cbranch_execz / s_or_b64)
-        auto tile = [&](auto q0c, auto q1c) {
+    // which of the wave's two groups take a key tile is a run of tiles per case (positions
+    // are non-decreasing, and group 1 is the later one): both groups for tiles [0, nkt0),
+    // group 1 alone up to nkt1, then barriers only up to the workgroup's nkt.  One loop per
+    // case with the tile body instantiated for it: no MFMA sits behind a per-instruction
+    // exec-mask branch (the compiler could not prove on[] uniform and wrapped every MFMA in
+    // s_and_saveexec / s_cbranch_execz / s_or_b64), and — unlike a three-way branch inside
+    // one loop — the accumulators need no register copies where the cases meet.
+    auto tile = [&](const int kt, const uint16_t* K, const uint16_t* Vt, auto q0c, auto q1c) {
             constexpr bool ON[QG] = {decltype(q0c)::value, decltype(q1c)::value};
             f32x4_t sacc[QG][4];
 #pragma unroll
@@ -551,14 +549,28 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
                 }
             }
         };
-        const bool on0 = kt * KT <= gpos[0], on1 = kt * KT <= gpos[1];
-        if (on0 && on1) tile(std::true_type{}, std::true_type{});
-        else if (on1) tile(std::false_type{}, std::true_type{});
-        else if (on0) tile(std::true_type{}, std::false_type{});
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs of tile kt+1
-        __syncthreads();                                     // ... and every other wave's
-        cur ^= 1;
+    int kt = 0;
+    auto run = [&](const int kend, auto q0c, auto q1c) {
+        for (; kt < kend; kt++) {
+            // into the other buffer: every wave finished tile kt-1 before the last barrier
+            if (kt + 1 < nkt) issue(kt + 1, cur ^ 1);
+            if constexpr (decltype(q0c)::value || decltype(q1c)::value)
+                tile(kt, Ks + cur * KT * HD, Vs + cur * KT * HD, q0c, q1c);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs of tile kt+1
+            __syncthreads();                                     // ... and every other wave's
+            cur ^= 1;
+        }
+    };
+    // tiles each group takes: kt * KT <= gpos (gpos = -1: none); gpos[1] >= gpos[0]
+    const int nkt0 = gpos[0] >= 0 ? min(nkt, gpos[0] / KT + 1) : 0;
+    const int nkt1 = gpos[1] >= 0 ? min(nkt, gpos[1] / KT + 1) : 0;
+    if (nkt1 > 0) {
+        run(nkt0, std::true_type{}, std::true_type{});
+        run(nkt1, std::false_type{}, std::true_type{});
+    } else {
+        run(nkt0, std::true_type{}, std::false_type{});
     }
+    run(nkt, std::false_type{}, std::false_type{});
 #pragma unroll
     for (int q = 0; q < QG; q++) {
         if (!gact[q]) continue;

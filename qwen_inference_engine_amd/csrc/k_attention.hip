@@ -510,6 +510,8 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
                         for (int r = 0; r < 4; r++) oacc[q][d][r] *= ar[r];
                 }
             }
+            // (Measured and dropped: softmax then P.V per group, so that group 1's softmax
+            // could issue beside group 0's MFMAs, V fragments read per group: 76.8 vs 75.3 µs.)
             const int q4 = fr >> 2, p4 = fr & 3;
 #pragma unroll
             for (int c = 0; c < 2; c++) {

@@ -328,6 +328,17 @@ __device__ __forceinline__ void dma16(const uint16_t* src, uint16_t* lds) {
                                      (__attribute__((address_space(3))) void*)(lds), 16, 0, 0);
 }
 
+// 16 bytes per lane from a buffer resource into LDS (buffer_load_dwordx4 … lds); `lds` is the
+// wave-instruction's 1-KiB base.  (The builtin exists for the device pass only: the host
+// pass, which emits the kernel's launch stub, must not instantiate it.)
+__device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t rs, uint16_t* lds, uint32_t voff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(lds), 16, voff, 0, 0, 0);
+#else
+    (void)rs; (void)lds; (void)voff;
+#endif
+}
+
 // ---------------------------------------------------------------------------
 // Prefill kernel: each wave owns two 16-row query groups, so every K fragment
 // (S^T = K.Q^T) and every V fragment (O += P.V) read from LDS feeds up to two MFMAs.
@@ -399,16 +410,28 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
     // 128); rows past kmax re-read row kmax (same page) and are masked by position.
     constexpr int RPI = 512 / HD;                 // key rows per 1 KiB wave-instruction
     constexpr int IPW = KT / RPI / 4;             // wave-instructions per wave per operand
+    // Buffer loads to LDS on a per-tile resource (round 5): the lane byte offsets inside a
+    // tile are constants of the launch and the tile base is scalar, so a tile's DMAs cost no
+    // VALU (the flat form recomputed 64-bit addresses and the row clamp per tile: ~40 VALU).
+    // The resource covers the tile's rows up to kmax only: rows past it read as zeros (their
+    // keys are masked, and P = 0 times a zero V row stays 0 whatever the cache holds there).
+    uint32_t koff[IPW], voff[IPW];
+#pragma unroll
+    for (int i = 0; i < IPW; i++) {
+        const int r = (wave * IPW + i) * RPI + lane / CPR, pch = lane % CPR;
+        koff[i] = (uint32_t)(r * HD + (pch ^ (r & (CPR - 1))) * 8) * 2;
+        voff[i] = (uint32_t)(r * HD + (pch ^ vswz(r)) * 8) * 2;
+    }
     auto issue = [&](int kt, int buf) {
         const int64_t tb = kv_tok<PG>(a.km, seq, kt * KT, HD);
+        const int rows = min(KT, kmax + 1 - kt * KT);
+        const auto rk = __builtin_amdgcn_make_buffer_rsrc((void*)(kb + tb), (short)0, rows * HD * 2, 0x00020000);
+        const auto rv = __builtin_amdgcn_make_buffer_rsrc((void*)(vb + tb), (short)0, rows * HD * 2, 0x00020000);
 #pragma unroll
         for (int i = 0; i < IPW; i++) {
             const int inst = wave * IPW + i;
-            const int r = inst * RPI + lane / CPR, pch = lane % CPR;
-            const int key = min(kt * KT + r, kmax);
-            const int64_t ro = tb + (int64_t)(key - kt * KT) * HD;
-            dma16(kb + ro + (pch ^ (r & (CPR - 1))) * 8, Ks + buf * KT * HD + inst * 512);
-            dma16(vb + ro + (pch ^ vswz(r)) * 8, Vs + buf * KT * HD + inst * 512);
+            buf_lds16(rk, Ks + buf * KT * HD + inst * 512, koff[i]);
+            buf_lds16(rv, Vs + buf * KT * HD + inst * 512, voff[i]);
         }
     };
 

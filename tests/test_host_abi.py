@@ -37,6 +37,19 @@ def test_library_exports_every_declared_symbol(qlib):
     assert names <= bound, sorted(names - bound)
 
 
+def test_built_libraries_leave_no_kernel_undefined():
+    """Every built libqie (release and the development build, when present) defines all of
+    its own qie:: symbols.  A device-only builtin reached by the host pass can drop a
+    kernel's launch stub without a compile error: the library then links, but fails to load
+    (undefined symbol) on the GPU box."""
+    libs = [_lib.LIB_PATH] + [p for p in [os.path.join(ROOT, "qwen_inference_engine_amd", "lib", "dev", "libqie.so")]
+                              if os.path.exists(p)]
+    for path in libs:
+        out = subprocess.check_output(["nm", "-D", "--undefined-only", path]).decode()
+        undef = [l.split()[-1] for l in out.splitlines() if "_ZN3qie" in l or " qie_" in l]
+        assert not undef, (path, undef[:5])
+
+
 def test_abi_version_and_error_channel(qlib):
     assert qlib.qie_abi_version() == 1
     # invalid call reports through qie_last_error without touching a GPU

@@ -1079,7 +1079,12 @@ static int launch_gemm8sk(int epi, const GemmParams& p, int n_mt, int tiles, hip
 static int g8_splitk(int64_t tiles, int64_t cus, int nk) {
     int best = 1;
     double best_t = 1e30;
-    for (int s = 1; s <= 4 && nk / s >= 64; s++) {
+    // k-tiles per part at least QIE_GEMM8_SK_MINK (dev A/B; default 64: K >= 4,096 per part).
+    // Round 5: split-K 2 for the O projection at P = 2,048 (112 tiles -> 224, K = 3,584) ran
+    // 94-98 vs 84 µs for the 256x128 kernel; QKV at 3 parts 114 vs 89 — the slab round trip
+    // costs more than the idle CUs at this K
+    const int mink = std::max(4, dev_env("QIE_GEMM8_SK_MINK", 64));
+    for (int s = 1; s <= 4 && nk / s >= mink; s++) {
         const double t = (double)((tiles * s + cus - 1) / cus) / s;
         if (t < best_t - 1e-9) {
             best_t = t;

@@ -1443,7 +1443,6 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
     // MI355X: down 23.7 vs 28.0 us, qkv 9.7 vs 10.9, o 6.6 vs 7.7, gate/up 42.9 vs 43.8).
     int rpw = env_int("QIE_GEMV_RPW", 2);
     if (rpw != 2 && rpw != 4) rpw = 2;
-    (void)cus;
     p.n_tasks = (rows + rpw - 1) / rpw;
     // Grid (QIE_GEMV_BLOCKS_PER_CU): default (auto) = one block per CU with ceil(tasks / CUs)
     // waves where 4..9 tasks per CU (Qwen2-7B QKV, O, down), else the occupancy-balanced
@@ -1493,7 +1492,26 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
     }
     // gate/up grid: full residency, grid-stride (-2, launch_gemv_t); QIE_GEMV_SWIGLU_BPC = N > 0
     // caps N blocks per CU, -1 the balanced grid (dev A/B)
-    if (a->epilogue == QIE_EPI_SWIGLU && MT == 1 && bpc < 0) bpc = env_int("QIE_GEMV_SWIGLU_BPC", -2);
+    //
+    // Round 5, grid caps measured per shape (same box, interleaved, in the graph: tools/ab_decode.py;
+    // outputs bit-identical — the grid only changes which wave takes which row task):
+    //  * gate/up, Qwen2-7B (K 3,584, 74 row tasks per CU; 198 VGPRs, 2 resident blocks per CU):
+    //    6 blocks per CU 42.7 -> 41.3 µs, 361.8 -> 366.7 tok/s — a sharp optimum (5: 357.4,
+    //    8: 358.1, 10: 343.2; the full-residency grid, 2 per CU, 361.8);
+    //  * gate/up, Qwen2-0.5B (K 896, 19 tasks per CU; 62 VGPRs): 3 per CU 6.48 -> 5.22 µs,
+    //    1,484 -> 1,542 tok/s (2: 1,543, 4: 1,511, 5: 1,483);
+    //  * lm_head (vocabulary rows, occupancy-balanced grid otherwise): K 896 5 per CU
+    //    53.4 -> 48.8 µs; K 3,584 2 per CU 167.3 -> 164.7 µs.
+    // Shapes outside those ranges keep the former grids (unmeasured there).
+    if (a->epilogue == QIE_EPI_SWIGLU && MT == 1 && bpc < 0) {
+        const int64_t tpc = p.n_tasks / cus;
+        int dflt = -2;
+        if (a->K <= 1024 && tpc <= 32) dflt = 3;
+        else if (a->K >= 3072 && a->K <= 4096 && tpc >= 64 && tpc <= 96) dflt = 6;
+        bpc = env_int("QIE_GEMV_SWIGLU_BPC", dflt);
+    }
+    if (vocab_rows && MT == 1 && bpc < 0)
+        bpc = env_int("QIE_GEMV_LM_BPC", a->K <= 1024 ? 5 : (a->K <= 4096 ? 2 : -1));
     // Batch-1 GEMVs without a fused norm on the one-block-per-CU grid (one row task per
     // wave: Qwen2-7B O, down) read x from L2 beside each weight chunk (XCH = 1) instead of
     // staging it in LDS behind a barrier: Qwen2-7B decode 355 -> 358 tok/s (two A/B rounds),

@@ -85,9 +85,13 @@ int main() {
     int cus = 0;
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     const int L = 28, ctx = 2304, max_ctx = 2560, nkv = 4;
+    // gate/up and lm_head grids: blocks per CU as the engine launches them (round 5: 6 and 2;
+    // GU_BPC / LM_BPC override, e.g. 4 and 4 for the round-4 grids)
+    const int gu_bpc = getenv("GU_BPC") ? atoi(getenv("GU_BPC")) : 6;
+    const int lm_bpc = getenv("LM_BPC") ? atoi(getenv("LM_BPC")) : 2;
     const Gemv qkv{"qkv", 4608, 3584, 2, 7, cus, 576}, o{"o", 3584, 3584, 1, 7, cus, 896},
-        gu{"gate_up", 37888, 3584, 2, 7, 4 * cus, 256}, down{"down", 3584, 18944, 2, 7, cus, 448},
-        head{"lm_head", 152064, 3584, 2, 8, 4 * cus, 256};
+        gu{"gate_up", 37888, 3584, 2, 7, gu_bpc * cus, 256}, down{"down", 3584, 18944, 2, 7, cus, 448},
+        head{"lm_head", 152064, 3584, 2, 8, lm_bpc * cus, 256};
     const Gemv* per_layer[4] = {&qkv, &o, &gu, &down};
     std::vector<u32x4*> wl[4];
     for (int j = 0; j < 4; j++)

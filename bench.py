@@ -39,7 +39,10 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # Measured stream bandwidth of the dominant kernel's own bytes at its own grid on this part
 # (frac also against a measured stream-copy peak): tools/step_floor.hip, 28
 # back-to-back gate/up-sized pure streams (271.6 MB each, grid-stride 4 blocks x 4 waves per
-# CU, 16-B nt loads) in one hipGraph: 42.29 us per launch (profiles/r05_step_floor.txt)
+# CU, 16-B nt loads) in one hipGraph: 42.29 us per launch, the fastest grid measured for the
+# plain stream (6 blocks per CU: 42.97; profiles/r05_step_floor.txt).  The engine's gate/up
+# on its 6-per-CU grid runs ~41.3 us, so frac_vs_stream can exceed 1: the probe is a plain
+# load loop, not a bound on what a kernel of those bytes can reach.
 STREAM_GATE_UP_GBS = 271.633408e6 / 42.29e-6 / 1e9
 STREAM_SRC = "profiles/r05_step_floor.txt (tools/step_floor.hip)"
 METRIC = "decode tokens/s + prefill tok/s, Qwen2-7B bf16 batch=1, 1/2/4/8 MI355X"

@@ -1297,8 +1297,11 @@ static int launch_skinny_x(const GemvParams& p, hipStream_t st) {
         cached_shm = shm;
         cached_nb = nb;
     }
-    const unsigned grid =
-        (unsigned)std::max<int64_t>(1, std::min<int64_t>(n_tiles, (int64_t)device_cu_count() * cached_nb));
+    // dev A/B: blocks per CU (0: all resident — config 4's tiled lm_head 100.1 µs; caps 1 / 2 / 3 / 6
+    // measured 101.9 / 100.5 / 111.0 / 127.7)
+    const int cap = dev_env("QIE_SKINNY_BPC", 0);
+    const unsigned grid = (unsigned)std::max<int64_t>(
+        1, std::min<int64_t>(n_tiles, (int64_t)device_cu_count() * (cap > 0 ? cap : cached_nb)));
     hipLaunchKernelGGL((skinny_mfma_kernel<EPI, WT, XL, NW, UO>), dim3(grid), dim3(NW * 64), shm, st, p);
     QIE_LAUNCH_CHECK();
     return 0;

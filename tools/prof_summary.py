@@ -60,6 +60,9 @@ ROLE = {
     "fp8_tile16_kernel": "fp8 16-row tiling of the decode projections (setup)",
     "gemm_big_kernel<1, 128> [g 224 x 512]": "prefill O GEMM (256x128 LDS-DMA, one round of 224 tiles, +residual)",
     "dequantize_fp8_kernel": "fp8 -> bf16 prefill copy (setup)",
+    # round 5: grids per measured shape (gate/up 6 blocks per CU, lm_head 2)
+    "gemv_kernel<1, 2, 2, 7, 4, 0, 256> [g 1536 x 256]": "decode gate/up GEMV (+RMSNorm in registers, SwiGLU), 6 blocks per CU  [dominant]",
+    "gemv_kernel<1, 2, 0, 8, 3, 0, 256> [g 512 x 256]": "lm_head GEMV (+final RMSNorm per wave, arg-max keys), 2 blocks per CU",
     # round 5: LDS-form fused norm (dec8_kernel<..., LF>), paged KV in the config-4 line
     "dec8_kernel<2, 8, 7, false, true, true>": "fp8 decode gate/up (+fused RMSNorm, LDS form, SwiGLU), tiled weights  [dominant]",
     "dec8_kernel<0, 8, 7, false, true, true>": "fp8 decode QKV (+fused RMSNorm, LDS form, bias), tiled weights",

@@ -1515,6 +1515,15 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
     }
     if (vocab_rows && MT == 1 && bpc < 0)
         bpc = env_int("QIE_GEMV_LM_BPC", a->K <= 1024 ? 5 : (a->K <= 4096 ? 2 : -1));
+    // The normed STORE projection (QKV), Qwen2-7B (K 3,584, 9 row tasks per CU): 2 blocks of 4
+    // waves per CU instead of one 9-wave block, 9.77 -> 9.26 µs, 367.4 -> 369.4 tok/s (1: 357.2,
+    // 3: 364.8, 4: 364.8).  The fused norm's sum of squares is then reduced over 256 threads
+    // instead of 576 (another fp32 order of the same sum; the parity tests bound it).
+    // Qwen2-0.5B's QKV: equal at 1-3 per CU, kept.
+    if (!vocab_rows && MT == 1 && p.norm_w && a->epilogue == QIE_EPI_STORE && bpc < 0) {
+        const int64_t tpc = p.n_tasks / cus;
+        bpc = env_int("QIE_GEMV_QKV_BPC", a->K >= 3072 && a->K <= 4096 && tpc >= 6 && tpc <= 12 ? 2 : -1);
+    }
     // Batch-1 GEMVs without a fused norm on the one-block-per-CU grid (one row task per
     // wave: Qwen2-7B O, down) read x from L2 beside each weight chunk (XCH = 1) instead of
     // staging it in LDS behind a barrier: Qwen2-7B decode 355 -> 358 tok/s (two A/B rounds),

@@ -1520,6 +1520,10 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
     // 3: 364.8, 4: 364.8).  The fused norm's sum of squares is then reduced over 256 threads
     // instead of 576 (another fp32 order of the same sum; the parity tests bound it).
     // Qwen2-0.5B's QKV: equal at 1-3 per CU, kept.
+    // (dev A/B) residual projections (O, down): caps 3 / 5 / 6 / 8 per CU all ran Qwen2-7B at
+    // 363.4-363.5 vs 369.6 tok/s on their one-block-per-CU layout; 0.5B equal
+
+    if (MT == 1 && a->epilogue == QIE_EPI_RESIDUAL && bpc < 0) bpc = env_int("QIE_GEMV_RES_BPC", -1);
     if (!vocab_rows && MT == 1 && p.norm_w && a->epilogue == QIE_EPI_STORE && bpc < 0) {
         const int64_t tpc = p.n_tasks / cus;
         bpc = env_int("QIE_GEMV_QKV_BPC", a->K >= 3072 && a->K <= 4096 && tpc >= 6 && tpc <= 12 ? 2 : -1);

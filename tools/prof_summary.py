@@ -63,6 +63,7 @@ ROLE = {
     # round 5: grids per measured shape (gate/up 6 blocks per CU, lm_head 2)
     "gemv_kernel<1, 2, 2, 7, 4, 0, 256> [g 1536 x 256]": "decode gate/up GEMV (+RMSNorm in registers, SwiGLU), 6 blocks per CU  [dominant]",
     "gemv_kernel<1, 2, 0, 8, 3, 0, 256> [g 512 x 256]": "lm_head GEMV (+final RMSNorm per wave, arg-max keys), 2 blocks per CU",
+    "gemv_kernel<1, 2, 0, 7, 2, 0, 256> [g 512 x 256]": "decode QKV GEMV (+RMSNorm, bias), 2 four-wave blocks per CU",
     # round 5: LDS-form fused norm (dec8_kernel<..., LF>), paged KV in the config-4 line
     "dec8_kernel<2, 8, 7, false, true, true>": "fp8 decode gate/up (+fused RMSNorm, LDS form, SwiGLU), tiled weights  [dominant]",
     "dec8_kernel<0, 8, 7, false, true, true>": "fp8 decode QKV (+fused RMSNorm, LDS form, bias), tiled weights",

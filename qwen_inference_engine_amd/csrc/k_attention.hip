@@ -1202,7 +1202,11 @@ static int fill_dec_params(DecodeAttnParams& a, const void* qkv, int64_t B, cons
     a.nq = n_heads;
     a.max_ctx = cache->max_ctx;
     const int senv = std::min(dev_env("QIE_DEC_SPLITS", 0), kDecMaxSplits);
-    a.splits_target = senv > 0 ? senv : kDecMSplits;
+    // split target: 32 (one-step splits up to 4k keys); at B >= 8, 8 — config 4 (B = 8, ctx
+    // 1,025-1,280) then runs two-step splits, half as many split blocks and combine inputs
+    // per row: 3,610 -> 3,637-3,645 tok/s same-box (at B = 1 the headline wants the CUs:
+    // targets 16 / 8 ran 349 / 340 vs 361 tok/s)
+    a.splits_target = senv > 0 ? senv : (B >= 8 ? 8 : kDecMSplits);
     a.dbg = dev_env("QIE_DEC_DBG", 0);
     a.sc1 = dev_env("QIE_DEC_SC1", 1);   // 9.79 -> 9.56 us per launch (ctx 2.3k, Qwen2-7B)
     // keys per block step (the launch picks the kernel instantiation with the same KS): 128.

@@ -758,8 +758,8 @@ int or_sample_ref(const bf16_t* logits, int64_t V, int k, float temperature, flo
  * attention residual, 2l + 2 after its MLP residual (the engine's qie_batch_debug_step). */
 /* fp8 activations (the engine's opts.prefill_fp8, QIE_LINEAR_ACT_FP8 in qie_ops.h): when set,
  * or_forward replaces the input rows of each layer projection (QKV, O, gate/up, down) by their
- * per-row e4m3 quantisation — s = the smallest power of two with max|x| / s <= 448 (1 for a
- * zero row), x -> e4m3_rne(x / s) * s — before the (unchanged) matmul.  The rounding is
+ * per-row e4m3 quantisation — s = the smallest power of two with max|x| / s <= 448, at least
+ * 2^-126 (1 for a zero row), x -> e4m3_rne(x / s) * s — before the (unchanged) matmul.  The rounding is
  * restated from the OCP e4m3fn value set itself (nearest representable value, ties to the
  * even code), independently of the engine's encoder.  Every dequantised value is a bf16. */
 void or_set_act_fp8(int v) { g_act_fp8 = v; }
@@ -800,6 +800,7 @@ void or_quant_rows_fp8(bf16_t* x, int64_t rows, int64_t cols, int32_t* exps) {
             e = E - 9;
             while (std::ldexp(448.0, e) < (double)amax) e++;
             while (std::ldexp(448.0, e - 1) >= (double)amax) e--;
+            if (e < -126) e = -126;   // the scale stays a normal float (an e8m0 exponent >= 1)
         }
         if (exps) exps[r] = e;
         for (int64_t c = 0; c < cols; c++) {

@@ -380,6 +380,7 @@ struct PeerComm : qie_comm {
         return 0;
     }
     bool graph_capturable() const override { return true; }
+    const unsigned* error_word() const override { return ctl + 2; }
     int error_state(void* stream) const override {   // stream-ordered (never the null stream)
         unsigned v = 0;
         if (hipMemcpyAsync(&v, ctl + 2, sizeof(v), hipMemcpyDeviceToHost, (hipStream_t)stream) != hipSuccess ||

@@ -665,10 +665,10 @@ static int enqueue_decode(qie_batch* b, const qie_sampling* smp) {
 
 // opts.prefill_fp8 (numerics flag): the prefill projections on the block-scaled fp8 MFMA
 // GEMM (QIE_LINEAR_ACT_FP8) — fp8 weights in the engine's arena, every projection input
-// quantised per row (qie_quantize_rows_fp8), K of each a multiple of 128
+// quantised per row (qie_quantize_rows_fp8), K of each a multiple of 128 — qie_engine_create
+// refuses the flag where that does not hold, so it is never dropped silently here
 static bool prefill_mx(const qie_engine* e) {
-    const int64_t H = e->spec.hidden, QD = (int64_t)e->sh.nq * e->spec.head_dim, I = e->sh.ffn;
-    return e->fp8 && e->opts.prefill_fp8 && H % 128 == 0 && QD % 128 == 0 && I % 128 == 0;
+    return e->fp8 && e->opts.prefill_fp8;
 }
 
 static int ensure_prefill_scratch(qie_batch* b, int64_t n) {
@@ -720,11 +720,23 @@ static int ensure_prefill_scratch(qie_batch* b, int64_t n) {
     return 0;
 }
 
+// The ids and (tensor parallel, peer backend) the exchange error word come back in ONE
+// stream-ordered batch with one synchronisation — not a second blocking round trip per token
+// (ADVICE r05); a backend without the word keeps comm_check's own read.
 static int sync_ids(qie_batch* b, int32_t* next_ids) {
     if (!next_ids) return 0;
-    QIE_HIP(hipMemcpyAsync(next_ids, b->d_ids, b->B * 4, hipMemcpyDeviceToHost, b->e->stream));
-    QIE_HIP(hipStreamSynchronize(b->e->stream));
-    return comm_check(b->e, "decode");
+    qie_engine* e = b->e;
+    QIE_HIP(hipMemcpyAsync(next_ids, b->d_ids, b->B * 4, hipMemcpyDeviceToHost, e->stream));
+    const unsigned* ew = use_comm(e) ? e->comm->error_word() : nullptr;
+    unsigned err = 0;
+    if (ew) QIE_HIP(hipMemcpyAsync(&err, ew, sizeof(err), hipMemcpyDeviceToHost, e->stream));
+    QIE_HIP(hipStreamSynchronize(e->stream));
+    if (ew) {
+        if (err) return fail(-7, "decode: tensor-parallel exchange failed on the device (error word %u: a peer rank "
+                                 "did not arrive within the bounded wait); the communicator is unusable", err);
+        return 0;
+    }
+    return comm_check(e, "decode");
 }
 
 }  // namespace qie
@@ -747,6 +759,18 @@ int qie_engine_create(const qie_model_spec* spec, const qie_engine_opts* opts, q
                 "qie_engine_create: tensor parallel %d needs n_kv_heads divisible by it (or dividing it, with at "
                 "most n_heads / n_kv_heads ranks per kv head), vocab divisible by it and ffn / tp a multiple of 8 "
                 "(use replicas for this model at this size)", tp);
+    // prefill_fp8 is a numerics choice (every projection input quantised to e4m3): refuse it
+    // where the engine could not honour it, instead of silently running bf16 activations
+    // against a caller (and an oracle) that expects the fp8-activation model
+    if (opts && opts->prefill_fp8) {
+        const int64_t qd = (int64_t)probe.nq * s.head_dim, ffl = s.ffn / tp;
+        QIE_REQUIRE(opts->weight_fp8, "qie_engine_create: prefill_fp8 needs weight_fp8 (fp8 weights are the "
+                                      "block-scaled MFMA's second operand)");
+        QIE_REQUIRE(s.hidden % 128 == 0 && qd % 128 == 0 && ffl % 128 == 0,
+                    "qie_engine_create: prefill_fp8 needs hidden (%lld), this rank's q width (%lld) and ffn / tp "
+                    "(%lld) to be multiples of 128 (the fp8 MFMA's k block)",
+                    (long long)s.hidden, (long long)qd, (long long)ffl);
+    }
     qie_engine* e = new qie_engine();
     e->spec = s;
     if (opts) e->opts = *opts;

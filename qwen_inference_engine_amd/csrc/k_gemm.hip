@@ -1485,6 +1485,11 @@ static int gemm_mx(const qie_linear_args* a, hipStream_t st) {
     QIE_REQUIRE(a->K % mx::BK == 0 && a->ldx >= a->K && a->ldx % 16 == 0,
                 "qie_linear: ACT_FP8 needs K %% 128 == 0 and ldx (bytes) %% 16 == 0");
     QIE_REQUIRE(a->norm_w == nullptr && a->argmax_keys == nullptr, "qie_linear: ACT_FP8 takes no fused norm / arg-max");
+    // the kernel keeps A row offsets (row * lda + column) in 32 bits: refuse what would wrap
+    // (e.g. 8 x 32k rows of the down projection's K = 18,944) instead of reading wrong rows
+    QIE_REQUIRE(((int64_t)cdiv(a->M, 256) * 256) * a->ldx < ((int64_t)1 << 32),
+                "qie_linear: ACT_FP8 with M (%lld) x ldx (%lld) >= 2^32 bytes of codes (split the rows)",
+                (long long)a->M, (long long)a->ldx);
     if (t16)
         QIE_REQUIRE(a->epilogue == QIE_EPI_SWIGLU ? a->N % 16 == 0
                                                   : a->seg_rows[0] % 16 == 0 && a->seg_rows[1] % 16 == 0 &&

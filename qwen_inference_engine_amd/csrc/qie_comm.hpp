@@ -29,4 +29,7 @@ struct qie_comm {
     // non-zero once an exchange failed on the device (the peer backend's bounded wait timed
     // out); read after the stream synchronised — a blocking copy of one word
     virtual int error_state(void* stream) const { (void)stream; return 0; }
+    // device word error_state reads (nullptr: the backend has none), so a caller that already
+    // copies results back can read it in the same stream-ordered batch, one synchronisation
+    virtual const unsigned* error_word() const { return nullptr; }
 };

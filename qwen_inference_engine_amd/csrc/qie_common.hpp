@@ -119,7 +119,10 @@ __host__ __device__ inline float e4m3_row_scale(float amax) {
     float s = ldexpf(1.f, e);                             // s >= amax / 448
     if (ldexpf(1.f, e - 1) * 448.f >= amax) s = ldexpf(1.f, e - 1);
     if (s * 448.f < amax) s *= 2.f;                       // exact checks: the division rounded
-    return s;
+    // never below the smallest normal: the scale's exponent field is the MFMA's e8m0 operand
+    // (read from the float bits), and a subnormal s would read as exponent 0
+    const float smin = ldexpf(1.f, -126);
+    return s < smin ? smin : s;
 }
 // 4 packed codes -> 4 floats (v_cvt_pk_f32_fp8; gfx950 "fp8" is OCP e4m3fn — checked
 // against e4m3_decode for all 256 codes by tests/test_gpu_fp8.py)

@@ -154,13 +154,15 @@ class OrderSet:
 def forced_decisions(oracle, hw, batch, prompt, n, seed=77, nthreads=0, progress=False, act_fp8=False):
     """Runs the protocol above on slot 0 of `batch` (an engine over the same weights as
     `hw`).  Returns the report dict; report["ok"] applies the rule:
-      * every step's engine logits within max(1e-3, 2 x the run's max order-0 vs order-2 /
-        order-7 norm-relative spread) of order 0;
+      * every step's engine logits within max(1e-3, 2 x the run's max order-0 vs order-2
+        norm-relative spread) of order 0;
       * no hard mismatch: an engine id that differs from order 0 must be a near-tie whose
         order-0 top-2 gap is within max(2 bf16 ulps of max|logit|, the run's max absolute
-        order-1 / order-2 / order-7 logit spread);
+        order-1 / order-2 logit spread);
     Order 7 is the reference's recorded nvcc -use_fast_math build (contracted fma, fast
-    division and exponent; or_set_sum_order): the engine's distance to it is reported too.
+    division and exponent; or_set_sum_order): the engine's distance to it and order 7's own
+    spread are reported as information only — the engine is not a fast-math build, so order 7
+    does not widen the bar.
       * near-tie flips <= max_flips(n)."""
     V = hw.spec.vocab
     P = len(prompt)
@@ -175,7 +177,8 @@ def forced_decisions(oracle, hw, batch, prompt, n, seed=77, nthreads=0, progress
         steps.append(dict(ids=[oracle.argmax(x) for x in lg], gpu=int(t_e), rel=norm_rel(ge, lg[0]),
                           rel01=norm_rel(lg[1], lg[0]), rel02=norm_rel(lg[2], lg[0]),
                           rel07=norm_rel(lg[3], lg[0]), rel_gpu7=norm_rel(ge, lg[3]),
-                          abs_spread=float(max(np.abs(f[k] - f[0]).max() for k in (1, 2, 3))),
+                          abs_spread=float(max(np.abs(f[k] - f[0]).max() for k in (1, 2))),
+                          abs_spread7=float(np.abs(f[3] - f[0]).max()),
                           lg0=lg[0], ulps=2 * 2.0 ** -7 * float(np.abs(f[0]).max())))
         if progress and (i % 16 == 0 or i + 1 == n):
             print(f"  forced decision {i + 1}/{n}: rel {steps[-1]['rel']:.2e}", flush=True)
@@ -186,7 +189,9 @@ def forced_decisions(oracle, hw, batch, prompt, n, seed=77, nthreads=0, progress
     rel01 = max(s["rel01"] for s in steps)
     rel07 = max(s["rel07"] for s in steps)
     abs_spread = max(s["abs_spread"] for s in steps)
-    bar = max(NORM_REL, SPREAD_FACTOR * max(rel02, rel07))
+    # the gate: orders 1 and 2 only (the engine is not a fast-math build); order 7's spread is
+    # reported beside it, never folded into the bar
+    bar = max(NORM_REL, SPREAD_FACTOR * rel02)
     flips = hard = agreed_flips = 0
     flip_gaps = []
     for s in steps:
@@ -216,6 +221,9 @@ def forced_decisions(oracle, hw, batch, prompt, n, seed=77, nthreads=0, progress
         "oracle_o1_spread": round(rel01, 6), "oracle_o2_spread": round(rel02, 6),
         "oracle_o7_spread": round(rel07, 6), "bar": round(bar, 6),
         "max_abs_spread": round(abs_spread, 5), "gpu_flip_top2_gaps": flip_gaps,
+        "oracle_o7_max_abs_spread": round(max(s["abs_spread7"] for s in steps), 5),
+        "bar_rule": "max(1e-3, 2 x max order-2 vs order-0 norm-rel spread); near-tie gap <= max(2 bf16 ulps, "
+                    "max |order-1 or order-2 - order-0| logit); order 7 reported, not gating",
         "median_top2_gap": round(float(np.median([abs(np.diff(np.sort(G.bf(s["lg0"]).astype(np.float64))[-2:]))[0]
                                                   for s in steps])), 5),
     }

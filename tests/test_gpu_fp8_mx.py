@@ -75,11 +75,15 @@ def test_quantize_rows_fp8_matches_oracle(oracle, qlib, M, K):
     xf = oracle.bf16_to_f32(x) * np.logspace(-20, 20, M, base=2.0).astype(np.float32)[:, None]
     x = oracle.f32_to_bf16(xf.astype(np.float32))
     x[M // 2] = 0                       # an all-zero row: scale 1, zero codes
+    # a tiny-amax row: its scale would be a subnormal float below 2^-126 (exponent field 0);
+    # clamped to 2^-126 on both sides
+    x[1] = oracle.f32_to_bf16((oracle.bf16_to_f32(rand_bf16(oracle, (K,), seed=3)) * 2.0 ** -121).astype(np.float32))
     q, e = _quant_dev(qlib, x)
     codes = G.host(q).reshape(M, K)
     ex = G.host(e)[:M].astype(np.int64) - 127
     dq_or, e_or = oracle.quant_rows_fp8(x)
     assert np.array_equal(ex, e_or)
+    assert ex.min() >= -126 and e_or[1] == -126
     got = W.e4m3_table()[codes].astype(np.float64) * np.exp2(ex.astype(np.float64))[:, None]
     assert np.array_equal(got, oracle.bf16_to_f32(dq_or).astype(np.float64))
 

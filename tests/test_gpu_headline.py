@@ -200,3 +200,68 @@ def test_fp8_tiled_batch1_short_prompt(oracle):
         if step + 1 < n_new:
             t = b.decode_step()[0]
     assert flips <= max_flips(n_new)
+
+
+# ---------------------------------------------------------------------------------------
+# The exact config-4 path bench.py's configs.config4 times (verdict r05 item 1): fp8 weights,
+# PAGED KV with 128-token pages, B = 8, 1,024-token prompts through qie_prefill_batch, graph
+# decode at ctx 1,025.. — the B >= 8 split rule (splits target 8: two-step 256-key splits
+# from ctx 1,025 on, k_attention.hip qie_attention_decode) on the paged kernel instance.
+C4_SPEC = S.QWEN2_7B.replace(n_layers=2)
+C4_B, C4_P, C4_STEPS = 8, 1024, 16
+C4_MAXC = C4_P + 256 + 16   # bench.py config 4's max_ctx (P + G + 16)
+
+
+def _c4_prompts():
+    return [[int(t) for t in rng(400 + i).integers(0, C4_SPEC.vocab, C4_P)] for i in range(C4_B)]
+
+
+def test_config4_paged_equals_contiguous_batch8():
+    """Paged (128-token pages) == contiguous, bit for bit, at B = 8 over the page boundary
+    at 1,024: the same batched prefill, then 16 free-running greedy graph steps (ctx 1,025 ..
+    1,040); ids and every step's logits identical."""
+    eng = Q.Engine(C4_SPEC, max_ctx=C4_MAXC, weight_fp8=True).init_synthetic(W.SynthParams(seed=0))
+    prompts = _c4_prompts()
+    runs = []
+    for pt in (None, 128):
+        b = eng.batch(C4_B, C4_MAXC, page_tokens=pt)
+        ids = [b.prefill_batch(0, prompts)]
+        lgs = [b.logits()]
+        for _ in range(C4_STEPS):
+            ids.append(list(b.decode_step()))
+            lgs.append(b.logits())
+        assert b.positions().tolist() == [C4_P + C4_STEPS] * C4_B
+        runs.append((ids, np.stack(lgs)))
+        b.close()
+    assert runs[0][0] == runs[1][0]
+    assert np.array_equal(runs[0][1], runs[1][1])
+
+
+def test_config4_paged128_fp8_batch8_prompt1024_matches_oracle(oracle):
+    """The bench's config-4 path against the oracle on the dequantised weights
+    (tests/parity.py check_step, bar from the order-0 vs order-2 spread of sequence 0 on the
+    same model): 8 prompts of 1,024 tokens in one batched prefill, then 16 teacher-forced
+    graph decode steps per sequence (ctx 1,025 .. 1,040)."""
+    syn = W.SynthParams(seed=0)
+    eng = Q.Engine(C4_SPEC, max_ctx=C4_MAXC, weight_fp8=True).init_synthetic(syn)
+    b = eng.batch(C4_B, C4_MAXC, page_tokens=128)
+    hw = W.HostWeights.synthetic(C4_SPEC, syn).fp8_dequantized()
+    prompts = _c4_prompts()
+    oms = [OrderPair(oracle, hw, C4_MAXC, with_spread=(i == 0)) for i in range(C4_B)]
+    traces = [oracle_trace(oracle, om, pr, C4_STEPS) for om, pr in zip(oms, prompts)]
+    bar_pair = oms[0]
+    t_e = b.prefill_batch(0, prompts)
+    flips = 0
+    for step in range(C4_STEPS):
+        lg_e = b.logits()
+        for i in range(C4_B):
+            ids, outs = traces[i]
+            lg0 = outs[step][0]
+            flips += check_step(lg_e[i], lg0, None, t_e[i], ids[step], f"paged c4 seq {i} step {step}",
+                                bar_pair.bars(lg0))
+            if t_e[i] != ids[step]:
+                b.set_position(i, C4_P + step, ids[step])
+        if step + 1 < C4_STEPS:
+            t_e = b.decode_step()
+    assert flips <= max_flips(C4_B * C4_STEPS)
+    assert b.page_stats()[2] == 128

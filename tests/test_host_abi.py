@@ -185,3 +185,22 @@ def test_batcher_groups_equal_length_admissions():
     rs = [Request(i, [0] * 8, 1, slot=s) for i, s in enumerate([0, 2, 3])]
     assert [[r.slot for r in run] for run in prefill_runs(rs)] == [[0], [2, 3]]
     assert prefill_runs([]) == []
+
+
+@pytest.mark.parametrize("fp8,tiny_widths", [(False, False), (True, True)])
+def test_prefill_fp8_refused_where_it_cannot_hold(qlib, fp8, tiny_widths):
+    """qie_engine_create refuses prefill_fp8 without fp8 weights, or when a projection width
+    (hidden, this rank's q width, ffn / tp) is not a multiple of the fp8 MFMA's 128-k block,
+    instead of silently running the bf16-activation model.  The check precedes
+    every HIP call, so it runs without a GPU."""
+    spec = S.tiny(n_layers=1, hidden=192, ffn=320) if tiny_widths else S.QWEN2_7B
+    if tiny_widths:
+        assert spec.hidden % 128 or spec.ffn % 128 or (spec.n_heads * spec.head_dim) % 128
+    sc = spec.to_c()
+    opts = _lib.EngineOptsC()
+    opts.max_ctx, opts.use_graph, opts.tp_size = 64, 0, 1
+    opts.weight_fp8, opts.prefill_fp8 = int(fp8), 1
+    h = C.c_void_p()
+    rc = qlib.qie_engine_create(C.byref(sc), C.byref(opts), C.byref(h))
+    assert rc == -22 and not h.value
+    assert b"prefill_fp8" in qlib.qie_last_error()

@@ -6,8 +6,10 @@
 // within ~1e-4 of sum|p| of the exact sum, NOT fp32-exact: the instruction's internal sum
 // of its 128 products loses bits (case 0-4: 8e-5..1.5e-4) — the accumulation bar of the
 // fp8-activation tests (tests/test_gpu_fp8_mx.py MX_ACC_REL) and oracle order 8's model.
-// Case 5 (A scales varying per 32-k block within a row) does not follow this lane map;
-// the engine passes one scale per row, so the per-block map is left unpinned.
+// Case 5 (A scales varying per 32-k block within a row) did not follow the per-block lane map
+// (r05: 1.17 x sum|p|); r06 prints the error under both candidate maps and names the one the
+// hardware follows.  The engine passes one scale per row (every lane of a row the same byte),
+// which both maps read identically.
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <cstdio>
@@ -79,23 +81,31 @@ int main() {
         hipMemcpy(dsb, hsb, 64, hipMemcpyHostToDevice);
         hipLaunchKernelGGL(probe, dim3(1), dim3(64), 0, 0, dA, dB, dsa, dsb, dC, 0);
         hipMemcpy(hC, dC, sizeof(hC), hipMemcpyDeviceToHost);
-        double maxerr = 0, maxabs = 0;
-        for (int i = 0; i < 16; i++)
-            for (int j = 0; j < 16; j++) {
-                double s = 0, sabs = 0;
-                for (int k = 0; k < 128; k++) {
-                    const int blk = k / 32;
-                    const double sA = std::ldexp(1.0, hsa[i + 16 * blk] - 127), sB = std::ldexp(1.0, hsb[j + 16 * blk] - 127);
-                    const double p = (double)e4m3(hA[i * 128 + k]) * sA * (double)e4m3(hB[j * 128 + k]) * sB;
-                    s += p;
-                    sabs += std::fabs(p);
+        // scale lane maps: 0 = lane (row + 16 * k-block) scales that row's 32-k block (the
+        // per-block reading); 1 = lane `row` (lanes 0..15) scales the row's whole 128-k span
+        // (one scale per row, the engine's use: every lane of a row passes the same byte)
+        double maxerr[2] = {0, 0};
+        for (int map = 0; map < 2; map++)
+            for (int i = 0; i < 16; i++)
+                for (int j = 0; j < 16; j++) {
+                    double s = 0, sabs = 0;
+                    for (int k = 0; k < 128; k++) {
+                        const int blk = map == 0 ? k / 32 : 0;
+                        const double sA = std::ldexp(1.0, hsa[i + 16 * blk] - 127),
+                                     sB = std::ldexp(1.0, hsb[j + 16 * blk] - 127);
+                        const double p = (double)e4m3(hA[i * 128 + k]) * sA * (double)e4m3(hB[j * 128 + k]) * sB;
+                        s += p;
+                        sabs += std::fabs(p);
+                    }
+                    maxerr[map] = std::fmax(maxerr[map], std::fabs(hC[i * 16 + j] - s) / (sabs + 1e-30));
                 }
-                maxerr = std::fmax(maxerr, std::fabs(hC[i * 16 + j] - s) / (sabs + 1e-30));
-                maxabs = std::fmax(maxabs, sabs);
-            }
-        std::printf("case %d: max |err| / sum|p| = %.3e%s\n", t, maxerr,
-                    t == 5 ? "  (per-k-block A scales: informational, the engine's scales are per row)" : "");
-        if (t != 5 && maxerr > 2e-4) fails++;   // the instruction's own accumulation: ~1e-4 of sum|p|
+        std::printf("case %d: max |err| / sum|p| = %.3e (per-32-k-block lane map) / %.3e (lane = row, one scale per "
+                    "128 k)%s\n", t, maxerr[0], maxerr[1],
+                    t == 5 ? "  <- per-k-block A scales: which map the hardware follows" : "");
+        if (t != 5 && maxerr[0] > 2e-4) fails++;   // the instruction's own accumulation: ~1e-4 of sum|p|
+        if (t == 5) std::printf("case 5 lane map: %s\n", maxerr[0] <= 2e-4 ? "per-32-k-block (lane = row + 16 blk)"
+                                                 : (maxerr[1] <= 2e-4 ? "lane = row, one scale per 128 k (lanes 16..63 ignored)"
+                                                                      : "neither modelled map"));
     }
     std::printf("%s\n", fails ? "FAIL" : "OK");
     return fails ? 1 : 0;

@@ -176,6 +176,15 @@ int qie_batch_history(qie_batch* b, int32_t seq, int32_t* host_ids, int32_t n);
 /* Rewind/set sequence `seq` to position pos with current token `token`
  * (KV rows >= pos are simply overwritten later). */
 int qie_batch_set_position(qie_batch* b, int32_t seq, int32_t pos, int32_t token);
+/* Decode structure of the batch's steps: 0 = five launches per layer (the reference path:
+ * QKV GEMV, attention, O GEMV, gate/up GEMV, down GEMV, hipGraph-captured); 1 = the whole
+ * layer stack as ONE persistent launch (one workgroup per CU, weight streams running ahead of
+ * the layer's dependency edges, tagged hand-offs between CUs; bit-identical outputs).  Mode 1
+ * covers batch 1, bf16 weights, one device, head_dim 128 and a contiguous KV cache; other
+ * batches return an error (QIE_EINVAL) naming what is not covered.  The next step re-captures
+ * the decode graph.  qie_batch_decode_mode returns the current mode. */
+int qie_batch_set_decode_mode(qie_batch* b, int32_t mode);
+int qie_batch_decode_mode(const qie_batch* b);
 /* Batch geometry: B slots, max_ctx positions per slot. */
 int qie_batch_dims(const qie_batch* b, int32_t* batch, int32_t* max_ctx);
 /* KV descriptor of slot `seq` for the operator tier (qie_kv_write, qie_attention with
@@ -194,7 +203,8 @@ int qie_engine_rope_tables(const qie_engine* e, const float** rope_cos, const fl
 /* Time `iters` launches of one of the decode step's kernels with hipEvents on
  * the engine stream (which: 0 = gate/up GEMV, 1 = down GEMV, 2 = QKV GEMV,
  * 3 = O GEMV, 4 = lm_head GEMV, 5 = attention; the layer GEMVs cycle through
- * layers 1..L-1 so no weight stays cache-resident).  Returns the average
+ * layers 1..L-1 so no weight stays cache-resident; 6 = the persistent layer stack of decode
+ * mode 1, all layers per launch, the sequence state restored afterwards).  Returns the average
  * microseconds per launch and the algorithmic bytes per launch. */
 int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* avg_us,
                           double* bytes);

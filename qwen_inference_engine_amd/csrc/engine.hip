@@ -31,6 +31,15 @@ int gemv_rope(const qie_linear_args* a, const int32_t* pos, const float* cs, con
 int gemm(const qie_linear_args* a, hipStream_t st);
 bool dec8_applies(const qie_linear_args* a);
 int dec8_reserve(hipStream_t st);
+bool persist_supported(const qie_model_spec& s, int B, int tp, bool fp8, bool paged, int ncu, const char** why);
+size_t persist_attn_table_bytes(int n_layers);
+int persist_attn_table(const qie_model_spec& s, const qie_layer_weights* h_layers, const void* qkv_scratch,
+                       const int32_t* pos, const float* rope_cos, const float* rope_sin, const qie_kv_cache* cache,
+                       void* dec_ws, void* d_attp, hipStream_t st);
+int persist_decode_launch(const qie_model_spec& s, const qie_layer_weights* d_layers, const void* d_attp,
+                          uint16_t* x_res, unsigned long long* granules, const unsigned* epoch, unsigned* err,
+                          const int32_t* pos, int splits_target, hipStream_t st);
+int64_t persist_granule_count(const qie_model_spec& s);
 }  // namespace qie
 
 
@@ -148,6 +157,13 @@ struct qie_batch {
     // qie_batch_debug_step: while set, the decode enqueue copies the residual stream after every
     // attention block and every MLP block into dbg_x ([2L + 1][B][H] bf16; slot 0 = the input)
     uint16_t* dbg_x = nullptr;
+    // decode structure (qie_batch_set_decode_mode): 0 = five launches per layer, 1 = the whole
+    // layer stack as one persistent launch (k_persist.hip).  pk_mem: hand-off granules, then the
+    // step epoch and the error word (zeroed once; the finalize kernel advances the epoch)
+    int decode_mode = 0;
+    void* pk_mem = nullptr;
+    qie_layer_weights* d_layers = nullptr;
+    void* d_attp = nullptr;      // the attention role's parameters per layer (persist_attn_table)
 };
 
 namespace qie {
@@ -180,8 +196,11 @@ __device__ __forceinline__ void write_rope_cur(const RopeCurArgs& r, int m, int 
 __global__ __launch_bounds__(256) void finalize_kernel(int m0, unsigned long long* keys, const int32_t* ids_in,
                                                        int32_t* ids_out, int32_t* pos, int32_t* step,
                                                        int32_t* hist, int hist_stride, const uint4* E,
-                                                       uint4* x_res, int64_t H8, int32_t vocab, RopeCurArgs rca) {
+                                                       uint4* x_res, int64_t H8, int32_t vocab, RopeCurArgs rca,
+                                                       unsigned* pk_epoch) {
     const int m = m0 + blockIdx.x;
+    // the persistent step's hand-off epoch advances once per step (k_persist.hip tags)
+    if (pk_epoch && blockIdx.x == 0 && threadIdx.x == 0) *pk_epoch += 1u;
     int32_t tok = keys ? key_idx(keys[m]) : ids_in[m];
     const int32_t p = pos[m];
     __syncthreads();
@@ -620,6 +639,11 @@ static int gather_logits(qie_batch* b, int m0, int M) {
     return 0;
 }
 
+// the persistent step's words behind its granules: [0] step epoch, [1] error word
+static unsigned* pk_epoch_ptr(const qie_batch* b) {
+    return (unsigned*)((unsigned long long*)b->pk_mem + persist_granule_count(b->e->spec));
+}
+
 // lm_head over rows [m0, m0+M) of x (already the residual stream), then the
 // sampler; leaves ids in d_keys (greedy) or d_ids.
 static int enqueue_head(qie_batch* b, const uint16_t* x, int64_t ldx, int m0, int M, const qie_sampling* smp) {
@@ -653,13 +677,27 @@ static int enqueue_head(qie_batch* b, const uint16_t* x, int64_t ldx, int m0, in
     }
     hipLaunchKernelGGL(finalize_kernel, dim3(M), dim3(256), 0, st, m0, greedy ? b->d_keys : nullptr,
                        b->d_ids, b->d_ids, b->d_pos, b->d_step, b->d_hist, b->max_ctx,
-                       (const uint4*)e->w.embed, (uint4*)b->x_res, (int64_t)s.hidden / 8, s.vocab, rope_cur_args(b));
+                       (const uint4*)e->w.embed, (uint4*)b->x_res, (int64_t)s.hidden / 8, s.vocab, rope_cur_args(b),
+                       b->pk_mem ? pk_epoch_ptr(b) : nullptr);
     QIE_LAUNCH_CHECK();
     return 0;
 }
 
+static bool pk_on(const qie_batch* b) { return b->decode_mode == 1 && b->pk_mem && !b->dbg_x; }
+
+// the split target of the batch-1 decode attention (qie_attention_decode's rule at B = 1)
+static int pk_splits_target(const qie_batch* b) { (void)b; return 32; }
+
+static int enqueue_layers_persistent(qie_batch* b) {
+    qie_engine* e = b->e;
+    return persist_decode_launch(e->spec, b->d_layers, b->d_attp, b->x_res, (unsigned long long*)b->pk_mem,
+                                 pk_epoch_ptr(b), pk_epoch_ptr(b) + 1, b->d_pos, pk_splits_target(b), e->stream);
+}
+
 static int enqueue_decode(qie_batch* b, const qie_sampling* smp) {
-    for (int l = 0; l < b->e->spec.n_layers; l++) QIE_TRY(enqueue_layer_decode(b, l));
+    if (pk_on(b)) QIE_TRY(enqueue_layers_persistent(b));
+    else
+        for (int l = 0; l < b->e->spec.n_layers; l++) QIE_TRY(enqueue_layer_decode(b, l));
     return enqueue_head(b, b->x_res, b->e->spec.hidden, 0, b->B, smp);
 }
 
@@ -723,14 +761,30 @@ static int ensure_prefill_scratch(qie_batch* b, int64_t n) {
 // The ids and (tensor parallel, peer backend) the exchange error word come back in ONE
 // stream-ordered batch with one synchronisation — not a second blocking round trip per token
 // (ADVICE r05); a backend without the word keeps comm_check's own read.
+// The persistent step's error word (a bounded hand-off wait that gave up): the step's outputs
+// are garbage and the call fails loudly (never a hang; k_persist.hip)
+static int pk_fail(unsigned w) {
+    return fail(-8, "decode: the persistent decode step gave up on a hand-off wait (error word 0x%x: a CU never "
+                    "published its part within the bound); outputs of this step are invalid", w);
+}
+static int pk_check(qie_batch* b) {
+    if (!b->pk_mem) return 0;
+    unsigned w = 0;
+    QIE_HIP(hipMemcpyAsync(&w, pk_epoch_ptr(b) + 1, 4, hipMemcpyDeviceToHost, b->e->stream));
+    QIE_HIP(hipStreamSynchronize(b->e->stream));
+    return w ? pk_fail(w) : 0;
+}
+
 static int sync_ids(qie_batch* b, int32_t* next_ids) {
-    if (!next_ids) return 0;
+    if (!next_ids) return pk_check(b);
     qie_engine* e = b->e;
     QIE_HIP(hipMemcpyAsync(next_ids, b->d_ids, b->B * 4, hipMemcpyDeviceToHost, e->stream));
     const unsigned* ew = use_comm(e) ? e->comm->error_word() : nullptr;
-    unsigned err = 0;
+    unsigned err = 0, pkw = 0;
     if (ew) QIE_HIP(hipMemcpyAsync(&err, ew, sizeof(err), hipMemcpyDeviceToHost, e->stream));
+    if (b->pk_mem) QIE_HIP(hipMemcpyAsync(&pkw, pk_epoch_ptr(b) + 1, 4, hipMemcpyDeviceToHost, e->stream));
     QIE_HIP(hipStreamSynchronize(e->stream));
+    if (pkw) return pk_fail(pkw);
     if (ew) {
         if (err) return fail(-7, "decode: tensor-parallel exchange failed on the device (error word %u: a peer rank "
                                  "did not arrive within the bounded wait); the communicator is unusable", err);
@@ -1231,7 +1285,7 @@ void qie_batch_destroy(qie_batch* b) {
     void* ps[] = {b->kc, b->vc, b->d_table, b->d_pos, b->d_rope_cur, b->d_step, b->d_hist, b->d_ids, b->d_keys, b->x_res, b->qkv, b->q,
                   b->att, b->h, b->logits, b->attn_ws, b->dec_ws, b->samp_ws, b->pf_x, b->pf_hn, b->pf_qkv, b->pf_q,
                   b->pf_att, b->pf_h, b->pf_pos, b->pf_ids, b->pf_attn_ws, b->part, b->logits_full,
-                  b->gather_tmp, b->pf_part, b->xn, b->pf_q8, b->pf_e8};
+                  b->gather_tmp, b->pf_part, b->xn, b->pf_q8, b->pf_e8, b->pk_mem, b->d_layers, b->d_attp};
     for (void* p : ps)
         if (p) hipFree(p);
     delete b;
@@ -1469,6 +1523,7 @@ int qie_decode(qie_batch* b, int32_t n_steps, const qie_sampling* smp, int32_t* 
     }
     QIE_HIP(hipStreamSynchronize(b->e->stream));
     QIE_TRY(comm_check(b->e, "qie_decode"));
+    QIE_TRY(pk_check(b));
     if (out_ids && n_steps > 0) {
         std::vector<int32_t> row(b->max_ctx);
         for (int m = 0; m < b->B; m++) {
@@ -1488,6 +1543,7 @@ int qie_batch_logits(qie_batch* b, void* host_out) {
     }
     QIE_HIP(hipStreamSynchronize(b->e->stream));
     QIE_TRY(comm_check(b->e, "qie_batch_logits"));
+    QIE_TRY(pk_check(b));
     QIE_HIP(d2h(b->e, host_out, src, (size_t)b->B * b->e->spec.vocab * 2));
     return 0;
 }
@@ -1523,6 +1579,37 @@ int qie_batch_set_position(qie_batch* b, int32_t seq, int32_t pos, int32_t token
     b->h_pos[seq] = pos;
     return 0;
 }
+
+int qie_batch_set_decode_mode(qie_batch* b, int32_t mode) {
+    QIE_REQUIRE(b && (mode == 0 || mode == 1), "qie_batch_set_decode_mode: bad arguments (mode 0 or 1)");
+    qie_engine* e = b->e;
+    if (mode == 1) {
+        const char* why = "";
+        QIE_REQUIRE(persist_supported(e->spec, b->B, e->sh.tp, e->fp8, b->d_table != nullptr, device_cu_count(), &why),
+                    "qie_batch_set_decode_mode: the persistent decode step does not cover this batch (%s)", why);
+        if (!b->pk_mem) {
+            const size_t gb = (size_t)persist_granule_count(e->spec) * 8 + 64;
+            QIE_TRY(dmalloc(&b->pk_mem, gb));
+            QIE_TRY(dmalloc((void**)&b->d_layers, sizeof(qie_layer_weights) * e->layers.size()));
+            QIE_TRY(dmalloc(&b->d_attp, persist_attn_table_bytes((int)e->layers.size())));
+            QIE_HIP(hipMemsetAsync(b->pk_mem, 0, gb, e->stream));
+            QIE_HIP(hipMemcpyAsync(b->d_layers, e->layers.data(), sizeof(qie_layer_weights) * e->layers.size(),
+                                   hipMemcpyHostToDevice, e->stream));
+            const qie_kv_cache cache = batch_cache(b, 0);
+            set_decode_rope_cur(b->d_rope_cur);
+            const int rc = persist_attn_table(e->spec, e->layers.data(), b->qkv, b->d_pos, e->rope_cos, e->rope_sin,
+                                              &cache, b->dec_ws, b->d_attp, e->stream);
+            set_decode_rope_cur(nullptr);
+            QIE_TRY(rc);
+            QIE_HIP(hipStreamSynchronize(e->stream));
+        }
+    }
+    if (mode != b->decode_mode) b->graph_ok = false;   // re-captured at the next step
+    b->decode_mode = mode;
+    return 0;
+}
+
+int qie_batch_decode_mode(const qie_batch* b) { return b ? b->decode_mode : -22; }
 
 int qie_batch_dims(const qie_batch* b, int32_t* batch, int32_t* max_ctx) {
     QIE_REQUIRE(b, "qie_batch_dims: null batch");
@@ -1566,9 +1653,68 @@ int qie_engine_rope_tables(const qie_engine* e, const float** rope_cos, const fl
 // back to back would leave a ~272 MB gate/up working set largely in the 256 MiB Infinity
 // Cache and time a cache hit rate no decode step sees (round-1 verdict).  lm_head (which 4)
 // has one weight; its 1.09 GB stream cannot stay resident.
-int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* avg_us, double* bytes) {
-    QIE_REQUIRE(b && iters > 0 && avg_us && bytes && which >= 0 && which <= 5, "qie_batch_time_kernel: bad arguments");
+// which == 6: the persistent layer stack (k_persist.hip) alone, `iters` back-to-back launches at
+// the current position.  Each launch gets its own hand-off epoch (a device array of fresh
+// values, so no kernel runs between the timed launches); the residual row is restored and the
+// real epoch advanced past them afterwards, and the KV rows the launches wrote at the current
+// position are rewritten by the next real step.  Bytes: every layer weight read once plus the
+// K / V rows the attention reads.
+static int time_persistent(qie_batch* b, int iters, double* avg_us, double* bytes) {
     qie_engine* e = b->e;
+    const qie_model_spec& s = e->spec;
+    QIE_REQUIRE(b->decode_mode == 1 && b->pk_mem, "qie_batch_time_kernel: which 6 needs decode mode 1");
+    const int64_t H = s.hidden, hd = s.head_dim, QD = (int64_t)s.n_heads * hd, KD = (int64_t)s.n_kv_heads * hd,
+                  I = s.ffn;
+    int32_t pos = 0;
+    unsigned ep = 0;
+    QIE_HIP(d2h(e, &pos, b->d_pos, 4));
+    QIE_HIP(d2h(e, &ep, pk_epoch_ptr(b), 4));
+    const int n = iters + 4;
+    std::vector<unsigned> eps(n);
+    for (int i = 0; i < n; i++) eps[i] = ep + 1 + (unsigned)i;
+    unsigned* d_eps = nullptr;
+    uint16_t* xsave = nullptr;
+    QIE_TRY(dmalloc((void**)&d_eps, n * 4));
+    QIE_TRY(dmalloc((void**)&xsave, H * 2));
+    QIE_HIP(hipMemcpyAsync(d_eps, eps.data(), n * 4, hipMemcpyHostToDevice, e->stream));
+    QIE_HIP(hipMemcpyAsync(xsave, b->x_res, H * 2, hipMemcpyDeviceToDevice, e->stream));
+    // launches back to back on the same input: x_res is only read at layer 0 and written at the
+    // last layer, so each launch sees a row of the same magnitude (restored afterwards)
+    auto run = [&](int i) {
+        return persist_decode_launch(s, b->d_layers, b->d_attp, b->x_res, (unsigned long long*)b->pk_mem, d_eps + i,
+                                     pk_epoch_ptr(b) + 1, b->d_pos, pk_splits_target(b), e->stream);
+    };
+    hipEvent_t t0, t1;
+    QIE_HIP(hipEventCreate(&t0));
+    QIE_HIP(hipEventCreate(&t1));
+    for (int i = 0; i < 4; i++) QIE_TRY(run(i));
+    QIE_HIP(hipEventRecord(t0, e->stream));
+    for (int i = 0; i < iters; i++) QIE_TRY(run(4 + i));
+    QIE_HIP(hipEventRecord(t1, e->stream));
+    QIE_HIP(hipEventSynchronize(t1));
+    float ms = 0;
+    QIE_HIP(hipEventElapsedTime(&ms, t0, t1));
+    hipEventDestroy(t0);
+    hipEventDestroy(t1);
+    const unsigned ep_after = ep + (unsigned)n + 1;
+    QIE_HIP(hipMemcpyAsync(b->x_res, xsave, H * 2, hipMemcpyDeviceToDevice, e->stream));
+    QIE_HIP(hipMemcpyAsync(pk_epoch_ptr(b), &ep_after, 4, hipMemcpyHostToDevice, e->stream));
+    QIE_HIP(hipStreamSynchronize(e->stream));
+    hipFree(d_eps);
+    hipFree(xsave);
+    QIE_TRY(pk_check(b));
+    const double per_layer = (double)(QD + 2 * KD) * H * 2 + (double)(QD + 2 * KD) * 2 * (s.qkv_bias ? 1 : 0) +
+                             (double)H * QD * 2 + 2.0 * I * H * 2 + (double)H * I * 2 + 2.0 * H * 2 +
+                             (double)(pos + 1) * KD * 2 * 2;
+    *bytes = per_layer * s.n_layers;
+    *avg_us = ms * 1000.0 / iters;
+    return 0;
+}
+
+int qie_batch_time_kernel(qie_batch* b, int32_t which, int32_t iters, double* avg_us, double* bytes) {
+    QIE_REQUIRE(b && iters > 0 && avg_us && bytes && which >= 0 && which <= 6, "qie_batch_time_kernel: bad arguments");
+    qie_engine* e = b->e;
+    if (which == 6) return time_persistent(b, iters, avg_us, bytes);
     const qie_model_spec& s = e->spec;
     const TpShard& sh = e->sh;   // this rank's shard sizes
     const int64_t H = s.hidden, hd = s.head_dim, QD = (int64_t)sh.nq * hd, KD = (int64_t)sh.nkv * hd;

@@ -346,6 +346,14 @@ class Batch:
         _lib.check(self.lib.qie_batch_debug_step(self.h, C.byref(sc), out, xs.ctypes.data), "qie_batch_debug_step")
         return list(out), xs
 
+    def set_decode_mode(self, mode: int) -> None:
+        """0: five launches per layer; 1: the persistent layer stack (qie_batch_set_decode_mode)."""
+        _lib.check(self.lib.qie_batch_set_decode_mode(self.h, mode), "qie_batch_set_decode_mode")
+
+    @property
+    def decode_mode(self) -> int:
+        return int(self.lib.qie_batch_decode_mode(self.h))
+
     def time_kernel(self, which: int = 0, iters: int = 20):
         us, by = C.c_double(), C.c_double()
         _lib.check(self.lib.qie_batch_time_kernel(self.h, which, iters, C.byref(us), C.byref(by)),

@@ -185,6 +185,13 @@ int qie_batch_set_position(qie_batch* b, int32_t seq, int32_t pos, int32_t token
  * the decode graph.  qie_batch_decode_mode returns the current mode. */
 int qie_batch_set_decode_mode(qie_batch* b, int32_t mode);
 int qie_batch_decode_mode(const qie_batch* b);
+/* Diagnostics of decode mode 1: enable != 0 makes the persistent step record s_memrealtime
+ * stamps (100 MHz, chip-wide) at its phase boundaries, [n_cu][n_layers][12] uint64 (slots:
+ * 0 layer start, 1 x gathered, 2 QKV done, 3 attention done (attention CUs), 4 attention
+ * output gathered (other CUs), 5 O done, 6 x' gathered + norm, 7 gate/up done, 8 h gathered,
+ * 9 down done); host_out (n >= that count) receives the last step's stamps; enable = 0
+ * frees the buffer.  Changing it re-captures the decode graph. */
+int qie_batch_pk_trace(qie_batch* b, int32_t enable, uint64_t* host_out, int64_t n);
 /* Batch geometry: B slots, max_ctx positions per slot. */
 int qie_batch_dims(const qie_batch* b, int32_t* batch, int32_t* max_ctx);
 /* KV descriptor of slot `seq` for the operator tier (qie_kv_write, qie_attention with

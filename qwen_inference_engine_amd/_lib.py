@@ -187,6 +187,7 @@ SIGNATURES = [
     ("qie_batch_dims", C.c_int, [_P, _PI32, _PI32]),
     ("qie_batch_set_decode_mode", C.c_int, [_P, _I32]),
     ("qie_batch_decode_mode", C.c_int, [_P]),
+    ("qie_batch_pk_trace", C.c_int, [_P, _I32, _P, C.c_int64]),
     ("qie_batch_kv_cache", C.c_int, [_P, _I32, C.POINTER(KvCacheC)]),
     ("qie_batch_reserve", C.c_int, [_P, _I32, _I32]),
     ("qie_engine_arena", C.c_int, [_P, C.POINTER(_P), _PI64]),

@@ -38,8 +38,9 @@ int persist_attn_table(const qie_model_spec& s, const qie_layer_weights* h_layer
                        void* dec_ws, void* d_attp, hipStream_t st);
 int persist_decode_launch(const qie_model_spec& s, const qie_layer_weights* d_layers, const void* d_attp,
                           uint16_t* x_res, unsigned long long* granules, const unsigned* epoch, unsigned* err,
-                          const int32_t* pos, int splits_target, hipStream_t st);
+                          const int32_t* pos, int splits_target, unsigned long long* ts, hipStream_t st);
 int64_t persist_granule_count(const qie_model_spec& s);
+int persist_ts_slots();
 }  // namespace qie
 
 
@@ -164,6 +165,7 @@ struct qie_batch {
     void* pk_mem = nullptr;
     qie_layer_weights* d_layers = nullptr;
     void* d_attp = nullptr;      // the attention role's parameters per layer (persist_attn_table)
+    unsigned long long* pk_ts = nullptr;   // qie_batch_pk_trace: phase timestamps [cu][layer][slots]
 };
 
 namespace qie {
@@ -691,7 +693,8 @@ static int pk_splits_target(const qie_batch* b) { (void)b; return 32; }
 static int enqueue_layers_persistent(qie_batch* b) {
     qie_engine* e = b->e;
     return persist_decode_launch(e->spec, b->d_layers, b->d_attp, b->x_res, (unsigned long long*)b->pk_mem,
-                                 pk_epoch_ptr(b), pk_epoch_ptr(b) + 1, b->d_pos, pk_splits_target(b), e->stream);
+                                 pk_epoch_ptr(b), pk_epoch_ptr(b) + 1, b->d_pos, pk_splits_target(b), b->pk_ts,
+                                 e->stream);
 }
 
 static int enqueue_decode(qie_batch* b, const qie_sampling* smp) {
@@ -1285,7 +1288,7 @@ void qie_batch_destroy(qie_batch* b) {
     void* ps[] = {b->kc, b->vc, b->d_table, b->d_pos, b->d_rope_cur, b->d_step, b->d_hist, b->d_ids, b->d_keys, b->x_res, b->qkv, b->q,
                   b->att, b->h, b->logits, b->attn_ws, b->dec_ws, b->samp_ws, b->pf_x, b->pf_hn, b->pf_qkv, b->pf_q,
                   b->pf_att, b->pf_h, b->pf_pos, b->pf_ids, b->pf_attn_ws, b->part, b->logits_full,
-                  b->gather_tmp, b->pf_part, b->xn, b->pf_q8, b->pf_e8, b->pk_mem, b->d_layers, b->d_attp};
+                  b->gather_tmp, b->pf_part, b->xn, b->pf_q8, b->pf_e8, b->pk_mem, b->d_layers, b->d_attp, b->pk_ts};
     for (void* p : ps)
         if (p) hipFree(p);
     delete b;
@@ -1611,6 +1614,29 @@ int qie_batch_set_decode_mode(qie_batch* b, int32_t mode) {
 
 int qie_batch_decode_mode(const qie_batch* b) { return b ? b->decode_mode : -22; }
 
+int qie_batch_pk_trace(qie_batch* b, int32_t enable, uint64_t* host_out, int64_t n) {
+    QIE_REQUIRE(b, "qie_batch_pk_trace: null batch");
+    qie_engine* e = b->e;
+    const int64_t need = (int64_t)device_cu_count() * e->spec.n_layers * persist_ts_slots();
+    if (enable && !b->pk_ts) {
+        QIE_TRY(dmalloc((void**)&b->pk_ts, (size_t)need * 8));
+        QIE_HIP(hipMemsetAsync(b->pk_ts, 0, (size_t)need * 8, e->stream));
+        b->graph_ok = false;
+    }
+    if (host_out) {
+        QIE_REQUIRE(b->pk_ts && n >= need, "qie_batch_pk_trace: tracing off or n < %lld", (long long)need);
+        QIE_HIP(hipStreamSynchronize(e->stream));
+        QIE_HIP(d2h(e, host_out, b->pk_ts, (size_t)need * 8));
+    }
+    if (!enable && b->pk_ts) {
+        QIE_HIP(hipStreamSynchronize(e->stream));
+        hipFree(b->pk_ts);
+        b->pk_ts = nullptr;
+        b->graph_ok = false;
+    }
+    return 0;
+}
+
 int qie_batch_dims(const qie_batch* b, int32_t* batch, int32_t* max_ctx) {
     QIE_REQUIRE(b, "qie_batch_dims: null batch");
     if (batch) *batch = b->B;
@@ -1682,7 +1708,7 @@ static int time_persistent(qie_batch* b, int iters, double* avg_us, double* byte
     // last layer, so each launch sees a row of the same magnitude (restored afterwards)
     auto run = [&](int i) {
         return persist_decode_launch(s, b->d_layers, b->d_attp, b->x_res, (unsigned long long*)b->pk_mem, d_eps + i,
-                                     pk_epoch_ptr(b) + 1, b->d_pos, pk_splits_target(b), e->stream);
+                                     pk_epoch_ptr(b) + 1, b->d_pos, pk_splits_target(b), nullptr, e->stream);
     };
     hipEvent_t t0, t1;
     QIE_HIP(hipEventCreate(&t0));

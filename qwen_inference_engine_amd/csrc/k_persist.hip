@@ -50,6 +50,10 @@ constexpr int kWaves = 8;
 constexpr int kU = 8;        // 1-KiB wave-loads per row in flight (one pass)
 constexpr int kStage = 1024; // outputs a CU owns in one projection (bf16 staging in LDS)
 constexpr int kMaxBias = 256;
+// granules per gathering thread: x-sized vectors (H / 2, and the attention output QD / 2) by
+// one wave, h (I / 2) by four; persist_supported checks the model fits
+constexpr int kGatherX = 40;   // H, QD <= 5,120 (64 threads x 40 granules)
+constexpr int kGatherH = 38;   // I <= 19,456 (256 threads x 38 granules)
 
 struct Params {
     const qie_layer_weights* layers;   // device copy, [n_layers]
@@ -64,7 +68,10 @@ struct Params {
     const DecodeAttnParams* attp;      // device [n_layers]: the attention role's parameters per layer
     const int32_t* pos;                // the sequence position (B = 1)
     int splits_target;
+    unsigned long long* ts;            // diagnostics (qie_batch_pk_trace): [cu][layer][kTsSlots] s_memrealtime
+    unsigned pf_mask;                  // waves that may run ahead into the next projection (bit w: wave w)
 };
+constexpr int kTsSlots = 12;
 
 __device__ __forceinline__ float bl(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bh(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
@@ -123,11 +130,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, int64_t
 }
 
 // ------------------------------------------------------------------ bounded hand-off waits
-struct Ctl {
-    int* dead;          // LDS: this block gave up
-    long long t0;       // start of the current wait
-};
-
 __device__ __forceinline__ unsigned long long ld_granule(const unsigned long long* g) {
     return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -135,48 +137,58 @@ __device__ __forceinline__ void st_granule(unsigned long long* g, unsigned tag, 
     __hip_atomic_store(g, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// re-poll one granule until its tag is `tag`; false (and the error word set) on a timeout or
-// when another block has failed
-__device__ __forceinline__ bool spin_granule(const unsigned long long* g, unsigned tag, unsigned long long& v,
-                                          const Params& p, unsigned code) {
-    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-    for (int it = 0;; it++) {
-        __builtin_amdgcn_s_sleep(1);
-        v = ld_granule(g);
-        if ((unsigned)(v >> 32) == tag) return true;
-        if ((it & 63) == 63) {
-            if (__hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return false;
-            if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > p.spin_ticks) {
-                __hip_atomic_fetch_or(p.err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                return false;
-            }
-        }
-    }
-}
-
-// threads t (0 <= t < nt) of the calling waves gather granules [0, n) of g into dst (u32 each);
-// a failure marks the block dead (LDS flag, read after the next barrier)
-template <int B>
+// Threads t (0 <= t < nt) of the calling waves gather granules [0, n) of g into dst (u32
+// payload each): thread t owns the M consecutive granules [t M, t M + M) (M even), read as 16-B
+// sc1 buffer loads (two granules per load: each granule still validates itself by its tag).
+// Whole sweeps: every granule still missing is re-loaded in ONE batch per pass — one memory round
+// trip per pass, never one dependent re-poll per granule (the first form spun on each missing
+// granule in turn: 6-10 us per gather, tools/pk_trace.py r06).  The byte offset is made opaque
+// each pass, so the loads are re-issued, not hoisted out of the poll loop.  A failure (timeout,
+// or another block's error word) marks the block dead (LDS flag, read after the next barrier).
+template <int M>
 __device__ __forceinline__ void gather(const unsigned long long* g, int n, unsigned tag, uint32_t* dst, int t, int nt,
                                        const Params& p, int* dead, unsigned code) {
-    bool ok = true;
-    for (int base = t; base < n; base += nt * B) {
-        unsigned long long v[B];
+    static_assert(M % 2 == 0 && M <= 64, "pairs, mask of 64");
+    (void)nt;
+    const int base = t * M;
+    const __amdgpu_buffer_rsrc_t rs = rsrc(g, (int64_t)n * 8);   // past n: zeros (tag 0, never awaited)
+    unsigned long long need = 0ull;
 #pragma unroll
-        for (int j = 0; j < B; j++) {
-            const int i = base + j * nt;
-            v[j] = ld_granule(g + (i < n ? i : 0));
+    for (int j = 0; j < M; j++)
+        if (base + j < n) need |= 1ull << j;
+    int vo = base * 8;
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    for (int pass = 0;; pass++) {
+        asm volatile("" : "+v"(vo));
+        u32x4 r[M / 2];
+#pragma unroll
+        for (int k = 0; k < M / 2; k++)
+            if ((need >> (2 * k)) & 3ull) r[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 16 * k, 0, 16);
+#pragma unroll
+        for (int k = 0; k < M / 2; k++) {
+            if (((need >> (2 * k)) & 1ull) && r[k].y == tag) {
+                dst[base + 2 * k] = r[k].x;
+                need &= ~(1ull << (2 * k));
+            }
+            if (((need >> (2 * k + 1)) & 1ull) && r[k].w == tag) {
+                dst[base + 2 * k + 1] = r[k].z;
+                need &= ~(1ull << (2 * k + 1));
+            }
         }
-#pragma unroll
-        for (int j = 0; j < B; j++) {
-            const int i = base + j * nt;
-            if (i < n) {
-                if ((unsigned)(v[j] >> 32) != tag && ok) ok = spin_granule(g + i, tag, v[j], p, code);
-                dst[i] = (uint32_t)v[j];
+        if (__builtin_amdgcn_ballot_w64(need != 0ull) == 0ull) return;   // this wave's share is in
+        __builtin_amdgcn_s_sleep(2);
+        if ((pass & 7) == 7) {
+            bool stop = __hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+            if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > p.spin_ticks) {
+                if (!stop) __hip_atomic_fetch_or(p.err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                stop = true;
+            }
+            if (__builtin_amdgcn_ballot_w64(stop) != 0ull) {
+                *dead = 1;
+                return;
             }
         }
     }
-    if (!ok) *dead = 1;
 }
 
 // ------------------------------------------------------------------ GEMV tasks
@@ -321,16 +333,17 @@ struct AttnHook {
     const Params* p;
     int* dead;
     __device__ void gather() {
-        const int nqg = G * hd / 2, nk = hd / 2, n = nqg + 2 * nk;
+        // q of the kv head's G heads (G hd / 2 granules), then its k and v rows (hd / 2 each)
+        const int nqg = G * hd / 2, nk = hd / 2;
         uint32_t* r32 = reinterpret_cast<uint32_t*>(row);
-        bool ok = true;
-        for (int i = threadIdx.x; i < n; i += kThreads) {
-            const int gi = i < nqg ? g * nqg + i : (i < nqg + nk ? (QD + g * hd) / 2 + (i - nqg) : (QD + KD + g * hd) / 2 + (i - nqg - nk));
-            unsigned long long v = ld_granule(g_qkv + gi);
-            if ((unsigned)(v >> 32) != tag && ok) ok = spin_granule(g_qkv + gi, tag, v, *p, 2u);
-            r32[gi] = (uint32_t)v;
+        const int t = threadIdx.x;
+        if (2 * t < nqg) pk::gather<2>(g_qkv + g * nqg, nqg, tag, r32 + g * nqg, t, kThreads, *p, dead, 2u);
+        const int tk = t - kThreads / 2;   // waves 4..5: k, then v
+        if (tk >= 0 && tk < nk) {
+            const int kv = tk < nk / 2 ? (QD + g * hd) / 2 : (QD + KD + g * hd) / 2;
+            const int tt = tk < nk / 2 ? tk : tk - nk / 2;
+            pk::gather<2>(g_qkv + kv, nk, tag, r32 + kv, tt, nk / 2, *p, dead, 2u);
         }
-        if (!ok) *dead = 1;
         __syncthreads();
     }
     __device__ void out1(int64_t i, uint16_t v) { stage[i - o0] = v; }
@@ -407,8 +420,18 @@ __global__ __launch_bounds__(kThreads, 1) void decode_layers_kernel(Params p) {
     };
     // first task of this wave in a projection with n local tasks (none: false)
     auto pf_issue = [&](bool has, const Task& t) {
+        has = has && ((p.pf_mask >> wave) & 1u);
         if (has) issue(t, 0, wv);
         pf = has;
+    };
+
+    // A gathering wave holds no run-ahead task (pf_issue never gives wave 0, nor the h gatherers,
+    // one): redefining the register set at the end of its gather ends the set's live range before
+    // the gather, so the gather's loads get those registers instead of spilling.
+    auto drop_wv = [&]() {
+#pragma unroll
+        for (int u = 0; u < kU; u++) wv[u][0] = wv[u][1] = u32x4{0u, 0u, 0u, 0u};
+        pf = false;
     };
 
     // run this wave's local tasks [0, n) of a projection; mk(i) = the task, epi(i, a0, a1) =
@@ -438,8 +461,14 @@ __global__ __launch_bounds__(kThreads, 1) void decode_layers_kernel(Params p) {
     // layer 0's first QKV task goes out before anything else (waves 1..7; wave 0 gathers)
     pf_issue(wave != 0 && wfirst < q1 - q0, qkv_task(0, q0 + (wfirst < q1 - q0 ? wfirst : 0)));
 
+    // phase timestamps (diagnostics only: one uniform branch when off)
+    auto ts = [&](int l, int slot) {
+        if (p.ts && tid == 0)
+            p.ts[((size_t)cu * p.n_layers + l) * kTsSlots + slot] = __builtin_amdgcn_s_memrealtime();
+    };
     for (int l = 0; l < p.n_layers; l++) {
         const unsigned tg = tagl(l);
+        ts(l, 0);
         // ============ QKV: x -> rms -> q, k, v (+bias)
         if (wave == 0) {
             // this CU's bias values and the norm weights first (no wait behind the gather)
@@ -455,10 +484,12 @@ __global__ __launch_bounds__(kThreads, 1) void decode_layers_kernel(Params p) {
                 for (int i = lane; i * 8 < H; i += 64)
                     *reinterpret_cast<uint4*>(xraw + i * 8) = *reinterpret_cast<const uint4*>(p.x_res + i * 8);
             } else {
-                gather<16>(p.g_x, H / 2, tg, reinterpret_cast<uint32_t*>(xraw), lane, 64, p, dead, 1u);
+                gather<kGatherX>(p.g_x, H / 2, tg, reinterpret_cast<uint32_t*>(xraw), lane, 64, p, dead, 1u);
             }
+            drop_wv();
         }
         bar();
+        ts(l, 1);
         if (*dead) return;
         ss_xfirst256(xraw, H, red);
         bar();
@@ -478,6 +509,7 @@ __global__ __launch_bounds__(kThreads, 1) void decode_layers_kernel(Params p) {
                 pf_issue(!att_cu && wave != 0 && i < o1 - o0, att_cu ? qkv_task(l, q0) : o_task(l, o0 + (i < o1 - o0 ? i : 0)));
             });
         bar();
+        ts(l, 2);
         if (wave == 0)
             for (int i = lane; i < q1 - q0; i += 64)
                 st_granule(p.g_qkv + q0 + i, tg, reinterpret_cast<const uint32_t*>(stage)[i]);
@@ -510,6 +542,7 @@ __global__ __launch_bounds__(kThreads, 1) void decode_layers_kernel(Params p) {
                     st_granule(p.g_att + g * (G * HD / 2) + i, tg, reinterpret_cast<const uint32_t*>(astage)[i]);
             }
             __syncthreads();
+            ts(l, 3);
             if (*dead) return;
             // no run-ahead task is pending here (pf is false on attention CUs): redefining the
             // register set ends its live range before the body, so the body gets those registers
@@ -518,8 +551,12 @@ __global__ __launch_bounds__(kThreads, 1) void decode_layers_kernel(Params p) {
         }
         // ============ O: attention out -> O rows (+residual) on the CUs that own them
         if (!att_cu) {
-            if (wave == 0) gather<16>(p.g_att, QD / 2, tg, reinterpret_cast<uint32_t*>(xn), lane, 64, p, dead, 3u);
+            if (wave == 0) {
+                gather<kGatherX>(p.g_att, QD / 2, tg, reinterpret_cast<uint32_t*>(xn), lane, 64, p, dead, 3u);
+                drop_wv();
+            }
             bar();
+            ts(l, 4);
             if (*dead) return;
         }
         run_tasks(
@@ -535,6 +572,7 @@ __global__ __launch_bounds__(kThreads, 1) void decode_layers_kernel(Params p) {
                 pf_issue(wave != 0 && i < n, gu_task(l, 2 * j0 + (i < n ? i : 0)));
             });
         bar();
+        ts(l, 5);
         if (wave == 0 && !att_cu)
             for (int i = lane; i < o1 - o0; i += 64)
                 st_granule(p.g_x1 + o0 + i, tg, reinterpret_cast<const uint32_t*>(stage)[i]);
@@ -542,11 +580,13 @@ __global__ __launch_bounds__(kThreads, 1) void decode_layers_kernel(Params p) {
         if (wave == 0) {
             for (int i = lane; i * 8 < H; i += 64)
                 *reinterpret_cast<uint4*>(nw + i * 8) = *reinterpret_cast<const uint4*>((const uint16_t*)PK_LW(LT, l, ffn_norm) + i * 8);
-            gather<16>(p.g_x1, H / 2, tg, reinterpret_cast<uint32_t*>(x1raw), lane, 64, p, dead, 4u);
+            gather<kGatherX>(p.g_x1, H / 2, tg, reinterpret_cast<uint32_t*>(x1raw), lane, 64, p, dead, 4u);
             const float ss = ss_wave(x1raw, H);
             if (lane == 0) red[0] = ss;
+            drop_wv();
         }
         bar();
+        ts(l, 6);
         if (*dead) return;
         normalize(x1raw, nw, xn, H, sqrtf((red[0] / (float)H) + p.eps), hf);
         bar();
@@ -564,12 +604,17 @@ __global__ __launch_bounds__(kThreads, 1) void decode_layers_kernel(Params p) {
                 pf_issue(wave >= 4 && i < n, dn_task(l, d0 + (i < n ? i : 0)));
             });
         bar();
+        ts(l, 7);
         if (wave == 0)
             for (int i = lane; i < j1 - j0; i += 64)
                 st_granule(p.g_h + j0 + i, tg, reinterpret_cast<const uint32_t*>(stage)[i]);
         // ============ down: h -> down rows (+residual) -> next layer's x
-        if (wave < 4) gather<16>(p.g_h, I / 2, tg, reinterpret_cast<uint32_t*>(hb), tid, 256, p, dead, 5u);
+        if (wave < 4) {
+            gather<kGatherH>(p.g_h, I / 2, tg, reinterpret_cast<uint32_t*>(hb), tid, 256, p, dead, 5u);
+            drop_wv();
+        }
         bar();
+        ts(l, 8);
         if (*dead) return;
         const bool last = l + 1 == p.n_layers;
         run_tasks(
@@ -585,6 +630,7 @@ __global__ __launch_bounds__(kThreads, 1) void decode_layers_kernel(Params p) {
                 pf_issue(!last && wave != 0 && i < q1 - q0, qkv_task(last ? l : l + 1, q0 + (i < q1 - q0 ? i : 0)));
             });
         bar();
+        ts(l, 9);
         if (wave == 0) {
             if (last) {
                 for (int i = lane; i < d1 - d0; i += 64)
@@ -628,6 +674,8 @@ bool persist_supported(const qie_model_spec& s, int B, int tp, bool fp8, bool pa
     if (s.head_dim != 128) return no("head_dim != 128");
     if (s.hidden % 512 || s.ffn % 512 || QD % 512) return no("widths not multiples of 512");
     if (G > 8) return no("group > 8");
+    if (s.hidden / 2 > 64 * pk::kGatherX || QD / 2 > 64 * pk::kGatherX || s.ffn / 2 > 256 * pk::kGatherH)
+        return no("widths beyond the gather capacity");
     const int nsplit_max = 32;
     if (s.n_kv_heads * nsplit_max >= ncu) return no("too few CUs for the attention jobs");
     const int QKVD = QD + 2 * KD;
@@ -659,7 +707,7 @@ int persist_attn_table(const qie_model_spec& s, const qie_layer_weights* h_layer
 
 int persist_decode_launch(const qie_model_spec& s, const qie_layer_weights* d_layers, const void* d_attp,
                           uint16_t* x_res, unsigned long long* granules, const unsigned* epoch, unsigned* err,
-                          const int32_t* pos, int splits_target, hipStream_t st) {
+                          const int32_t* pos, int splits_target, unsigned long long* ts, hipStream_t st) {
     pk::Params p;
     p.layers = d_layers;
     p.n_layers = s.n_layers;
@@ -685,6 +733,8 @@ int persist_decode_launch(const qie_model_spec& s, const qie_layer_weights* d_la
     p.attp = (const DecodeAttnParams*)d_attp;
     p.pos = pos;
     p.splits_target = splits_target;
+    p.ts = ts;
+    p.pf_mask = (unsigned)dev_env("QIE_PK_PF_MASK", 0xFF);
     const size_t shm = persist_lds_bytes(p.H, p.I, p.QD, p.KD, p.nq / p.nkv, p.hd);
     static bool raised = false;
     if (!raised) {
@@ -697,6 +747,8 @@ int persist_decode_launch(const qie_model_spec& s, const qie_layer_weights* d_la
     QIE_LAUNCH_CHECK();
     return 0;
 }
+
+int persist_ts_slots() { return pk::kTsSlots; }
 
 int64_t persist_granule_count(const qie_model_spec& s) {
     const int QD = s.n_heads * s.head_dim, KD = s.n_kv_heads * s.head_dim;

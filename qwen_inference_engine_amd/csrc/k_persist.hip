@@ -45,8 +45,10 @@ namespace pk {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kThreads = 512;
-constexpr int kWaves = 8;
+// waves per workgroup (one workgroup per CU): 8 at head_dim 128 (the attention body runs on all
+// 8), 4 at head_dim 64 (its MFMA tiles need a 16-dim P.V slice per wave: 64 / 16)
+template <int HD>
+constexpr int waves_for() { return HD == 128 ? 8 : 4; }
 constexpr int kU = 8;        // 1-KiB wave-loads per row in flight (one pass)
 constexpr int kStage = 1024; // outputs a CU owns in one projection (bf16 staging in LDS)
 constexpr int kMaxBias = 256;
@@ -70,6 +72,7 @@ struct Params {
     int splits_target;
     unsigned long long* ts;            // diagnostics (qie_batch_pk_trace): [cu][layer][kTsSlots] s_memrealtime
     unsigned pf_mask;                  // waves that may run ahead into the next projection (bit w: wave w)
+    int xw_even;                       // row share of a CU on an even XCD, per 100 of an odd one's (gate/up, down)
 };
 constexpr int kTsSlots = 12;
 
@@ -288,7 +291,7 @@ __device__ __forceinline__ void normalize(const uint16_t* x, const uint16_t* nw,
                                           bool hf) {
 #pragma clang fp contract(off)
     const float inv = 1.0f / rms;
-    for (int i = threadIdx.x; i * 8 < K; i += kThreads) {
+    for (int i = threadIdx.x; i * 8 < K; i += blockDim.x) {
         float f[8], wf[8];
         unpack8(*reinterpret_cast<const uint4*>(x + i * 8), f);
         unpack8(*reinterpret_cast<const uint4*>(nw + i * 8), wf);
@@ -314,6 +317,14 @@ __device__ __forceinline__ void span(int n, int parts, int i, int& lo, int& hi) 
     lo = (int)((int64_t)n * i / parts);
     hi = (int)((int64_t)n * (i + 1) / parts);
 }
+// the same with CU weights: even CUs (blockIdx % 8 even: XCDs 0, 2, 4, 6 under round-robin
+// placement) weigh we, odd ones 100 — a speed share, never correctness (every item is owned once)
+__device__ __forceinline__ void wspan(int n, int parts, int i, int we, int& lo, int& hi) {
+    auto W = [&](int c) { return (int64_t)((c + 1) / 2) * we + (int64_t)(c / 2) * 100; };
+    const int64_t tot = W(parts);
+    lo = (int)((int64_t)n * W(i) / tot);
+    hi = (int)((int64_t)n * W(i + 1) / tot);
+}
 
 __device__ __forceinline__ void bar() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // LDS writes visible; VMEM loads stay in flight
@@ -322,6 +333,7 @@ __device__ __forceinline__ void bar() {
 
 // attention role hook (attn_decode.hpp): q / k / v row of kv head g from the QKV granules,
 // outputs into an LDS staging row
+template <int NT>
 struct AttnHook {
     static constexpr bool on = true;
     const unsigned long long* g_qkv;
@@ -337,8 +349,8 @@ struct AttnHook {
         const int nqg = G * hd / 2, nk = hd / 2;
         uint32_t* r32 = reinterpret_cast<uint32_t*>(row);
         const int t = threadIdx.x;
-        if (2 * t < nqg) pk::gather<2>(g_qkv + g * nqg, nqg, tag, r32 + g * nqg, t, kThreads, *p, dead, 2u);
-        const int tk = t - kThreads / 2;   // waves 4..5: k, then v
+        if (2 * t < nqg) pk::gather<2>(g_qkv + g * nqg, nqg, tag, r32 + g * nqg, t, NT, *p, dead, 2u);
+        const int tk = t - NT / 2;   // from the middle wave on: k, then v
         if (tk >= 0 && tk < nk) {
             const int kv = tk < nk / 2 ? (QD + g * hd) / 2 : (QD + KD + g * hd) / 2;
             const int tt = tk < nk / 2 ? tk : tk - nk / 2;
@@ -353,8 +365,9 @@ struct AttnHook {
 };
 
 // ------------------------------------------------------------------ the kernel
-template <int HD>
-__global__ __launch_bounds__(kThreads, 1) void decode_layers_kernel(Params p) {
+template <int HD, int NW = waves_for<HD>()>
+__global__ __launch_bounds__(NW * 64, 1) void decode_layers_kernel(Params p) {
+    constexpr int kWaves = NW, kThreads = NW * 64;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -393,8 +406,8 @@ __global__ __launch_bounds__(kThreads, 1) void decode_layers_kernel(Params p) {
     int q0, q1, o0 = 0, o1 = 0, j0, j1, d0, d1;
     span(QKVD / 2, ncu, cu, q0, q1);
     if (!att_cu) span(H / 2, nO, cu - nA, o0, o1);
-    span(I / 2, ncu, cu, j0, j1);
-    span(H / 2, ncu, cu, d0, d1);
+    wspan(I / 2, ncu, cu, p.xw_even, j0, j1);
+    wspan(H / 2, ncu, cu, p.xw_even, d0, d1);
     // local task i of a projection -> wave (i + 1) % 8: wave 0 (the gathering wave) last
     const int wfirst = (wave + kWaves - 1) % kWaves;
 
@@ -518,7 +531,7 @@ __global__ __launch_bounds__(kThreads, 1) void decode_layers_kernel(Params p) {
             const int g = cu / nsplit, s = cu % nsplit;
             DecodeAttnParams a = sld_struct(p.attp + l);   // layer, q / k norms set by the host
             a.qkv = hb;   // generic pointer into LDS: the body reads its row from the gathered image
-            AttnHook hk;
+            AttnHook<kThreads> hk;
             hk.g_qkv = p.g_qkv;
             hk.row = hb;
             hk.stage = astage;
@@ -531,7 +544,7 @@ __global__ __launch_bounds__(kThreads, 1) void decode_layers_kernel(Params p) {
             hk.tag = tg;
             hk.p = &p;
             hk.dead = dead;
-            const bool comb = attn_decode_mfma2_body<HD, false, kWaves, false, kDecMStep, AttnHook>(
+            const bool comb = attn_decode_mfma2_body<HD, false, kWaves, false, kDecMStep, AttnHook<kThreads>>(
                 a, g * a.nsplit_max + s, 0, &hk);
             // the combiner's ticket reset (and every partial store) is performed before anything
             // this CU publishes later — the next layer's splits take tickets only after that
@@ -601,7 +614,7 @@ __global__ __launch_bounds__(kThreads, 1) void decode_layers_kernel(Params p) {
             },
             [&] {   // run-ahead: down's first task (waves 4..7; waves 0..3 gather h)
                 const int i = wfirst, n = d1 - d0;
-                pf_issue(wave >= 4 && i < n, dn_task(l, d0 + (i < n ? i : 0)));
+                pf_issue(wave >= kWaves / 2 && i < n, dn_task(l, d0 + (i < n ? i : 0)));
             });
         bar();
         ts(l, 7);
@@ -609,8 +622,8 @@ __global__ __launch_bounds__(kThreads, 1) void decode_layers_kernel(Params p) {
             for (int i = lane; i < j1 - j0; i += 64)
                 st_granule(p.g_h + j0 + i, tg, reinterpret_cast<const uint32_t*>(stage)[i]);
         // ============ down: h -> down rows (+residual) -> next layer's x
-        if (wave < 4) {
-            gather<kGatherH>(p.g_h, I / 2, tg, reinterpret_cast<uint32_t*>(hb), tid, 256, p, dead, 5u);
+        if (wave < kWaves / 2) {   // the first half gathers h; the second has down's first tasks in flight
+            gather<kGatherH>(p.g_h, I / 2, tg, reinterpret_cast<uint32_t*>(hb), tid, kThreads / 2, p, dead, 5u);
             drop_wv();
         }
         bar();
@@ -671,10 +684,14 @@ bool persist_supported(const qie_model_spec& s, int B, int tp, bool fp8, bool pa
     if (tp != 1) return no("tensor parallel");
     if (fp8) return no("fp8 weights");
     if (paged) return no("paged KV cache");
-    if (s.head_dim != 128) return no("head_dim != 128");
-    if (s.hidden % 512 || s.ffn % 512 || QD % 512) return no("widths not multiples of 512");
+    if (s.head_dim != 128 && s.head_dim != 64) return no("head_dim not 64 or 128");
+    if (s.hidden % 16 || s.ffn % 16 || QD % 16 || KD % 16) return no("widths not multiples of 16");
+    // every CU owns at least one down granule: the x hand-off then orders every CU's reads of a
+    // layer's buffers before any write of the next layer's (k_persist.hip header)
+    if (s.hidden / 2 < ncu) return no("hidden / 2 < CUs");
     if (G > 8) return no("group > 8");
-    if (s.hidden / 2 > 64 * pk::kGatherX || QD / 2 > 64 * pk::kGatherX || s.ffn / 2 > 256 * pk::kGatherH)
+    const int nw = s.head_dim == 128 ? 8 : 4;
+    if (s.hidden / 2 > 64 * pk::kGatherX || QD / 2 > 64 * pk::kGatherX || s.ffn / 2 > 32 * nw * pk::kGatherH)
         return no("widths beyond the gather capacity");
     const int nsplit_max = 32;
     if (s.n_kv_heads * nsplit_max >= ncu) return no("too few CUs for the attention jobs");
@@ -735,15 +752,21 @@ int persist_decode_launch(const qie_model_spec& s, const qie_layer_weights* d_la
     p.splits_target = splits_target;
     p.ts = ts;
     p.pf_mask = (unsigned)dev_env("QIE_PK_PF_MASK", 0xFF);
+    p.xw_even = dev_env("QIE_PK_XW", 100);
     const size_t shm = persist_lds_bytes(p.H, p.I, p.QD, p.KD, p.nq / p.nkv, p.hd);
-    static bool raised = false;
-    if (!raised) {
-        QIE_HIP(hipFuncSetAttribute((const void*)pk::decode_layers_kernel<128>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm + 4096));
-        raised = true;
+    const void* fn = s.head_dim == 128 ? (const void*)pk::decode_layers_kernel<128> : (const void*)pk::decode_layers_kernel<64>;
+    static bool raised[2] = {false, false};
+    bool& r = raised[s.head_dim == 128 ? 1 : 0];
+    if (!r) {
+        QIE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm + 4096));
+        r = true;
     }
-    hipLaunchKernelGGL(pk::decode_layers_kernel<128>, dim3((unsigned)device_cu_count()), dim3(pk::kThreads), shm, st,
-                       p);
+    if (s.head_dim == 128)
+        hipLaunchKernelGGL(pk::decode_layers_kernel<128>, dim3((unsigned)device_cu_count()), dim3(64 * pk::waves_for<128>()),
+                           shm, st, p);
+    else
+        hipLaunchKernelGGL(pk::decode_layers_kernel<64>, dim3((unsigned)device_cu_count()), dim3(64 * pk::waves_for<64>()),
+                           shm, st, p);
     QIE_LAUNCH_CHECK();
     return 0;
 }

@@ -44,7 +44,8 @@ def _gen(b, prompt, steps, mode):
     (S.QWEN2_7B.replace(n_layers=2), 2040, 24),     # 16 -> 17 splits at ctx 2,049
     (QWEN3_T, 100, 170),                            # qk-norm, no bias, 4 q heads per kv head
     (QWEN3_T.replace(numerics="hf"), 60, 80),       # HF numerics (rotate_half RoPE, HF norms)
-], ids=["qwen2-7b-short", "qwen2-7b-2k", "qwen3-qknorm", "qwen3-hf"])
+    (S.QWEN2_0_5B.replace(n_layers=3), 128, 140),   # hd 64 (4-wave workgroups), config 2's ctx 129..
+], ids=["qwen2-7b-short", "qwen2-7b-2k", "qwen3-qknorm", "qwen3-hf", "qwen2-0.5b"])
 def test_persistent_equals_launches(spec, P, steps):
     syn = SYN if spec.hidden < 2048 else W.SynthParams(seed=0)
     max_ctx = P + steps + 8
@@ -75,9 +76,9 @@ def test_persistent_mode_switch_and_refusals():
         eng.batch(2, 512).set_decode_mode(1)
     with pytest.raises(_lib.QieError, match="paged"):
         eng.batch(1, 512, page_tokens=128).set_decode_mode(1)
-    small = Q.Engine(S.tiny("t64", n_layers=1, hidden=512, n_heads=8, n_kv_heads=2, head_dim=64, ffn=1024,
+    small = Q.Engine(S.tiny("t32", n_layers=1, hidden=256, n_heads=4, n_kv_heads=2, head_dim=64, ffn=512,
                             vocab=512), max_ctx=64).init_synthetic(SYN)
-    with pytest.raises(_lib.QieError, match="head_dim"):
+    with pytest.raises(_lib.QieError, match="hidden / 2 < CUs"):
         small.batch(1, 64).set_decode_mode(1)
 
 

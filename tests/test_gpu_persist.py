@@ -3,7 +3,8 @@ five-launch step it replaces (mode 0), BIT FOR BIT, and against the oracle.
 
 Mode 1 runs every layer of a batch-1 decode step in ONE launch: each CU streams its rows of
 every projection with the launch path's exact per-lane fp32 order, the RMSNorms in the launch
-path's orders, the attention as the stand-alone kernel's body (8 waves), and hands activations
+path's orders, the attention as the stand-alone kernel's body (8 waves at head_dim 128, 4 at 64),
+and hands activations
 between CUs as tagged granules.  Every output is therefore the same bytes as mode 0's — ids and
 logits are compared for equality, not within a tolerance.  Contexts cover one split (ctx <=
 256), the 1 -> 3 split change at 257, and 16 -> 17 splits around 2,048 (the headline's range);

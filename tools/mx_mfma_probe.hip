@@ -106,6 +106,39 @@ int main() {
         if (t == 5) std::printf("case 5 lane map: %s\n", maxerr[0] <= 2e-4 ? "per-32-k-block (lane = row + 16 blk)"
                                                  : (maxerr[1] <= 2e-4 ? "lane = row, one scale per 128 k (lanes 16..63 ignored)"
                                                                       : "neither modelled map"));
+        if (t == 5) {
+            // fit, per A row i, the scale exponent the hardware applied to each 32-k block b
+            // (all (e0..e3) in [-3, 3]^4, least max relative error over the 16 columns): the
+            // exponents name the lane group whose scale byte was used (hsa = 126 + lane / 16)
+            for (int i = 0; i < 16; i++) {
+                double S[4][16];
+                for (int b = 0; b < 4; b++)
+                    for (int j = 0; j < 16; j++) {
+                        double sum = 0;
+                        for (int k = 32 * b; k < 32 * b + 32; k++)
+                            sum += (double)e4m3(hA[i * 128 + k]) * (double)e4m3(hB[j * 128 + k]) *
+                                   std::ldexp(1.0, hsb[j + 16 * b] - 127);
+                        S[b][j] = sum;
+                    }
+                int best[4] = {0, 0, 0, 0};
+                double berr = 1e300;
+                for (int c = 0; c < 7 * 7 * 7 * 7; c++) {
+                    const int e[4] = {c % 7 - 3, (c / 7) % 7 - 3, (c / 49) % 7 - 3, (c / 343) % 7 - 3};
+                    double err = 0;
+                    for (int j = 0; j < 16; j++) {
+                        double v = 0, a = 0;
+                        for (int b = 0; b < 4; b++) {
+                            v += std::ldexp(S[b][j], e[b]);
+                            a += std::fabs(std::ldexp(S[b][j], e[b]));
+                        }
+                        err = std::fmax(err, std::fabs(hC[i * 16 + j] - v) / (a + 1e-30));
+                    }
+                    if (err < berr) { berr = err; for (int b = 0; b < 4; b++) best[b] = e[b]; }
+                }
+                std::printf("case 5 row %2d: fitted block exponents %d %d %d %d (err %.1e); lane groups %d %d %d %d\n", i,
+                            best[0], best[1], best[2], best[3], berr, best[0] + 1, best[1] + 1, best[2] + 1, best[3] + 1);
+            }
+        }
     }
     std::printf("%s\n", fails ? "FAIL" : "OK");
     return fails ? 1 : 0;

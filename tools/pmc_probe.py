@@ -24,7 +24,8 @@ def main():
     fp8b8 = os.environ.get("PMC_CONFIG") == "fp8b8"   # BASELINE config 4: fp8 weights, batch 8, prompt 1024
     P, B = (1024, 8) if fp8b8 else (2048, 1)
     eng = Q.Engine(spec, max_ctx=P + 64, weight_fp8=fp8b8).init_synthetic(W.SynthParams(seed=0))
-    b = eng.batch(B, P + 64)
+    # PMC_PAGED=N: the paged KV cache of N-token pages (bench.py's config 4 runs 128)
+    b = eng.batch(B, P + 64, page_tokens=int(os.environ["PMC_PAGED"]) if os.environ.get("PMC_PAGED") else None)
     prompts = np.random.default_rng(1).integers(0, spec.vocab, (B, P))
     if B > 1:
         b.prefill_batch(0, prompts)

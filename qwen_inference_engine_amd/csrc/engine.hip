@@ -1466,6 +1466,28 @@ static int launch_step(qie_batch* b, const qie_sampling* smp) {
             return rc;
         }
         if (he != hipSuccess) return fail((int)he, "graph capture: %s", hipGetErrorString(he));
+        if (dev_env("QIE_GRAPH_DUMP", 0)) {   // dev: every node of the decode graph (type, grid, block, LDS)
+            size_t n = 0;
+            hipGraphGetNodes(g, nullptr, &n);
+            std::vector<hipGraphNode_t> nodes(n);
+            hipGraphGetNodes(g, nodes.data(), &n);
+            size_t max_shm = 0;
+            for (size_t i = 0; i < n; i++) {
+                hipGraphNodeType t;
+                hipGraphNodeGetType(nodes[i], &t);
+                if (t == hipGraphNodeTypeKernel) {
+                    hipKernelNodeParams kp{};
+                    hipGraphKernelNodeGetParams(nodes[i], &kp);
+                    max_shm = std::max(max_shm, (size_t)kp.sharedMemBytes);
+                    fprintf(stderr, "graph node %zu: kernel %p grid %u,%u,%u block %u,%u,%u dyn_lds %u\n", i, kp.func,
+                            kp.gridDim.x, kp.gridDim.y, kp.gridDim.z, kp.blockDim.x, kp.blockDim.y, kp.blockDim.z,
+                            kp.sharedMemBytes);
+                } else {
+                    fprintf(stderr, "graph node %zu: type %d\n", i, (int)t);
+                }
+            }
+            fprintf(stderr, "graph: %zu nodes, max dynamic LDS %zu B\n", n, max_shm);
+        }
         he = hipGraphInstantiate(&b->gexec, g, nullptr, nullptr, 0);
         hipGraphDestroy(g);
         if (he != hipSuccess) return fail((int)he, "graph instantiate: %s", hipGetErrorString(he));

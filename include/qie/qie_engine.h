@@ -78,9 +78,24 @@ int qie_comm_create_peer(int32_t world, int32_t rank, int32_t device, qie_comm**
 int qie_comm_peer_connect(qie_comm* c, const void* handles);
 int qie_comm_create_peer_local(int32_t world, qie_comm** out);
 int qie_comm_peer_error(const qie_comm* c, int32_t* err);
+/* Peer backend exchange form, set identically on every rank between steps
+ * (a captured decode graph keeps the form it was captured with): tagged = 1 sends
+ * row-parallel exchanges of <= 131,072 elements as {generation tag, f32} words that the
+ * readers poll directly (no flags, no system fences), 0 the flagged form; push = 1 (with
+ * tagged) lets a batch-1 projection's GEMV epilogue write those words itself, so the
+ * exchange kernel only waits and reduces.  Results are bit-identical in every form.
+ * Defaults: env QIE_PEER_TAGGED / QIE_PEER_PUSH, else 1 / 1. */
+int qie_comm_peer_set_mode(qie_comm* c, int32_t tagged, int32_t push);
 /* x (bf16 [n]) = bf16(x + bf16(sum over ranks of part)), in place on x (part may be
  * overwritten): the exchange after a row-parallel projection */
 int qie_comm_allreduce_residual_bf16(qie_comm* c, const float* part, void* x, int64_t n, void* stream);
+/* Measurement: `count` row-parallel exchanges of n elements captured in one hipGraph on
+ * `stream` and replayed `reps` times (after one warm replay); *us_out = microseconds per
+ * exchange (hipEvents).  form 0: as the engine runs them (the current mode), 1: the flagged
+ * form, 2: the flagged form with n = 0 (the synchronisation alone at the same grid).  Every
+ * rank must call it with the same arguments. */
+int qie_comm_time_exchange(qie_comm* c, const float* part, void* x, int64_t n, int32_t count, int32_t reps,
+                           int32_t form, void* stream, float* us_out);
 int qie_comm_rank(const qie_comm* c, int32_t* world, int32_t* rank);
 int qie_comm_allreduce_sum_f32(qie_comm* c, float* buf, int64_t n, void* stream);
 /* in place: element-wise max over ranks of u64 words (the greedy arg-max keys) */

@@ -150,6 +150,8 @@ SIGNATURES = [
     ("qie_comm_create_peer_local", C.c_int, [_I32, C.POINTER(_P)]),
     ("qie_comm_peer_error", C.c_int, [_P, _PI32]),
     ("qie_comm_allreduce_residual_bf16", C.c_int, [_P, _P, _P, _I64, _P]),
+    ("qie_comm_peer_set_mode", C.c_int, [_P, _I32, _I32]),
+    ("qie_comm_time_exchange", C.c_int, [_P, _P, _P, _I64, _I32, _I32, _I32, _P, C.POINTER(C.c_float)]),
     ("qie_comm_rank", C.c_int, [_P, _PI32, _PI32]),
     ("qie_comm_allreduce_sum_f32", C.c_int, [_P, _P, _I64, _P]),
     ("qie_comm_allreduce_max_u64", C.c_int, [_P, _P, _I64, _P]),

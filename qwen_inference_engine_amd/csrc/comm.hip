@@ -202,6 +202,9 @@ constexpr int kPeerMaxWorld = 8;
 constexpr int kPeerBlocks = 16;
 constexpr int64_t kPeerFlagBytes = 4096;             // [2][8][16] uint32 flags, padded
 constexpr int64_t kPeerCap = 2 << 20;                // data bytes per (parity, rank) slot
+// the tagged slots (peer_tag_kernel) follow the flagged ones: [2][8] x kPeerTagCap bytes
+constexpr int64_t kPeerTagOff = kPeerFlagBytes + 2 * kPeerMaxWorld * kPeerCap;
+static_assert(kPeerMaxWorld == kPeerTagMaxWorld, "tagged slots cover every rank");
 
 struct PeerArgs {
     char* buf[kPeerMaxWorld];   // every rank's exchange buffer (this rank's own included)
@@ -308,6 +311,86 @@ __global__ __launch_bounds__(256) void peer_kernel(PeerArgs A, const void* src, 
     }
 }
 
+// Tagged row-parallel exchange (decode sizes, n <= kPeerTagCap / 8): x = bf16(x + bf16(sum of
+// the W partials)), the same rank-ordered sum as kPeerSumResid, bit for bit.  Each partial is
+// written as 8-byte words {e + 1, f32} by relaxed SYSTEM-scope atomic stores (write-through to
+// the owner's uncached buffer, single-copy atomic), and the reader polls the words themselves:
+// no system fence before a flag, no flag round trip, no fence after it.  PUSHED: the producer
+// GEMV already wrote this rank's words from its epilogue (set_gemv_push), so the kernel only
+// waits, reduces and advances the generation.  A word of generation e - 2 (the other value
+// the slot can hold: parity reuse, as above) carries tag e - 1, never e + 1.
+template <bool PUSHED>
+__global__ __launch_bounds__(256) void peer_tag_kernel(PeerArgs A, const float* part, uint16_t* x, int64_t n) {
+    __shared__ unsigned e_s, err_s;
+    const int blk = blockIdx.x, tid = threadIdx.x;
+    if (tid == 0) {
+        e_s = __hip_atomic_load(A.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        err_s = __hip_atomic_load(A.ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (err_s) return;   // poisoned communicator (see peer_kernel)
+    const unsigned e = e_s;
+    const uint64_t tag = (uint64_t)(e + 1);
+    const int64_t i0 = n * blk / gridDim.x, i1 = n * (blk + 1) / gridDim.x;
+    if constexpr (!PUSHED) {
+        for (int64_t i = i0 + tid; i < i1; i += 256) {
+            const uint64_t w = tag | ((uint64_t)__float_as_uint(part[i]) << 32);
+#pragma unroll
+            for (int q = 0; q < kPeerTagMaxWorld; q++)
+                if (q < A.world)
+                    __hip_atomic_store(peer_tag_slot(A.buf[q] + kPeerTagOff, e, A.rank) + i, w, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    char* mine = A.buf[A.rank] + kPeerTagOff;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    bool late = false;
+    for (int64_t i = i0 + tid; i < i1 && !late; i += 256) {
+        uint64_t w[kPeerTagMaxWorld];
+#pragma unroll
+        for (int q = 0; q < kPeerTagMaxWorld; q++)
+            w[q] = q < A.world ? __hip_atomic_load(peer_tag_slot(mine, e, q) + i, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_SYSTEM)
+                               : tag;
+        for (;;) {
+            bool ready = true;
+#pragma unroll
+            for (int q = 0; q < kPeerTagMaxWorld; q++) ready &= (uint32_t)w[q] == (uint32_t)tag;
+            if (ready) break;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull) {   // ~10 s at 100 MHz
+                late = true;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+            for (int q = 0; q < kPeerTagMaxWorld; q++)
+                if ((uint32_t)w[q] != (uint32_t)tag)
+                    w[q] = __hip_atomic_load(peer_tag_slot(mine, e, q) + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        if (late) break;
+        float s = __uint_as_float((uint32_t)(w[0] >> 32));
+#pragma unroll
+        for (int q = 1; q < kPeerTagMaxWorld; q++)
+            if (q < A.world) s += __uint_as_float((uint32_t)(w[q] >> 32));
+        x[i] = f2bf(bf2f(x[i]) + rbf(s));
+    }
+    if (late) {
+        __hip_atomic_store(A.ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        err_s = 1;
+    }
+    __syncthreads();
+    // timed out: x may be partly updated (the communicator is poisoned and the engine fails
+    // its next synchronising call); the generation does not advance past the late rank
+    if (err_s) return;
+    if (tid == 0) {   // the last block of this generation advances it
+        const unsigned old = __hip_atomic_fetch_add(A.ctl + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == gridDim.x - 1) {
+            __hip_atomic_store(A.ctl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(A.ctl, e + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 struct PeerComm : qie_comm {
     char* own = nullptr;          // this rank's exchange buffer (uncached)
     unsigned* ctl = nullptr;      // generation, ticket, error
@@ -343,7 +426,36 @@ struct PeerComm : qie_comm {
         for (int64_t o = 0; o < n; o += per) QIE_TRY_C(run<kPeerSumF32>(buf + o, buf + o, std::min(per, n - o), st));
         return 0;
     }
+    // tagged form for decode-sized exchanges, producer-side push (qie_comm_peer_set_mode; env
+    // defaults QIE_PEER_TAGGED / QIE_PEER_PUSH, 1 each)
+    int tagged = dev_env("QIE_PEER_TAGGED", 1);
+    int push = dev_env("QIE_PEER_PUSH", 1);
+    bool tagged_on() const { return tagged != 0; }
+    static unsigned tag_blocks() {
+        static const int v = dev_env("QIE_PEER_TAG_BLOCKS", kPeerBlocks);
+        return (unsigned)std::max(1, std::min(v, 256));
+    }
+    template <bool PUSHED>
+    int run_tagged(const float* part, uint16_t* x, int64_t n, hipStream_t st) {
+        hipLaunchKernelGGL((peer_tag_kernel<PUSHED>), dim3(tag_blocks()), dim3(256), 0, st, args(), part, x, n);
+        QIE_LAUNCH_CHECK();
+        return 0;
+    }
+    bool peer_push(PeerPush* out, int64_t n) const override {
+        if (!push || !tagged_on() || n <= 0 || n * 8 > kPeerTagCap) return false;
+        for (int r = 0; r < kPeerTagMaxWorld; r++) out->tb[r] = r < world ? peer[r] + kPeerTagOff : nullptr;
+        out->gen = ctl;
+        out->world = world;
+        out->rank = rank;
+        return true;
+    }
+    int allreduce_residual_pushed(uint16_t* x, int64_t n, hipStream_t st) override {
+        QIE_REQUIRE(n > 0 && n * 8 <= kPeerTagCap, "peer exchange: pushed exchange of %lld elements exceeds a slot",
+                    (long long)n);
+        return run_tagged<true>(nullptr, x, n, st);
+    }
     int allreduce_residual_bf16(const float* part, uint16_t* x, int64_t n, hipStream_t st) override {
+        if (n > 0 && n * 8 <= kPeerTagCap && tagged_on()) return run_tagged<false>(part, x, n, st);
         const int64_t per = kPeerCap / 4;   // a multiple of 8
         for (int64_t o = 0; o < n; o += per)
             QIE_TRY_C(run<kPeerSumResid>(part + o, x + o, std::min(per, n - o), st));
@@ -391,9 +503,11 @@ struct PeerComm : qie_comm {
 };
 
 static int peer_alloc(PeerComm* c) {
-    const size_t bytes = (size_t)kPeerFlagBytes + (size_t)2 * kPeerMaxWorld * kPeerCap;
+    const size_t tag_bytes = (size_t)2 * kPeerMaxWorld * kPeerTagCap;
+    const size_t bytes = (size_t)kPeerTagOff + tag_bytes;
     QIE_HIP(hipExtMallocWithFlags((void**)&c->own, bytes, hipDeviceMallocUncached));
     QIE_HIP(hipMemset(c->own, 0, kPeerFlagBytes));
+    QIE_HIP(hipMemset(c->own + kPeerTagOff, 0, tag_bytes));   // tag 0: no generation's
     QIE_HIP(hipMalloc((void**)&c->ctl, 64));
     QIE_HIP(hipMemset(c->ctl, 0, 64));
     return 0;
@@ -537,6 +651,61 @@ int qie_comm_peer_error(const qie_comm* comm, int32_t* err) {
 int qie_comm_allreduce_residual_bf16(qie_comm* c, const float* part, void* x, int64_t n, void* stream) {
     QIE_REQUIRE(c && part && x && n >= 0, "qie_comm_allreduce_residual_bf16: bad arguments");
     return c->allreduce_residual_bf16(part, (uint16_t*)x, n, (hipStream_t)stream);
+}
+
+int qie_comm_peer_set_mode(qie_comm* comm, int32_t tagged, int32_t push) {
+    auto* c = dynamic_cast<PeerComm*>(comm);
+    QIE_REQUIRE(c && (tagged == 0 || tagged == 1) && (push == 0 || push == 1),
+                "qie_comm_peer_set_mode: a peer communicator and 0/1 flags");
+    c->tagged = tagged;
+    c->push = push;
+    return 0;
+}
+
+int qie_comm_time_exchange(qie_comm* c, const float* part, void* x, int64_t n, int32_t count, int32_t reps,
+                           int32_t form, void* stream, float* us_out) {
+    QIE_REQUIRE(c && part && x && n >= 0 && count >= 1 && reps >= 1 && form >= 0 && form <= 2 && us_out && stream,
+                "qie_comm_time_exchange: bad arguments");
+    auto* pc = dynamic_cast<PeerComm*>(c);
+    QIE_REQUIRE(form == 0 || pc, "qie_comm_time_exchange: forms 1 and 2 are the peer backend's");
+    QIE_REQUIRE(c->graph_capturable(), "qie_comm_time_exchange: backend is not graph-capturable");
+    hipStream_t st = (hipStream_t)stream;
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int rc = 0;
+    QIE_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+    for (int i = 0; i < count && rc == 0; i++) {
+        if (form == 0) rc = c->allreduce_residual_bf16(part, (uint16_t*)x, n, st);
+        else rc = pc->run<kPeerSumResid>(part, x, form == 2 ? 0 : n, st);
+    }
+    const hipError_t ce = hipStreamEndCapture(st, &g);
+    if (rc || ce != hipSuccess) {
+        if (g) hipGraphDestroy(g);
+        return rc ? rc : fail((int)ce, "qie_comm_time_exchange: capture: %s", hipGetErrorString(ce));
+    }
+    float ms = 0.f;
+    auto run = [&]() -> int {
+        QIE_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+        QIE_HIP(hipEventCreate(&e0));
+        QIE_HIP(hipEventCreate(&e1));
+        QIE_HIP(hipGraphLaunch(ge, st));
+        QIE_HIP(hipStreamSynchronize(st));
+        QIE_HIP(hipEventRecord(e0, st));
+        for (int r = 0; r < reps; r++) QIE_HIP(hipGraphLaunch(ge, st));
+        QIE_HIP(hipEventRecord(e1, st));
+        QIE_HIP(hipEventSynchronize(e1));
+        QIE_HIP(hipEventElapsedTime(&ms, e0, e1));
+        return 0;
+    };
+    rc = run();
+    if (e0) hipEventDestroy(e0);
+    if (e1) hipEventDestroy(e1);
+    if (ge) hipGraphExecDestroy(ge);
+    hipGraphDestroy(g);
+    if (rc) return rc;
+    *us_out = ms * 1000.f / ((float)count * (float)reps);
+    return 0;
 }
 
 int qie_comm_rank(const qie_comm* c, int32_t* world, int32_t* rank) {

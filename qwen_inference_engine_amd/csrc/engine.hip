@@ -524,8 +524,21 @@ static int row_parallel(qie_batch* b, qie_linear_args& a, uint16_t* x, float* pa
     }
     a.y = part;
     a.epilogue = QIE_EPI_F32;
-    QIE_TRY(qie_linear(&a, e->stream));
     const int64_t n = rows * e->spec.hidden;
+    // peer backend, one row: the GEMV's epilogue pushes each finished output straight into
+    // every rank's tagged exchange slot (the send overlaps the projection's tail), and the
+    // exchange kernel only waits, reduces and adds (comm.hip peer_tag_kernel)
+    PeerPush pp;
+    if (rows == 1 && e->comm->peer_push(&pp, n)) {
+        set_gemv_push(&pp);
+        const int rc = qie_linear(&a, e->stream);
+        const bool taken = gemv_push_taken();
+        set_gemv_push(nullptr);
+        QIE_TRY(rc);
+        if (taken) return e->comm->allreduce_residual_pushed(x, n, e->stream);
+        return e->comm->allreduce_residual_bf16(part, x, n, e->stream);
+    }
+    QIE_TRY(qie_linear(&a, e->stream));
     return e->comm->allreduce_residual_bf16(part, x, n, e->stream);   // one kernel on the peer backend
 }
 

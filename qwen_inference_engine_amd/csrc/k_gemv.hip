@@ -59,6 +59,9 @@ struct GemvParams {
     int epre;          // M = 1: the first task's epilogue operands (bias / residual) loaded up front
     int mkdiv;         // x-first fused norm: REF quotient by the FMA-corrected reciprocal (dev A/B)
     int t16;           // skinny kernel, fp8: weights in the 16-row tiled layout (qie_fp8_tile16)
+    // F32 epilogue under tensor parallelism (peer backend, M = 1): push = {tag, value} words
+    // straight into every rank's tagged exchange slot (push.world > 0) instead of y
+    PeerPush push;
 };
 
 // REF RMSNorm quotient f / rms: the FMA-corrected product with the reciprocal (Markstein),
@@ -638,10 +641,27 @@ __global__ __launch_bounds__(LB) void gemv_kernel(GemvParams p) {
                         yr[col[i]] = f2bf(u * a);
                     }
                 } else if constexpr (EPI == QIE_EPI_F32) {
-                    float* yf = reinterpret_cast<float*>(p.y) + (int64_t)m * p.ldy;
+                    if (p.push.world > 0) {
+                        // the row-parallel exchange's send, issued as each row finishes
+                        // (comm.hip peer_tag_kernel<true> waits for and reduces it)
+                        const unsigned e = __hip_atomic_load(p.push.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
-                    for (int i = 0; i < RPW; i++)
-                        if (col[i] < p.N) yf[col[i]] = acc[m][i];
+                        for (int i = 0; i < RPW; i++) {
+                            if (col[i] >= p.N) continue;
+                            const uint64_t w = (uint64_t)(e + 1) | ((uint64_t)__float_as_uint(acc[m][i]) << 32);
+                            const int64_t at = (int64_t)m * p.ldy + col[i];
+#pragma unroll
+                            for (int q = 0; q < kPeerTagMaxWorld; q++)
+                                if (q < p.push.world)
+                                    __hip_atomic_store(peer_tag_slot(p.push.tb[q], e, p.push.rank) + at, w,
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        }
+                    } else {
+                        float* yf = reinterpret_cast<float*>(p.y) + (int64_t)m * p.ldy;
+#pragma unroll
+                        for (int i = 0; i < RPW; i++)
+                            if (col[i] < p.N) yf[col[i]] = acc[m][i];
+                    }
                 } else if constexpr (EPI == QIE_EPI_RESIDUAL) {
                     const bool pre = epre_on && task == task0;
 #pragma unroll
@@ -1345,6 +1365,13 @@ struct RopeArgs {
     int64_t rows = 0;
 };
 static thread_local RopeArgs g_rope;
+static thread_local const PeerPush* g_push = nullptr;
+static thread_local bool g_push_taken = false;
+void set_gemv_push(const PeerPush* pp) {
+    g_push = pp;
+    g_push_taken = false;
+}
+bool gemv_push_taken() { return g_push_taken; }
 
 int gemv(const qie_linear_args* a, hipStream_t st);
 
@@ -1403,6 +1430,8 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
     // 16-row tiled fp8 weights the batched-decode kernel did not take (the vocabulary
     // projection): the skinny kernel reads them, at any 1 <= M <= 16 (qie_linear checked the shape)
     p.t16 = (a->flags & QIE_LINEAR_FP8_T16) ? 1 : 0;
+    p.push = PeerPush{};
+    g_push_taken = false;
     if ((a->M >= 2 || p.t16) && a->M <= 16 && (p.t16 || env_int("QIE_SKINNY_MFMA", 1) != 0)) {
         const bool fp8w = (a->flags & QIE_LINEAR_FP8) != 0;
         const int kstep = 64;
@@ -1433,6 +1462,10 @@ int gemv(const qie_linear_args* a, hipStream_t st) {
         }
     }
     if (a->M > 8) return gemm(a, st);   // 9..16 rows the skinny kernel could not take
+    if (g_push && a->M == 1 && a->epilogue == QIE_EPI_F32) {   // every M = 1 launch below is gemv_kernel
+        p.push = *g_push;
+        g_push_taken = true;
+    }
     p.dbg = a->M == 1 ? env_int("QIE_GEMV_DBG", 0) : 0;   // dev timing experiments (1 no norm, 2 no bias)
     const int MT = a->M <= 1 ? 1 : a->M <= 2 ? 2 : a->M <= 4 ? 4 : 8;
     p.xlds = ((size_t)MT * a->K * 2 <= kGemvLdsCap) ? 1 : 0;

@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+namespace qie { struct PeerPush; }
+
 struct qie_comm {
     int world = 1, rank = 0;
     virtual ~qie_comm() = default;
@@ -32,4 +34,12 @@ struct qie_comm {
     // device word error_state reads (nullptr: the backend has none), so a caller that already
     // copies results back can read it in the same stream-ordered batch, one synchronisation
     virtual const unsigned* error_word() const { return nullptr; }
+    // Producer-side push (peer backend, tagged form): true when an n-element row-parallel
+    // exchange may take its partials from the producer's epilogue (*out filled); the
+    // exchange is then allreduce_residual_pushed — wait on the tagged words, reduce, add.
+    virtual bool peer_push(qie::PeerPush* out, int64_t n) const { (void)out; (void)n; return false; }
+    virtual int allreduce_residual_pushed(uint16_t* x, int64_t n, hipStream_t st) {
+        (void)x; (void)n; (void)st;
+        return -1;
+    }
 };

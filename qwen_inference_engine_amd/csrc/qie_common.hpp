@@ -270,6 +270,25 @@ __host__ __device__ constexpr int rope_cur_stride(int hd) { return 8 + hd; }
 // the decode attention launches of this host thread read this table (null: none)
 void set_decode_rope_cur(const float* rc);
 
+// Peer-backend tagged exchange (comm.hip): rank r's partial of generation e sits in every
+// rank's buffer at tagged slot [e & 1][r] as 8-byte words {tag = e + 1, f32 value}, so a
+// reader polls the data itself (no flag, no release fence: each word is one atomic store).
+constexpr int64_t kPeerTagCap = 1 << 20;   // bytes per tagged (parity, rank) slot
+constexpr int kPeerTagMaxWorld = 8;
+// What a producer kernel needs to push its fp32 outputs straight into the tagged slots.
+struct PeerPush {
+    char* tb[kPeerTagMaxWorld];   // every rank's tagged region base
+    const unsigned* gen;          // this rank's generation word
+    int world, rank;
+};
+__device__ __forceinline__ uint64_t* peer_tag_slot(char* tb, unsigned e, int src) {
+    return reinterpret_cast<uint64_t*>(tb + (int64_t)((e & 1) * kPeerTagMaxWorld + src) * kPeerTagCap);
+}
+// The M = 1 GEMV launches of this host thread push their F32-epilogue outputs (null: none);
+// gemv_push_taken() reports whether the last launch did.
+void set_gemv_push(const PeerPush* pp);
+bool gemv_push_taken();
+
 // Device properties cached per process (CU count for persistent grids).
 int device_cu_count();
 

@@ -118,6 +118,13 @@ class Comm:
         _lib.check(self.lib.qie_comm_peer_error(self.h, C.byref(e)), "qie_comm_peer_error")
         return e.value
 
+    def set_peer_mode(self, tagged: bool = True, push: bool = True) -> None:
+        """Peer backend exchange form (qie_comm_peer_set_mode): tagged words polled by the
+        readers, pushed by the producing GEMV (defaults), or the flagged form; the same on
+        every rank, before the decode graph that should use it is captured."""
+        _lib.check(self.lib.qie_comm_peer_set_mode(self.h, int(bool(tagged)), int(bool(push))),
+                   "qie_comm_peer_set_mode")
+
     @staticmethod
     def local(world: int) -> List["Comm"]:
         lib = _lib.load()

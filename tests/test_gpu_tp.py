@@ -72,9 +72,12 @@ def run_ranks(world, fn, timeout=300, backend="local"):
     return out
 
 
-def greedy_trace(spec, world, prompt, n_new, forced=None, backend="local"):
-    """Per-rank (ids, per-step logits); `forced` = ids to teacher-force after each step."""
+def greedy_trace(spec, world, prompt, n_new, forced=None, backend="local", peer_mode=None):
+    """Per-rank (ids, per-step logits); `forced` = ids to teacher-force after each step;
+    peer_mode = (tagged, push) for the peer backend (None: its defaults)."""
     def fn(rank, comm):
+        if peer_mode is not None:
+            comm.set_peer_mode(*peer_mode)
         eng = Q.Engine(spec, max_ctx=128, comm=comm).init_synthetic(SYN)
         b = eng.batch(1, 128)
         raw, lgs = [b.prefill(0, prompt)], []   # the engine's own choices, before forcing
@@ -122,26 +125,33 @@ def test_tp_matches_single_gpu(name):
 
 @pytest.mark.parametrize("name", ["qwen2-bias-hd64", "qwen3-qknorm-hd128", "g7-kvrep-tp2"])
 def test_peer_backend_equals_local(name):
-    """The peer backend (one kernel per exchange: push into every rank's buffer, per-block
-    generation flags, rank-ordered reduce with the residual add fused; decode steps CAPTURED
-    in each rank's hipGraph and replayed concurrently on one GPU) produces the local
-    backend's ids and logits bit for bit: both sum the ranks in order 0..world-1."""
+    """The peer backend (one kernel per exchange, rank-ordered reduce with the residual add
+    fused; decode steps CAPTURED in each rank's hipGraph and replayed concurrently on one GPU)
+    produces the local backend's ids and logits bit for bit in each of its three forms: the
+    flagged form (push into every rank's buffer, per-block generation flags), the tagged form
+    ({generation, f32} words polled directly) and the tagged form fed by the O / down GEMVs'
+    own epilogues (the default).  Every form sums the ranks in order 0..world-1."""
     spec, world = CONFIGS[name]
     prompt = list(rng(3).integers(0, spec.vocab, 13))
     loc = greedy_trace(spec, world, prompt, 10)
-    peer = greedy_trace(spec, world, prompt, 10, backend="peer")
-    for r in range(world):
-        assert peer[r][0] == loc[r][0]
-        assert np.array_equal(peer[r][1], loc[r][1])
+    for mode in ((0, 0), (1, 0), (1, 1)):
+        peer = greedy_trace(spec, world, prompt, 10, backend="peer", peer_mode=mode)
+        for r in range(world):
+            assert peer[r][0] == loc[r][0], f"peer mode {mode}, rank {r}: ids"
+            assert np.array_equal(peer[r][1], loc[r][1]), f"peer mode {mode}, rank {r}: logits"
 
 
-def test_peer_comm_collectives():
+@pytest.mark.parametrize("n,tagged", [((2 << 20) // 4 + 4104, 1), (131072, 1), (24584, 0), (1003, 1)],
+                         ids=["chunked", "tagged-full-slot", "flagged-decode", "tagged-odd"])
+def test_peer_comm_collectives(n, tagged):
     """qie_comm peer collectives on 2 in-process ranks: the fused all-reduce + residual add
-    equals the rank-ordered fp32 sum then bf16(x + bf16(sum)) bit for bit, across the
-    2-MiB slot (chunked: several generations in one call), and so does the plain fp32
-    all-reduce; each rank runs on its own stream (a shared stream would serialise them)."""
+    equals the rank-ordered fp32 sum then bf16(x + bf16(sum)) bit for bit — across the
+    2-MiB slot (flagged form, chunked: several generations in one call), at decode sizes in
+    the tagged form (up to its full 131,072-element slot) and in the flagged form — and so
+    does the plain fp32 all-reduce; each rank runs on its own stream (a shared stream would
+    serialise them)."""
     lib = Q._lib.load()
-    world, n = 2, (2 << 20) // 4 + 4104        # one full slot + a remainder (multiple of 8)
+    world = 2
     parts = [np.random.default_rng(10 + r).standard_normal(n).astype(np.float32) for r in range(world)]
     x0 = G.to_bf16(np.random.default_rng(5).standard_normal(n).astype(np.float32))
     want_sum = parts[0].copy()
@@ -149,6 +159,8 @@ def test_peer_comm_collectives():
         want_sum = (want_sum + parts[r]).astype(np.float32)
     want_x = G.to_bf16(G.bf(x0) + G.bf(G.to_bf16(want_sum)))
     comms = Q.Comm.peer_local(world)
+    for c in comms:
+        c.set_peer_mode(tagged=bool(tagged), push=True)
     bufs = [(G.dev(parts[r]), G.dev(x0), G.dev(parts[r])) for r in range(world)]
     errs = [None] * world
 

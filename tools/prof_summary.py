@@ -160,12 +160,15 @@ def main(tag="r01", src="gpurun_out/prof", desc=HEADLINE, how="tools/gpu_check.s
         lines.append(f"| `{name}` | {ROLE.get(name, '')} | {len(v)} | {statistics.mean(v):.2f} | "
                      f"{statistics.median(v):.2f} | {sum(v) / 1e3:.3f} | {100 * sum(v) / total:.2f} |")
     lines += in_graph_decode(trace)
-    lines += ["", "Raw per-kernel stats (rocprofv3 `--stats`, template arguments folded): "
-              f"`{tag}_kernel_stats.csv`."]
+    stats = os.path.join(src, "run_kernel_stats.csv")
+    if os.path.exists(stats):
+        lines += ["", "Raw per-kernel stats (rocprofv3 `--stats`, template arguments folded): "
+                  f"`{tag}_kernel_stats.csv`."]
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     with open(os.path.join(ROOT, "profiles", f"{tag}_rocprof_summary.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
-    shutil.copy(os.path.join(src, "run_kernel_stats.csv"), os.path.join(ROOT, "profiles", f"{tag}_kernel_stats.csv"))
+    if os.path.exists(stats):
+        shutil.copy(stats, os.path.join(ROOT, "profiles", f"{tag}_kernel_stats.csv"))
     print("\n".join(lines))
 
 

@@ -434,6 +434,16 @@ def config5(Q, S, W, a, comm, group, rank, local):
         eng.sync()
         dt = group.max(time.perf_counter() - t0)
         ms = dt * 1e3 / steps
+        # the step's numbers first: an exchange measurement that fails below costs only its own entry
+        step_bytes = spec.decode_weight_bytes() + spec.kv_bytes_per_position() * (P + (steps + 1) / 2.0)
+        per_gpu = step_bytes / world / (ms * 1e-3) / 1e9
+        res.update({"value": round(steps / dt, 3), "unit": "tokens/s", "ms_per_step": round(ms, 4), "steps": steps,
+                    "ctx_timed": [P + 1, P + steps], "prefill_tok_s": round(P / t_pf, 1),
+                    "prefill_ms": round(t_pf * 1e3, 3),
+                    "prefill_tflops_job": round(spec.prefill_flops(P, 1) / t_pf / 1e12, 1),
+                    "step_roofline": {"bytes_per_step": step_bytes, "achieved_GBps_per_gpu": round(per_gpu, 1),
+                                      "frac": round(per_gpu / HBM_PEAK_GBS, 4),
+                                      "roofline_tok_s": round(HBM_PEAK_GBS * 1e9 * world / step_bytes, 1)}})
         H, L = spec.hidden, spec.n_layers
         import ctypes as C
         part, x, keys = C.c_void_p(), C.c_void_p(), C.c_void_p()
@@ -462,13 +472,26 @@ def config5(Q, S, W, a, comm, group, rank, local):
             Q._lib.check(lib.qie_comm_allreduce_max_u64(comm.h, keys, 1, st), "exchange")
         eng.sync()
         key_ms = group.max(time.perf_counter() - t0) * 1e3 / 32
-        ex_us = time_exchange(0)
+        if a.comm == "peer":
+            ex_us = time_exchange(0)
+            how = ("row-parallel exchanges: 2L captured in one hipGraph on the engine stream (qie_comm_time_exchange, "
+                   "hipEvents), max over ranks; the key exchange eager")
+        else:   # RCCL: eager, as the r05 line measured it (its captured form is not rehearsed on one GPU)
+            for _ in range(2 * L):
+                Q._lib.check(lib.qie_comm_allreduce_residual_bf16(comm.h, part, x, H, st), "exchange")
+            eng.sync()
+            group.barrier()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                for _ in range(2 * L):
+                    Q._lib.check(lib.qie_comm_allreduce_residual_bf16(comm.h, part, x, H, st), "exchange")
+            eng.sync()
+            ex_us = group.max(time.perf_counter() - t0) * 1e6 / (reps * 2 * L)
+            how = "row-parallel exchanges enqueued eagerly on the engine stream, max over ranks; the key exchange eager"
         ex_ms = (2 * L * ex_us) / 1e3 + key_ms
         exch = {"ms_per_step": round(ex_ms, 4), "frac_of_step": round(ex_ms / ms, 4),
                 "per_step": f"{2 * L} all-reduce+residual of {H} fp32 + 1 max-u64 arg-max key",
-                "us_per_exchange": round(ex_us, 3), "key_exchange_ms": round(key_ms, 4),
-                "timing": "row-parallel exchanges: 2L captured in one hipGraph on the engine stream "
-                          "(qie_comm_time_exchange, hipEvents), max over ranks; the key exchange eager"}
+                "us_per_exchange": round(ex_us, 3), "key_exchange_ms": round(key_ms, 4), "timing": how}
         if a.comm == "peer":
             # verdict r05 item 6: the exchange's cost with and without the producer-side send.
             # "with": tagged words pushed by the O / down GEMV epilogues (the default mode, the
@@ -513,16 +536,7 @@ def config5(Q, S, W, a, comm, group, rank, local):
             ex_ms = ex_with
             exch["ms_per_step"] = round(ex_with, 4)
             exch["frac_of_step"] = round(ex_with / ms, 4)
-        step_bytes = spec.decode_weight_bytes() + spec.kv_bytes_per_position() * (P + (steps + 1) / 2.0)
-        per_gpu = step_bytes / world / (ms * 1e-3) / 1e9
-        res.update({"value": round(steps / dt, 3), "unit": "tokens/s", "ms_per_step": round(ms, 4), "steps": steps,
-                    "ctx_timed": [P + 1, P + steps], "prefill_tok_s": round(P / t_pf, 1),
-                    "prefill_ms": round(t_pf * 1e3, 3),
-                    "prefill_tflops_job": round(spec.prefill_flops(P, 1) / t_pf / 1e12, 1),
-                    "step_roofline": {"bytes_per_step": step_bytes, "achieved_GBps_per_gpu": round(per_gpu, 1),
-                                      "frac": round(per_gpu / HBM_PEAK_GBS, 4),
-                                      "roofline_tok_s": round(HBM_PEAK_GBS * 1e9 * world / step_bytes, 1)},
-                    "exchange": exch})
+        res["exchange"] = exch
     except Exception as ex:   # reported, never silently dropped
         res["error"] = str(ex)[:300]
     finally:

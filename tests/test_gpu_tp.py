@@ -298,6 +298,34 @@ def test_engine_tp_two_processes_peer_forced_decisions(oracle, tmp_path):
     assert rep["ok"], rep
 
 
+def test_peer_batch2_forms_equal_local():
+    """Two sequences per decode step: the row-parallel exchanges carry [2][H] (the tagged form
+    WITHOUT the producer push — the push is a batch-1 path — and the flagged form), the
+    prompts of different lengths; the peer backend's ids and logits equal the local
+    backend's bit for bit in both forms, graph-captured."""
+    spec, world = CONFIGS["qwen2-bias-hd64"]
+    prompts = [list(rng(11 + i).integers(0, spec.vocab, n)) for i, n in enumerate([17, 6])]
+
+    def trace(backend, mode=None):
+        def fn(rank, comm):
+            if mode is not None:
+                comm.set_peer_mode(*mode)
+            eng = Q.Engine(spec, max_ctx=96, comm=comm).init_synthetic(SYN)
+            b = eng.batch(2, 96)
+            first = [b.prefill(s, p) for s, p in enumerate(prompts)]
+            ids = b.decode(12).tolist()
+            if backend == "peer":
+                assert comm.peer_error() == 0, "a peer exchange timed out"
+            return first, ids, b.logits()
+        return run_ranks(world, fn, backend=backend)
+    loc = trace("local")
+    for mode in ((1, 1), (0, 0)):
+        peer = trace("peer", mode)
+        for r in range(world):
+            assert peer[r][0] == loc[r][0] and peer[r][1] == loc[r][1], f"peer mode {mode}, rank {r}: ids"
+            assert np.array_equal(peer[r][2], loc[r][2]), f"peer mode {mode}, rank {r}: logits"
+
+
 def test_tp_sampling_ranks_agree():
     spec, world = CONFIGS["qwen2-bias-hd64"]
     prompt = list(rng(5).integers(0, spec.vocab, 9))

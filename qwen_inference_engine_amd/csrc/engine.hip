@@ -1625,11 +1625,26 @@ int qie_batch_set_decode_mode(qie_batch* b, int32_t mode) {
         const char* why = "";
         QIE_REQUIRE(persist_supported(e->spec, b->B, e->sh.tp, e->fp8, b->d_table != nullptr, device_cu_count(), &why),
                     "qie_batch_set_decode_mode: the persistent decode step does not cover this batch (%s)", why);
-        if (!b->pk_mem) {
+        if (!b->pk_mem || !b->d_layers || !b->d_attp) {
+            // all three or none: a failed allocation leaves the batch in mode 0 with nothing held
             const size_t gb = (size_t)persist_granule_count(e->spec) * 8 + 64;
-            QIE_TRY(dmalloc(&b->pk_mem, gb));
-            QIE_TRY(dmalloc((void**)&b->d_layers, sizeof(qie_layer_weights) * e->layers.size()));
-            QIE_TRY(dmalloc(&b->d_attp, persist_attn_table_bytes((int)e->layers.size())));
+            hipFree(b->pk_mem);
+            hipFree(b->d_layers);
+            hipFree(b->d_attp);
+            b->pk_mem = nullptr;
+            b->d_layers = nullptr;
+            b->d_attp = nullptr;
+            void *pk = nullptr, *dl = nullptr, *ap = nullptr;
+            if (dmalloc(&pk, gb) || dmalloc(&dl, sizeof(qie_layer_weights) * e->layers.size()) ||
+                dmalloc(&ap, persist_attn_table_bytes((int)e->layers.size()))) {
+                hipFree(pk);
+                hipFree(dl);
+                hipFree(ap);
+                return fail(-2, "qie_batch_set_decode_mode: device allocation failed: %s", qie_last_error());
+            }
+            b->pk_mem = pk;
+            b->d_layers = (qie_layer_weights*)dl;
+            b->d_attp = ap;
             QIE_HIP(hipMemsetAsync(b->pk_mem, 0, gb, e->stream));
             QIE_HIP(hipMemcpyAsync(b->d_layers, e->layers.data(), sizeof(qie_layer_weights) * e->layers.size(),
                                    hipMemcpyHostToDevice, e->stream));

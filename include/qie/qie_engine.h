@@ -195,9 +195,12 @@ int qie_batch_set_position(qie_batch* b, int32_t seq, int32_t pos, int32_t token
  * QKV GEMV, attention, O GEMV, gate/up GEMV, down GEMV, hipGraph-captured); 1 = the whole
  * layer stack as ONE persistent launch (one workgroup per CU, weight streams running ahead of
  * the layer's dependency edges, tagged hand-offs between CUs; bit-identical outputs).  Mode 1
- * covers batch 1, bf16 weights, one device, head_dim 128 and a contiguous KV cache; other
- * batches return an error (QIE_EINVAL) naming what is not covered.  The next step re-captures
- * the decode graph.  qie_batch_decode_mode returns the current mode. */
+ * covers batch 1, bf16 weights, one device, head_dim 64 or 128 and a contiguous KV cache;
+ * other batches return an error (QIE_EINVAL) naming what is not covered.  The next step
+ * re-captures the decode graph.  qie_batch_decode_mode returns the current mode.  Mode 1 is
+ * SLOWER on MI355X (Qwen2-7B 317.5 vs 370.9 tok/s, Qwen2-0.5B 1,065 vs 1,566: its cross-CU
+ * hand-offs cost more than the kernel boundaries they replace); mode 0 is
+ * the default and the measured path. */
 int qie_batch_set_decode_mode(qie_batch* b, int32_t mode);
 int qie_batch_decode_mode(const qie_batch* b);
 /* Diagnostics of decode mode 1: enable != 0 makes the persistent step record s_memrealtime

@@ -510,6 +510,7 @@ static int peer_alloc(PeerComm* c) {
     QIE_HIP(hipMemset(c->own + kPeerTagOff, 0, tag_bytes));   // tag 0: no generation's
     QIE_HIP(hipMalloc((void**)&c->ctl, 64));
     QIE_HIP(hipMemset(c->ctl, 0, 64));
+    QIE_HIP(hipDeviceSynchronize());   // zeroed before any stream's exchange kernel can run
     return 0;
 }
 

@@ -309,8 +309,10 @@ static void drop_pages(qie_batch* b, int seq) {
 // uploads the host table (ordered after everything already on the stream)
 static int flush_table(qie_batch* b) {
     if (!b->d_table || !b->table_dirty) return 0;
+    // on the engine stream (non-blocking: a legacy-null-stream copy is not ordered before its
+    // kernels), complete before the host table may change again
+    QIE_HIP(hipMemcpyAsync(b->d_table, b->h_table.data(), b->h_table.size() * 4, hipMemcpyHostToDevice, b->e->stream));
     QIE_HIP(hipStreamSynchronize(b->e->stream));
-    QIE_HIP(hipMemcpy(b->d_table, b->h_table.data(), b->h_table.size() * 4, hipMemcpyHostToDevice));
     b->table_dirty = false;
     return 0;
 }
@@ -322,8 +324,9 @@ static int build_rope(qie_engine* e) {
     QIE_TRY(qie_rope_table_host(c.data(), s.data(), rows, hd, e->spec.rope_theta, e->spec.numerics));
     QIE_TRY(dmalloc((void**)&e->rope_cos, c.size() * 4));
     QIE_TRY(dmalloc((void**)&e->rope_sin, s.size() * 4));
-    QIE_HIP(hipMemcpy(e->rope_cos, c.data(), c.size() * 4, hipMemcpyHostToDevice));
-    QIE_HIP(hipMemcpy(e->rope_sin, s.data(), s.size() * 4, hipMemcpyHostToDevice));
+    QIE_HIP(hipMemcpyAsync(e->rope_cos, c.data(), c.size() * 4, hipMemcpyHostToDevice, e->stream));
+    QIE_HIP(hipMemcpyAsync(e->rope_sin, s.data(), s.size() * 4, hipMemcpyHostToDevice, e->stream));
+    QIE_HIP(hipStreamSynchronize(e->stream));   // the host tables go out of scope
     e->rope_rows = rows;
     return 0;
 }
@@ -1044,8 +1047,11 @@ static int load_weights_sharded(qie_engine* e, const char* weights_bin, const ch
             }
         }
         if (!rc) {
-            hipError_t he = hipMemcpy((char*)e->arena + local->t[i].off0, host.data(), (size_t)(x.rows * x.cols * 2),
-                                      hipMemcpyHostToDevice);
+            // stream-ordered before the engine's kernels (its stream is non-blocking: a copy on the
+            // legacy null stream is not), complete before the staging vector is refilled
+            hipError_t he = hipMemcpyAsync((char*)e->arena + local->t[i].off0, host.data(),
+                                           (size_t)(x.rows * x.cols * 2), hipMemcpyHostToDevice, e->stream);
+            if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
             if (he != hipSuccess) rc = fail((int)he, "H2D: %s", hipGetErrorString(he));
         }
     }

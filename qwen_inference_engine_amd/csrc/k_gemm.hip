@@ -1025,7 +1025,7 @@ static int g8_workspace(hipStream_t st, int slabs, int tiles, G8Split* out) {
         w = G8Ws{};
         QIE_HIP(hipMalloc((void**)&w.slab, sb));
         QIE_HIP(hipMalloc((void**)&w.cnt, cn * 4));
-        QIE_HIP(hipMemset(w.cnt, 0, cn * 4));
+        QIE_HIP(hipMemsetAsync(w.cnt, 0, cn * 4, st));   // ordered before this stream's GEMMs
         w.slab_bytes = sb;
         w.cnt_n = cn;
     }

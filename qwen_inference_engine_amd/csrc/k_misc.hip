@@ -582,8 +582,12 @@ int qie_free(void* ptr) {
     return 0;
 }
 
+// The stream-less helpers are complete on return: the engine's and the callers' streams are
+// non-blocking, so a copy or memset left on the legacy null stream would not be ordered
+// before their kernels.
 int qie_memcpy_h2d(void* dst, const void* src, int64_t bytes) {
     QIE_HIP(hipMemcpy(dst, src, (size_t)bytes, hipMemcpyHostToDevice));
+    QIE_HIP(hipStreamSynchronize(nullptr));
     return 0;
 }
 
@@ -595,6 +599,7 @@ int qie_memcpy_d2h(void* dst, const void* src, int64_t bytes) {
 
 int qie_memset(void* ptr, int value, int64_t bytes) {
     QIE_HIP(hipMemset(ptr, value, (size_t)bytes));
+    QIE_HIP(hipStreamSynchronize(nullptr));
     return 0;
 }
 

@@ -311,6 +311,25 @@ __global__ __launch_bounds__(256) void peer_kernel(PeerArgs A, const void* src, 
     }
 }
 
+// Exchange buffers are uncached device memory.  A freed one goes to a process-wide pool and is
+// handed to the next communicator instead of back to the allocator: physical pages that were
+// mapped uncached are never recycled into ordinary (cached) allocations of the process — a
+// weight arena placed on them after the peer tests read back 40 whole 128-B lines of a
+// freshly written tensor as stale zeros (test_tp_weights_bin_equals_synthetic, r06).
+static std::mutex g_peer_pool_mu;
+static std::vector<char*> g_peer_pool;
+static char* peer_pool_get() {
+    std::lock_guard<std::mutex> lk(g_peer_pool_mu);
+    if (g_peer_pool.empty()) return nullptr;
+    char* p = g_peer_pool.back();
+    g_peer_pool.pop_back();
+    return p;
+}
+static void peer_pool_put(char* p) {
+    std::lock_guard<std::mutex> lk(g_peer_pool_mu);
+    g_peer_pool.push_back(p);
+}
+
 // Tagged row-parallel exchange (decode sizes, n <= kPeerTagCap / 8): x = bf16(x + bf16(sum of
 // the W partials)), the same rank-ordered sum as kPeerSumResid, bit for bit.  Each partial is
 // written as 8-byte words {e + 1, f32} by relaxed SYSTEM-scope atomic stores (write-through to
@@ -401,7 +420,7 @@ struct PeerComm : qie_comm {
     ~PeerComm() override {
         for (int r = 0; r < kPeerMaxWorld; r++)
             if (opened[r] && peer[r]) hipIpcCloseMemHandle(peer[r]);
-        if (own_alloc && own) hipFree(own);
+        if (own_alloc && own) peer_pool_put(own);
         if (ctl) hipFree(ctl);
         if (tmp) hipFree(tmp);
     }
@@ -505,7 +524,8 @@ struct PeerComm : qie_comm {
 static int peer_alloc(PeerComm* c) {
     const size_t tag_bytes = (size_t)2 * kPeerMaxWorld * kPeerTagCap;
     const size_t bytes = (size_t)kPeerTagOff + tag_bytes;
-    QIE_HIP(hipExtMallocWithFlags((void**)&c->own, bytes, hipDeviceMallocUncached));
+    c->own = peer_pool_get();
+    if (!c->own) QIE_HIP(hipExtMallocWithFlags((void**)&c->own, bytes, hipDeviceMallocUncached));
     QIE_HIP(hipMemset(c->own, 0, kPeerFlagBytes));
     QIE_HIP(hipMemset(c->own + kPeerTagOff, 0, tag_bytes));   // tag 0: no generation's
     QIE_HIP(hipMalloc((void**)&c->ctl, 64));

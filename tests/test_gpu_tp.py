@@ -347,20 +347,45 @@ def test_tp_weights_bin_equals_synthetic(tmp_path):
     hw.write_weights_bin(binp, meta)
     prompt = [5, 9, 2, 7, 1, 3]
 
+    import ctypes as C
+    lib = Q._lib.load()
+    vl = spec.vocab // world
+    head = hw.tensors["lm_head.weight"]
+
+    def head_slice(e, rank):
+        """this rank's lm_head rows as the engine holds them, against the host generator's"""
+        w = Q._lib.ModelWeightsC()
+        G.check(lib.qie_engine_weights(e.h, C.byref(w), None))
+        got = np.empty((vl, spec.hidden), np.uint16)
+        G.check(lib.qie_memcpy_d2h(got.ctypes.data, w.lm_head, got.nbytes))
+        want = head[rank * vl:(rank + 1) * vl]
+        bad = np.flatnonzero(got != want)
+        if len(bad) == 0:
+            return 0
+        return (len(bad), int(bad[0]), int(bad[-1]), [(int(got.flat[i]), int(want.flat[i])) for i in bad[:4]],
+                int(w.lm_head) % 4096)
+
     def fn(rank, comm):
         out = []
-        for src in ("syn", "bin"):
+        for src in ("syn", "bin", "syn"):   # the repeat: run-to-run determinism of the same engine
             e = Q.Engine(spec, max_ctx=64, comm=comm)
             e = e.init_synthetic(SYN) if src == "syn" else e.load_weights_bin(binp, meta)
+            bad_w = head_slice(e, rank)
             b = e.batch(1, 64)
-            ids = [b.prefill(0, prompt)] + list(b.decode(6)[:, 0])
-            out.append((ids, b.logits()))
+            ids, lgs = [b.prefill(0, prompt)], [b.logits()]
+            for _ in range(6):
+                ids.append(int(b.decode_step()[0]))
+                lgs.append(b.logits())
+            out.append((ids, np.stack(lgs), bad_w))
         return out
     res = run_ranks(world, fn)
     for r in range(world):
-        (i1, l1), (i2, l2) = res[r]
-        assert i1 == i2
-        assert np.array_equal(l1, l2)
+        for k, what in ((1, "weights.bin"), (2, "synthetic, second engine")):
+            (i1, l1, w1), (i2, l2, w2) = res[r][0], res[r][k]
+            bad = [(s, int((l1[s] != l2[s]).sum())) for s in range(len(l1)) if not np.array_equal(l1[s], l2[s])]
+            assert i1 == i2 and not bad, (f"rank {r}, {what} vs synthetic: ids {'equal' if i1 == i2 else 'differ'}, "
+                                          f"(step, differing logits) {bad[:4]}; lm_head elements off the host "
+                                          f"generator: synthetic {w1}, {what} {w2}")
 
 
 def test_rccl_single_rank_communicator():

@@ -238,14 +238,12 @@ struct PrefillAttnParams {
 // makespan of the balanced split on 256 CUs).  Scores go to the log2 domain once
 // (dot * log2(e) / sqrt(hd)) and are exponentiated with v_exp_f32: the reference build
 // compiles with -use_fast_math, i.e. __expf / __fdividef.
-template <int HD, bool PG>
-__global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnParams a) {
+template <int HD, bool PG, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_prefill_mfma2_kernel(PrefillAttnParams a) {
     constexpr int KT = 64;
     constexpr int CPR = HD / 8;
     constexpr int KSTEPS = HD / 32;
     constexpr int DT = HD / 16;
-    constexpr int CHUNKS = KT * CPR;
-    constexpr int LPT = CHUNKS / 256;
     constexpr int QG = 2;                  // 16-row query groups per wave
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint16_t* Ks = reinterpret_cast<uint16_t*>(smem);
@@ -267,12 +265,12 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
     const uint16_t* vb = a.vc + head_off;
     // this wave's groups: pair j = (j, ngr-1-j); the workgroup's latest row is wave 0's
     // second group (positions are non-decreasing within a sequence)
-    const int j = blockIdx.x * 4 + wave;
+    const int j = blockIdx.x * NW + wave;
     const int grp[QG] = {j, ngr - 1 - j};
     bool gact[QG];
     gact[0] = j < npair;
     gact[1] = j < npair && grp[1] != j;
-    const int kmax = a.pos[row0 + min(16 * (ngr - 1 - (int)blockIdx.x * 4) + 15, R - 1)];
+    const int kmax = a.pos[row0 + min(16 * (ngr - 1 - (int)blockIdx.x * NW) + 15, R - 1)];
     const int nkt = kmax / KT + 1;
 
     int qpos[QG], gpos[QG], gmin[QG];
@@ -297,7 +295,7 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_mfma2_kernel(PrefillAttnP
     // ds_write pass.  A 64-key tile never straddles a page (page_tokens is a multiple of
     // 128); rows past kmax re-read row kmax (same page) and are masked by position.
     constexpr int RPI = 512 / HD;                 // key rows per 1 KiB wave-instruction
-    constexpr int IPW = KT / RPI / 4;             // wave-instructions per wave per operand
+    constexpr int IPW = KT / RPI / NW;            // wave-instructions per wave per operand
     // Buffer loads to LDS on a per-tile resource (round 5): the lane byte offsets inside a
     // tile are constants of the launch and the tile base is scalar, so a tile's DMAs cost no
     // VALU (the flat form recomputed 64-bit addresses and the row clamp per tile: ~40 VALU).
@@ -640,12 +638,15 @@ int qie_attention(const void* q, int64_t M, const int32_t* pos, int32_t rows_per
         pa.full_tiles = dev_env("QIE_ATTN_PF_FULL", 1);
         const size_t shm = (size_t)2 * 2 * 64 * cache->head_dim * 2;
         const bool pg = pa.km.table != nullptr;
-        // balanced causal split: ceil(ceil(R / 16) / 2) group pairs, 4 per workgroup
+        // balanced causal split: ceil(ceil(R / 16) / 2) group pairs, NW per workgroup
         const int npair = ((rows_per_seq + 15) / 16 + 1) / 2;
-        dim3 g2((unsigned)((npair + 3) / 4), (unsigned)n_heads, (unsigned)(M / rows_per_seq));
-        auto k2 = cache->head_dim == 128 ? (pg ? attn_prefill_mfma2_kernel<128, true> : attn_prefill_mfma2_kernel<128, false>)
-                                         : (pg ? attn_prefill_mfma2_kernel<64, true> : attn_prefill_mfma2_kernel<64, false>);
-        hipLaunchKernelGGL(k2, g2, dim3(256), shm, (hipStream_t)stream, pa);
+        const int nw = dev_env("QIE_ATTN_PF_NW", 4) == 8 ? 8 : 4;
+        dim3 g2((unsigned)((npair + nw - 1) / nw), (unsigned)n_heads, (unsigned)(M / rows_per_seq));
+        auto k2 = nw == 8 ? (cache->head_dim == 128 ? (pg ? attn_prefill_mfma2_kernel<128, true, 8> : attn_prefill_mfma2_kernel<128, false, 8>)
+                                                    : (pg ? attn_prefill_mfma2_kernel<64, true, 8> : attn_prefill_mfma2_kernel<64, false, 8>))
+                          : (cache->head_dim == 128 ? (pg ? attn_prefill_mfma2_kernel<128, true, 4> : attn_prefill_mfma2_kernel<128, false, 4>)
+                                                    : (pg ? attn_prefill_mfma2_kernel<64, true, 4> : attn_prefill_mfma2_kernel<64, false, 4>));
+        hipLaunchKernelGGL(k2, g2, dim3(64 * nw), shm, (hipStream_t)stream, pa);
         QIE_LAUNCH_CHECK();
         return 0;
     }

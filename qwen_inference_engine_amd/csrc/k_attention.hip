@@ -640,7 +640,10 @@ int qie_attention(const void* q, int64_t M, const int32_t* pos, int32_t rows_per
         const bool pg = pa.km.table != nullptr;
         // balanced causal split: ceil(ceil(R / 16) / 2) group pairs, NW per workgroup
         const int npair = ((rows_per_seq + 15) / 16 + 1) / 2;
-        const int nw = dev_env("QIE_ATTN_PF_NW", 4) == 8 ? 8 : 4;
+        // 8 waves (16 row groups) per workgroup: each staged K/V tile feeds twice the rows, half
+        // the LDS-DMA traffic of 4-wave workgroups (P = 2,048, 7B: 74.1-74.7 -> 69.9-70.7 us,
+        // bit-identical; tools/attn_nw_check.py).  Dev A/B: QIE_ATTN_PF_NW = 4.
+        const int nw = dev_env("QIE_ATTN_PF_NW", 8) == 4 ? 4 : 8;
         dim3 g2((unsigned)((npair + nw - 1) / nw), (unsigned)n_heads, (unsigned)(M / rows_per_seq));
         auto k2 = nw == 8 ? (cache->head_dim == 128 ? (pg ? attn_prefill_mfma2_kernel<128, true, 8> : attn_prefill_mfma2_kernel<128, false, 8>)
                                                     : (pg ? attn_prefill_mfma2_kernel<64, true, 8> : attn_prefill_mfma2_kernel<64, false, 8>))

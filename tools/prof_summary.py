@@ -24,7 +24,7 @@ ROLE = {
     "attn_decode_mfma2_kernel<128, false, 4, false>": "decode attention (fused RoPE/KV append, split-K, in-launch combine)",
     "rmsnorm_kernel": "prefill RMSNorm",
     "qkv_post_kernel<false>": "prefill RoPE + KV-cache write",
-    "attn_prefill_mfma2_kernel<128, false>": "prefill flash attention (MFMA, 32 rows/wave)",
+    "attn_prefill_mfma2_kernel<128, false, 8>": "prefill flash attention (MFMA, 32 rows/wave, 8-wave workgroups)",
     "gemm_big_kernel<2, 256>": "prefill gate/up GEMM (256x256 LDS-DMA, SwiGLU)",
     "gemm_big_kernel<1, 128>": "prefill O / down GEMM (256x128 LDS-DMA, +residual)",
     "gemm_big_kernel<0, 256>": "prefill QKV GEMM (256x256 LDS-DMA, one round, +bias)",
@@ -72,7 +72,7 @@ ROLE = {
     "dec8_kernel<1, 4, 8, true, true, false>": "fp8 decode down (+residual), split-K 10 x (8 waves x 4 units), tiled",
     "dec8_kernel<0, 4, 8, true, true, false>": "bench live timing of down (store epilogue)",
     "attn_decode_mfma2_kernel<128, true, 4, false, 128>": "decode attention, paged KV (fused RoPE/KV append, split-K, in-launch combine)",
-    "attn_prefill_mfma2_kernel<128, true>": "prefill flash attention, paged KV (MFMA, 32 rows/wave)",
+    "attn_prefill_mfma2_kernel<128, true, 8>": "prefill flash attention, paged KV (MFMA, 32 rows/wave, 8-wave workgroups)",
 }
 
 

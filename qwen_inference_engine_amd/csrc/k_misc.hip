@@ -186,7 +186,12 @@ struct QkvPostArgs {
     uint16_t* q_out;
 };
 
-template <bool PG>
+// Round 6: the wave's heads are taken in batches of kQkvBatch whose source pairs are all
+// loaded before the first store (the row-at-a-time form waited one memory round trip per head,
+// nine in a row per wave at Qwen2-7B widths); the arithmetic per element is unchanged.
+constexpr int kQkvBatch = 10;
+
+template <bool PG, bool HF>
 __global__ __launch_bounds__(256) void qkv_post_kernel(QkvPostArgs a) {
 #pragma clang fp contract(off)
     const int64_t m = blockIdx.x;
@@ -197,62 +202,74 @@ __global__ __launch_bounds__(256) void qkv_post_kernel(QkvPostArgs a) {
     const int p = a.pos[m];
     const int64_t seq = m / a.rows_per_seq;
     const uint16_t* row = a.qkv + m * (int64_t)(QD + 2 * KD);
-    const bool hf = a.numerics == QIE_NUMERICS_HF;
     const bool active = lane < half;
-    const int i0 = hf ? lane : 2 * lane;
-    const int i1 = hf ? lane + half : 2 * lane + 1;
+    const int i0 = HF ? lane : 2 * lane;
+    const int i1 = HF ? lane + half : 2 * lane + 1;
     const float c = active ? a.cs[(int64_t)p * half + lane] : 0.f;
     const float s = active ? a.sn[(int64_t)p * half + lane] : 0.f;
-    for (int h = wave; h < ptot; h += 4) {
-        const uint16_t* src;
-        uint16_t* dst;
-        const uint16_t* nw = nullptr;
-        bool rope = true;
-        if (h < a.nq) {
-            src = row + h * hd;
-            dst = a.q_out + m * (int64_t)QD + h * hd;
-            nw = a.q_norm;
-        } else if (h < a.nq + a.nkv) {
-            const int g = h - a.nq;
-            src = row + QD + g * hd;
-            dst = a.kc + kv_run_off(a.km, (int64_t)a.layer * a.nkv + g, hd) + kv_tok<PG>(a.km, seq, p, hd);
-            nw = a.k_norm;
-        } else {
-            const int g = h - a.nq - a.nkv;
-            src = row + QD + KD + g * hd;
-            dst = a.vc + kv_run_off(a.km, (int64_t)a.layer * a.nkv + g, hd) + kv_tok<PG>(a.km, seq, p, hd);
-            rope = false;
-        }
-        float x0 = active ? bf2f(src[i0]) : 0.f;
-        float x1 = active ? bf2f(src[i1]) : 0.f;
-        if (rope && nw) {
-            float ss = wave_sum(x0 * x0 + x1 * x1);
-            float rms = sqrtf((ss / (float)hd) + a.eps);
-            if (hf) {
-                float inv = 1.0f / rms;
-                x0 = rbf(bf2f(nw[i0]) * rbf(x0 * inv));
-                x1 = rbf(bf2f(nw[i1]) * rbf(x1 * inv));
-            } else {
-                x0 = rbf((x0 / rms) * bf2f(nw[i0]));
-                x1 = rbf((x1 / rms) * bf2f(nw[i1]));
+    // q, k and v heads are contiguous in the projection row: head h starts at h * hd
+    for (int h0 = wave; h0 < ptot; h0 += 4 * kQkvBatch) {
+        uint32_t raw[kQkvBatch];   // the lane's pair of head h0 + 4 b: element i0 low, i1 high
+#pragma unroll
+        for (int b = 0; b < kQkvBatch; b++) {
+            const int h = h0 + 4 * b;
+            raw[b] = 0;
+            if (h < ptot && active) {
+                const uint16_t* src = row + h * hd;
+                raw[b] = HF ? (uint32_t)src[i0] | ((uint32_t)src[i1] << 16)
+                            : reinterpret_cast<const uint32_t*>(src)[lane];
             }
         }
-        float y0 = x0, y1 = x1;
-        if (rope) {
-            if (hf) {
-                y0 = rbf(rbf(x0 * c) + rbf(-x1 * s));
-                y1 = rbf(rbf(x1 * c) + rbf(x0 * s));
+#pragma unroll
+        for (int b = 0; b < kQkvBatch; b++) {
+            const int h = h0 + 4 * b;
+            if (h >= ptot) break;   // wave-uniform
+            uint16_t* dst;
+            const uint16_t* nw = nullptr;
+            bool rope = true;
+            if (h < a.nq) {
+                dst = a.q_out + m * (int64_t)QD + h * hd;
+                nw = a.q_norm;
+            } else if (h < a.nq + a.nkv) {
+                const int g = h - a.nq;
+                dst = a.kc + kv_run_off(a.km, (int64_t)a.layer * a.nkv + g, hd) + kv_tok<PG>(a.km, seq, p, hd);
+                nw = a.k_norm;
             } else {
-                y0 = x0 * c - x1 * s;
-                y1 = x1 * c + x0 * s;
+                const int g = h - a.nq - a.nkv;
+                dst = a.vc + kv_run_off(a.km, (int64_t)a.layer * a.nkv + g, hd) + kv_tok<PG>(a.km, seq, p, hd);
+                rope = false;
             }
-        }
-        if (active) {
-            if (hf) {
-                dst[i0] = f2bf(y0);
-                dst[i1] = f2bf(y1);
-            } else {
-                reinterpret_cast<uint32_t*>(dst)[lane] = pack2(y0, y1);
+            float x0 = active ? bf2f((uint16_t)(raw[b] & 0xffffu)) : 0.f;
+            float x1 = active ? bf2f((uint16_t)(raw[b] >> 16)) : 0.f;
+            if (rope && nw) {
+                float ss = wave_sum(x0 * x0 + x1 * x1);
+                float rms = sqrtf((ss / (float)hd) + a.eps);
+                if (HF) {
+                    float inv = 1.0f / rms;
+                    x0 = rbf(bf2f(nw[i0]) * rbf(x0 * inv));
+                    x1 = rbf(bf2f(nw[i1]) * rbf(x1 * inv));
+                } else {
+                    x0 = rbf((x0 / rms) * bf2f(nw[i0]));
+                    x1 = rbf((x1 / rms) * bf2f(nw[i1]));
+                }
+            }
+            float y0 = x0, y1 = x1;
+            if (rope) {
+                if (HF) {
+                    y0 = rbf(rbf(x0 * c) + rbf(-x1 * s));
+                    y1 = rbf(rbf(x1 * c) + rbf(x0 * s));
+                } else {
+                    y0 = x0 * c - x1 * s;
+                    y1 = x1 * c + x0 * s;
+                }
+            }
+            if (active) {
+                if (HF) {
+                    dst[i0] = f2bf(y0);
+                    dst[i1] = f2bf(y1);
+                } else {
+                    reinterpret_cast<uint32_t*>(dst)[lane] = pack2(y0, y1);
+                }
             }
         }
     }
@@ -708,8 +725,10 @@ int qie_qkv_post(const void* qkv, int64_t M, const int32_t* pos, int32_t rows_pe
     a.eps = eps;
     a.numerics = numerics;
     a.q_out = (uint16_t*)q_out;
-    hipLaunchKernelGGL((a.km.table ? qkv_post_kernel<true> : qkv_post_kernel<false>), dim3((unsigned)M), dim3(256), 0,
-                       (hipStream_t)stream, a);
+    const bool hf = numerics == QIE_NUMERICS_HF;
+    auto fn = a.km.table ? (hf ? qkv_post_kernel<true, true> : qkv_post_kernel<true, false>)
+                         : (hf ? qkv_post_kernel<false, true> : qkv_post_kernel<false, false>);
+    hipLaunchKernelGGL(fn, dim3((unsigned)M), dim3(256), 0, (hipStream_t)stream, a);
     QIE_LAUNCH_CHECK();
     return 0;
 }

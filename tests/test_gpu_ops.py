@@ -223,8 +223,9 @@ def _cache(kc, vc, L, nkv, hd, ctx, seq_stride):
 @pytest.mark.parametrize("qkn", [False, True])
 @pytest.mark.parametrize("num", ["ref", "hf"])
 @pytest.mark.parametrize("mode", ["prefill", "decode"])
-def test_qkv_post(oracle, qlib, hd, qkn, num, mode):
-    nq, nkv, L, ctx, layer = 6, 2, 3, 40, 1
+@pytest.mark.parametrize("heads", [(6, 2), (48, 4)])   # 56 heads: two load batches per wave
+def test_qkv_post(oracle, qlib, hd, qkn, num, mode, heads):
+    (nq, nkv), L, ctx, layer = heads, 3, 40, 1
     QD, KD = nq * hd, nkv * hd
     if mode == "prefill":
         M, rps = 9, 9
